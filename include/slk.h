@@ -1,0 +1,139 @@
+/*
+ * slk.h — C-ABI of the MI355X-native split-CNN step (libslk.so, gfx950).
+ *
+ * The reference (eliasandronicou/split-learning-k8s) has no native code and no FFI: every op of its
+ * hot path is a torch CPU call made by src/model_def.py, src/client_part.py and src/server_part.py.
+ * Each entry point below replaces one (or a fused group) of those calls; the reference call site is
+ * cited next to each declaration. The Python host layer (split-learning-k8s_amd/splitcnn/_lib.py)
+ * binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions (all entry points):
+ *   - Plain pointers to DEVICE memory, sizes as int, the HIP stream as `void*` (hipStream_t).
+ *   - Every buffer, including workspaces, is allocated by the caller. The library never allocates,
+ *     frees or synchronises, so every call is safe inside HIP-graph capture.
+ *   - Return value: 0 on success, otherwise a hipError_t code (1 = hipErrorInvalidValue for bad
+ *     arguments). slk_error_string() turns it into text. Nothing throws across the ABI.
+ *   - Stateless and reentrant; ordering comes only from the caller's stream.
+ *   - Layouts are the reference's logical NCHW layouts (torch contiguous):
+ *       x      f32 [B,1,28,28]      client input           (client_part.py:110,114)
+ *       act    f32 [B,32,26,26]     cut-layer activations  (client_part.py:114,118)
+ *       pooled f32 [B,64,12,12]     = flatten [B,9216], index c*144+h*12+w (model_def.py:20-21,26-27)
+ *       code   u8  [B,64,12,12]     max-pool argmax in its 2x2 window, row-major 0..3, first max wins;
+ *                                   4 = pooled value <= 0 (ReLU blocks the gradient)
+ *       logits f32 [B,10]; labels i64 [B]
+ *       W1 f32[32,1,3,3] b1[32]  W2 f32[64,32,3,3] b2[64]  W3 f32[10,9216] b3[10]  (model_def.py:8,18,22)
+ *   - Flat parameter blocks (what the fused SGD updates in one launch):
+ *       client: [W1 (288) | b1 (32)]                     = SLK_CLIENT_NPARAM floats
+ *       server: [W2 (18432) | b2 (64) | W3 (92160) | b3 (10)] = SLK_SERVER_NPARAM floats
+ *   - Arithmetic is fp32 throughout (the reference's dtype); weight-gradient reductions use
+ *     per-workgroup slabs summed in a fixed order, so every result is run-to-run bit-stable.
+ */
+#ifndef SLK_H
+#define SLK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLK_ABI_VERSION 1
+
+#define SLK_CLIENT_NPARAM 320
+#define SLK_SERVER_NPARAM 110666
+#define SLK_OFF_W2 0
+#define SLK_OFF_B2 18432
+#define SLK_OFF_W3 18496
+#define SLK_OFF_B3 110656
+
+int slk_abi_version(void);
+const char* slk_error_string(int err);
+
+/* ---------------------------------------------------------------- client stage (ModelPartA) */
+
+/* act = relu(conv2d(x, W1, b1)), stride 1, no padding.
+ * Replaces ModelPartA.forward (src/model_def.py:11-12) as called at src/client_part.py:114. */
+int slk_conv1_fwd(const float* x, const float* W1, const float* b1, float* act, int B, void* stream);
+
+/* Client backward: relu-bwd mask (act > 0) applied to the cut gradient, then conv1 weight/bias
+ * gradient. No input gradient (the data needs none). Writes per-group partial slabs
+ * [slk_conv1_wgrad_nslab(B)][320] into `slabs`; reduce them with slk_sgd_from_slabs or
+ * slk_reduce_slabs. Replaces `activations.backward(server_grads)` (src/client_part.py:132). */
+int slk_conv1_wgrad(const float* x, const float* act, const float* cut_grad, float* slabs, int B,
+                    void* stream);
+int slk_conv1_wgrad_nslab(int B);
+
+/* ---------------------------------------------------------------- server stage (ModelPartB) */
+
+/* pooled = maxpool2(relu(conv2d(act, W2, b2))) and its argmax code, fused (MFMA f32 implicit GEMM).
+ * Replaces ModelPartB.forward lines src/model_def.py:25-27 as called at src/server_part.py:48. */
+int slk_conv2_fwd_pool(const float* act, const float* W2, const float* b2, float* pooled,
+                       uint8_t* code, int B, void* stream);
+
+/* logits = pooled @ W3^T + b3.  Replaces model_def.py:28 (fc1). */
+int slk_fc_fwd(const float* pooled, const float* W3, const float* b3, float* logits, int B,
+               void* stream);
+
+/* Cross-entropy (mean reduction, no label smoothing) forward+backward from logits:
+ * loss_i[b] = logsumexp(z_b) - z_b[y_b];  dlogits = (softmax(z) - onehot(y)) * grad_scale.
+ * grad_scale = 1/B reproduces nn.CrossEntropyLoss()'s mean (src/server_part.py:16,49,51).
+ * An out-of-range label writes NaN loss/dlogits for that row and sets *err_flag (may be NULL). */
+int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, float* loss_i, float* dlogits,
+                     float grad_scale, int* err_flag, int B, void* stream);
+
+/* dpooled = dlogits @ W3 (fc1 input gradient). Replaces the fc1 part of loss.backward()
+ * (src/server_part.py:51). */
+int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpooled, int B, void* stream);
+
+/* Fused server head: fc1 forward, cross-entropy forward+backward and fc1 input gradient in one
+ * launch (pooled is read from HBM once for the logits and once, L2-hot, for nothing else).
+ * Outputs logits, loss_i, dlogits, dpooled. Replaces server_part.py:48(fc1 part),49,51(fc1 part). */
+int slk_fc_xent(const float* pooled, const float* W3, const float* b3, const int64_t* labels,
+                float* logits, float* loss_i, float* dlogits, float* dpooled, float grad_scale,
+                int* err_flag, int B, void* stream);
+
+/* fc1 weight/bias gradient partials: slabs [slk_fc_wgrad_nslab(B)][92170] laid out as
+ * [dW3 (10*9216) | db3 (10)], i.e. the tail of the server flat block. */
+int slk_fc_wgrad(const float* dlogits, const float* pooled, float* slabs, int B, void* stream);
+int slk_fc_wgrad_nslab(int B);
+
+/* Cut-layer gradient: cut_grad = conv2 input gradient of maxpool/relu-masked dpooled
+ * (uses `code` from slk_conv2_fwd_pool). This is `client_activations.grad` of
+ * src/server_part.py:45,51,57. MFMA f32 implicit GEMM. */
+int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const float* W2, float* cut_grad,
+                    int B, void* stream);
+
+/* conv2 weight/bias gradient partials: slabs [slk_conv2_wgrad_nslab(B)][18496] laid out as
+ * [dW2 (64*288) | db2 (64)], i.e. the head of the server flat block. MFMA f32. */
+int slk_conv2_wgrad(const float* act, const float* dpooled, const uint8_t* code, float* slabs,
+                    int B, void* stream);
+int slk_conv2_wgrad_nslab(int B);
+
+/* ---------------------------------------------------------------- reductions / optimizer */
+
+/* out[i] = sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed order). */
+int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, void* stream);
+
+/* Fused deterministic slab reduction + SGD (lr, no momentum, no weight decay):
+ * g = sum_s slabs[s*n+i]; grad[i] = g (if grad != NULL); param[i] -= lr * g.
+ * Replaces optimizer.step() of optim.SGD(lr=0.01) (client_part.py:17,133; server_part.py:15,52). */
+int slk_sgd_from_slabs(float* param, float* grad, const float* slabs, int nslab, int n, float lr,
+                       void* stream);
+
+/* param[i] -= lr * grad[i]  (flat multi-tensor SGD; torch.optim.SGD semantics, momentum 0). */
+int slk_sgd(float* param, const float* grad, int n, float lr, void* stream);
+
+/* out[slot] = mean(loss_i[0..B))  (fixed-order reduction; the device-side loss log entry that
+ * replaces mlflow.log_metric("loss", loss.item(), step) at src/server_part.py:55). */
+int slk_loss_mean(const float* loss_i, int B, float* out, int slot, void* stream);
+
+/* Loss log ring: ring[*counter % capacity] = mean(loss_i); ++*counter (one device thread).
+ * The slot comes from device memory, so a captured HIP graph logs every replay into a new slot;
+ * the host flushes the ring every N steps instead of a per-step .item() sync. */
+int slk_loss_log(const float* loss_i, int B, float* ring, int capacity, int* counter, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SLK_H */

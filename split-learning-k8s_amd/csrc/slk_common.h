@@ -1,0 +1,56 @@
+// slk_common.h — shared helpers for the gfx950 split-CNN kernels (internal; not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slk.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Fixed model geometry (src/model_def.py:8,18,20,22).
+namespace slk {
+constexpr int IN_HW = 28;            // x: 1 x 28 x 28
+constexpr int C1 = 32;               // conv1 out channels
+constexpr int A_HW = 26;             // cut activation spatial size
+constexpr int A_PIX = A_HW * A_HW;   // 676
+constexpr int A_SAMPLE = C1 * A_PIX; // 21632 floats per sample (86,528 B)
+constexpr int C2 = 64;               // conv2 out channels
+constexpr int O_HW = 24;             // conv2 output spatial size
+constexpr int P_HW = 12;             // pooled spatial size
+constexpr int P_WIN = P_HW * P_HW;   // 144 pooling windows per channel
+constexpr int P_SAMPLE = C2 * P_WIN; // 9216 = fc1 in_features
+constexpr int NCLS = 10;
+constexpr int K2 = C1 * 9;           // conv2 reduction length per output (288)
+constexpr int W2_N = C2 * K2;        // 18432
+constexpr int W3_N = NCLS * P_SAMPLE;// 92160
+constexpr int CODE_NONE = 4;         // pooled value <= 0: ReLU blocks the gradient
+}  // namespace slk
+
+#define SLK_CHECK_ARG(cond)                 \
+    do {                                    \
+        if (!(cond)) return (int)hipErrorInvalidValue; \
+    } while (0)
+
+static inline int slk_launch_status() { return (int)hipGetLastError(); }
+
+static inline hipStream_t slk_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// f32-input MFMA wrappers (exact f32, k-ordered fma chain; cdna_hip_programming.md §3).
+// 32x32x2: lane l supplies A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31];
+//          D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5), r in [0,16).
+// 16x16x4: lane l supplies A[i=l&15][k=l>>4] and B[k=l>>4][j=l&15];
+//          D: col = l&15, row = 4*(l>>4) + r, r in [0,4).
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}

@@ -1,0 +1,84 @@
+"""ctypes binding of libslk.so (include/slk.h).
+
+The library must already be built (splitcnn.build / __graft_entry__.build()). There is no CPU or
+PyTorch fallback: if the library is missing, or the device is not a ROCm GPU, every op raises.
+torch is imported first so that the process's HIP runtime is torch's libamdhip64.so.7; libslk.so
+names the same soname and therefore binds to that one runtime instance.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libslk.so)
+
+from .build import LIB_PATH
+
+_c_float_p = ctypes.c_void_p  # device pointers travel as integers
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+_SIGS = {
+    "slk_abi_version": [],
+    "slk_error_string": [_I],
+    "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],
+    "slk_conv1_wgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_conv1_wgrad_nslab": [_I],
+    "slk_conv2_fwd_pool": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_fc_fwd": [_P, _P, _P, _P, _I, _P],
+    "slk_xent_fwd_bwd": [_P, _P, _P, _P, _F, _P, _I, _P],
+    "slk_fc_dgrad": [_P, _P, _P, _I, _P],
+    "slk_fc_xent": [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _I, _P],
+    "slk_fc_wgrad": [_P, _P, _P, _I, _P],
+    "slk_fc_wgrad_nslab": [_I],
+    "slk_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad_nslab": [_I],
+    "slk_reduce_slabs": [_P, _I, _I, _P, _P],
+    "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
+    "slk_sgd": [_P, _P, _I, _F, _P],
+    "slk_loss_mean": [_P, _I, _P, _I, _P],
+    "slk_loss_log": [_P, _I, _P, _I, _P, _P],
+}
+_RESTYPES = {"slk_error_string": ctypes.c_char_p}
+
+SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+class SLKError(RuntimeError):
+    """A libslk.so entry point returned a nonzero hipError_t."""
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libslk.so once and attach the signatures; raises if it is missing or incomplete."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"splitcnn: {path} is missing. Build the HIP kernels first "
+            "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)  # AttributeError here means the .so does not match slk.h
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke an slk_* entry point and raise SLKError on a nonzero hipError_t."""
+    err = getattr(load(), name)(*args)
+    if err != 0:
+        msg = load().slk_error_string(err)
+        raise SLKError(f"{name} failed: hipError {err} ({msg.decode() if msg else '?'})")
+
+
+def query(name: str, *args) -> int:
+    """Invoke a size-query entry point (returns a value, not a status)."""
+    return int(getattr(load(), name)(*args))

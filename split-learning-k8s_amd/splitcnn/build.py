@@ -1,0 +1,62 @@
+"""Build libslk.so (the gfx950 HIP kernels + C-ABI) in-tree with hipcc.
+
+The library is built into this package directory so it travels with the repository snapshot to the
+GPU box (a JIT cache under ~/.cache would not). `python -m splitcnn.build` or
+`__graft_entry__.build()` drive it; it cross-compiles without a GPU.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
+INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include")
+LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
+SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip"]
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the splitcnn kernels need ROCm's hipcc to build")
+
+
+def _inputs():
+    srcs = [os.path.join(CSRC_DIR, s) for s in SOURCES]
+    hdrs = [os.path.join(CSRC_DIR, f) for f in os.listdir(CSRC_DIR) if f.endswith(".h")]
+    hdrs.append(os.path.join(INCLUDE_DIR, "slk.h"))
+    return srcs, hdrs
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    srcs, hdrs = _inputs()
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(f) > t for f in srcs + hdrs)
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    """Compile every HIP source for gfx950 and link libslk.so next to this file."""
+    if not force and not needs_build():
+        return LIB_PATH
+    srcs, _ = _inputs()
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", INCLUDE_DIR, *srcs, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build_library(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,297 @@
+"""The split-CNN step engine: client stage, server stage and the 1-GPU fused trainer.
+
+This is the MI355X-native form of the reference's step contract (src/client_part.py:110-138 <->
+src/server_part.py:25-58):
+
+    client:  zero_grad; act = model(x)                         (client_part.py:112-114)
+             send {act.detach(), labels, step}                 (client_part.py:117-125)
+    server:  act.requires_grad_(True); zero_grad; fwd; CE loss; backward; SGD step;
+             log loss at step; return act.grad                 (server_part.py:45-58)
+    client:  act.backward(cut_grad); SGD step; step += 1      (client_part.py:131-138)
+
+API: ``ClientStage.forward(x) -> act``, ``ServerStage.step(act, labels, step) ->
+(cut_grad, loss)``, ``ClientStage.backward_step(cut_grad)``. Each stage keeps its parameters in ONE
+flat device block (the module's Parameters become views of it, so state_dict / load_state_dict keep
+working) and its gradients in another; the weight-gradient slabs of the wgrad kernels are reduced in
+fixed order inside the fused SGD launch. Nothing synchronises with the host: the loss goes to a
+device ring (LossLog) flushed every N steps, replacing the per-step mlflow.log_metric REST call
+(server_part.py:55). `SplitTrainer` runs both stages on one GPU and captures the whole step in a
+HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .model_def import ModelPartA, ModelPartB
+
+LR = 0.01  # optim.SGD(lr=0.01) on both sides (client_part.py:17, server_part.py:15)
+
+
+def _flatten_params(params: List[nn.Parameter], device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Move `params` into one flat fp32 block; each Parameter becomes a view of it."""
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, dtype=torch.float32, device=device)
+    gflat = torch.zeros(n, dtype=torch.float32, device=device)
+    off = 0
+    for p in params:
+        k = p.numel()
+        flat[off:off + k].copy_(p.detach().reshape(-1).to(device=device, dtype=torch.float32))
+        p.data = flat[off:off + k].view(p.shape)
+        p.grad = gflat[off:off + k].view(p.shape)
+        off += k
+    return flat, gflat
+
+
+class _Buffers:
+    """Per-batch-size scratch owned by a stage (allocated once, reused every step)."""
+
+    def __init__(self):
+        self._b = {}
+
+    def get(self, name, shape, dtype, device):
+        t = self._b.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != device:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self._b[name] = t
+        return t
+
+
+class LossLog:
+    """Device-side loss log: one ring slot per server step, written by slk_loss_log (the device
+    counter advances inside the kernel, so graph replays log too). `flush()` copies the ring to the
+    host once and returns/sinks [(step, loss)] — the replacement of mlflow.log_metric("loss", ...,
+    step=step) (src/server_part.py:55)."""
+
+    def __init__(self, device, capacity: int = 4096, sink: Optional[Callable[[int, float], None]] = None):
+        self.device = torch.device(device)
+        self.capacity = capacity
+        self.ring = torch.zeros(capacity, dtype=torch.float32, device=self.device)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.sink = sink
+        self._flushed = 0            # number of entries already flushed
+        self._steps: List[int] = []  # host-side step ids, in logging order (no device sync needed)
+        self.history: List[Tuple[int, float]] = []
+
+    def note_step(self, step: int):
+        self._steps.append(int(step))
+
+    def flush(self) -> List[Tuple[int, float]]:
+        count = int(self.counter.item())
+        new = count - self._flushed
+        if new <= 0:
+            return []
+        if new > self.capacity:
+            raise RuntimeError(f"LossLog overflow: {new} unflushed steps > capacity {self.capacity}")
+        ring = self.ring.cpu()
+        out = []
+        for i in range(self._flushed, count):
+            step = self._steps[i] if i < len(self._steps) else i
+            loss = float(ring[i % self.capacity])
+            out.append((step, loss))
+            if self.sink is not None:
+                self.sink(step, loss)
+        self._flushed = count
+        self.history.extend(out)
+        return out
+
+
+class ClientStage:
+    """Client half: ModelPartA on one device + SGD (src/client_part.py:16-17,112-133)."""
+
+    def __init__(self, model: Optional[ModelPartA] = None, lr: float = LR, device="cuda"):
+        self.device = torch.device(device)
+        self.model = (model if model is not None else ModelPartA()).to(self.device)
+        self.lr = lr
+        self.params, self.grads = _flatten_params(
+            [self.model.conv1.weight, self.model.conv1.bias], self.device)
+        self._buf = _Buffers()
+        self._x = None
+        self._act = None
+
+    @property
+    def W1(self):
+        return self.model.conv1.weight
+
+    @property
+    def b1(self):
+        return self.model.conv1.bias
+
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """act = relu(conv1(x)) (client_part.py:114). Keeps x/act for backward_step."""
+        B = x.shape[0]
+        act = out if out is not None else self._buf.get("act", (B, 32, 26, 26), torch.float32, self.device)
+        ops.conv1_fwd(x, self.W1.detach(), self.b1.detach(), out=act)
+        self._x, self._act = x, act
+        return act
+
+    def backward_step(self, cut_grad: torch.Tensor, x: Optional[torch.Tensor] = None,
+                      act: Optional[torch.Tensor] = None) -> None:
+        """act.backward(cut_grad); optimizer.step() (client_part.py:132-133): relu-bwd + conv1
+        wgrad slabs, then one fused reduce+SGD launch over the 320 client parameters."""
+        x = self._x if x is None else x
+        act = self._act if act is None else act
+        B = x.shape[0]
+        slabs = self._buf.get("slabs", (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
+        ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
+        self.apply_grad_slabs(slabs)
+
+    def wgrad_slabs(self, cut_grad, x=None, act=None):
+        x = self._x if x is None else x
+        act = self._act if act is None else act
+        B = x.shape[0]
+        slabs = self._buf.get("slabs", (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
+        return ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
+
+    def apply_grad_slabs(self, slabs):
+        ops.sgd_from_slabs(self.params, self.grads, slabs, self.lr)
+
+    def apply_grad(self):
+        """SGD from the (already reduced / all-reduced) flat gradient block."""
+        ops.sgd(self.params, self.grads, self.lr)
+
+
+class ServerStage:
+    """Server half: ModelPartB + CrossEntropyLoss + SGD + loss log (src/server_part.py:14-16,25-58)."""
+
+    def __init__(self, model: Optional[ModelPartB] = None, lr: float = LR, device="cuda",
+                 loss_log: Optional[LossLog] = None):
+        self.device = torch.device(device)
+        self.model = (model if model is not None else ModelPartB()).to(self.device)
+        self.lr = lr
+        m = self.model
+        self.params, self.grads = _flatten_params(
+            [m.conv2.weight, m.conv2.bias, m.fc1.weight, m.fc1.bias], self.device)
+        self.loss_log = loss_log if loss_log is not None else LossLog(self.device)
+        self.err_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._buf = _Buffers()
+
+    def _b(self, name, shape, dtype=torch.float32):
+        return self._buf.get(name, shape, dtype, self.device)
+
+    def forward_backward(self, act: torch.Tensor, labels: torch.Tensor, grad_scale: float,
+                         cut_grad: Optional[torch.Tensor] = None):
+        """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
+        conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss)."""
+        B = act.shape[0]
+        m = self.model
+        W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
+        W3, b3 = m.fc1.weight.detach(), m.fc1.bias.detach()
+        pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
+                                          code=self._b("code", (B, 64, 12, 12), torch.uint8))
+        _, loss_i, dlogits, dpooled = ops.fc_xent(
+            pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
+            loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
+            dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag)
+        if cut_grad is None:
+            cut_grad = self._b("cut_grad", (B, 32, 26, 26))
+        ops.conv2_dgrad(dpooled, code, W2, out=cut_grad)
+        s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
+                                   slabs=self._b("s2", (ops.conv2_wgrad_nslab(B), ops.CONV2_SLAB)))
+        s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+        return cut_grad, loss_i, s2, s3
+
+    def apply_grad_slabs(self, s2, s3):
+        """optimizer.step() (server_part.py:52): two fused reduce+SGD launches, one per slab kind."""
+        ops.sgd_from_slabs(self.params[:ops.CONV2_SLAB], self.grads[:ops.CONV2_SLAB], s2, self.lr)
+        ops.sgd_from_slabs(self.params[ops.CONV2_SLAB:], self.grads[ops.CONV2_SLAB:], s3, self.lr)
+
+    def apply_grad(self):
+        ops.sgd(self.params, self.grads, self.lr)
+
+    def reduce_grads(self, s2, s3):
+        """Reduce slabs into the flat gradient block without stepping (for all-reduce topologies)."""
+        ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB])
+        ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:])
+
+    def log_loss(self, loss_i, step: Optional[int] = None):
+        ops.loss_log(loss_i, self.loss_log.ring, self.loss_log.counter)
+        if step is not None:
+            self.loss_log.note_step(step)
+
+    def step(self, act: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
+             cut_grad: Optional[torch.Tensor] = None):
+        """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i).
+        The mean loss for `step` lands in the device loss log."""
+        B = act.shape[0]
+        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad)
+        self.apply_grad_slabs(s2, s3)
+        self.log_loss(loss_i, step)
+        return cut_grad, loss_i
+
+    def check_labels(self):
+        """Raise if any label seen so far was outside [0, 10) (torch raises IndexError there)."""
+        if int(self.err_flag.item()) != 0:
+            raise IndexError("splitcnn: a label was out of range [0, 10)")
+
+
+class SplitTrainer:
+    """Both stages fused on ONE GPU (BASELINE config 2): the cut tensor is handed over in place.
+
+    `step(x, y)` = client fwd -> server fwd/loss/bwd/SGD -> client bwd/SGD, exactly one reference
+    step. With `graph=True` the step is captured once per batch size into a HIP graph (static input
+    buffers; `step` copies into them unless the caller hands in those very buffers)."""
+
+    def __init__(self, client: Optional[ModelPartA] = None, server: Optional[ModelPartB] = None,
+                 lr: float = LR, device="cuda", graph: bool = True, loss_log: Optional[LossLog] = None):
+        self.device = torch.device(device)
+        self.client = ClientStage(client, lr, self.device)
+        self.server = ServerStage(server, lr, self.device, loss_log)
+        self.graph = graph
+        self._graphs = {}
+        self.global_step = 0
+
+    @property
+    def loss_log(self) -> LossLog:
+        return self.server.loss_log
+
+    def _eager(self, x, y):
+        act = self.client.forward(x)
+        cut_grad, _ = self.server.step(act, y)
+        self.client.backward_step(cut_grad)
+
+    def static_inputs(self, B: int):
+        g = self._graph_for(B)
+        return g["x"], g["y"]
+
+    def _graph_for(self, B: int):
+        g = self._graphs.get(B)
+        if g is not None:
+            return g
+        x = torch.zeros((B, 1, 28, 28), dtype=torch.float32, device=self.device)
+        y = torch.zeros((B,), dtype=torch.int64, device=self.device)
+        # warm up on a side stream (allocations happen here, not during capture), then restore the
+        # parameters and the loss log so the warm-up leaves no trace.
+        saved_c, saved_s = self.client.params.clone(), self.server.params.clone()
+        saved_ctr = self.server.loss_log.counter.clone()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._eager(x, y)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._eager(x, y)
+        self.client.params.copy_(saved_c)
+        self.server.params.copy_(saved_s)
+        self.server.loss_log.counter.copy_(saved_ctr)
+        g = {"graph": graph, "x": x, "y": y}
+        self._graphs[B] = g
+        return g
+
+    def step(self, x: torch.Tensor, y: torch.Tensor):
+        B = x.shape[0]
+        if self.graph:
+            g = self._graph_for(B)
+            if x.data_ptr() != g["x"].data_ptr():
+                g["x"].copy_(x, non_blocking=True)
+            if y.data_ptr() != g["y"].data_ptr():
+                g["y"].copy_(y, non_blocking=True)
+            g["graph"].replay()
+        else:
+            self._eager(x, y)
+        self.server.loss_log.note_step(self.global_step)
+        self.global_step += 1

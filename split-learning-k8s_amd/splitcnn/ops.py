@@ -1,0 +1,217 @@
+"""Tensor-level wrappers over the libslk.so C-ABI (include/slk.h).
+
+Every function takes device tensors, checks device / dtype / shape / contiguity on the host (the
+kernels assume the exact shapes of src/model_def.py), allocates outputs and workspaces with torch's
+caching allocator when the caller does not pass them, and launches on torch's current HIP stream.
+Nothing here synchronises, so a sequence of these calls can be captured in a HIP graph.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+CLIENT_NPARAM = 320
+SERVER_NPARAM = 110666
+OFF_W2, OFF_B2, OFF_W3, OFF_B3 = 0, 18432, 18496, 110656
+CONV2_SLAB = 18496   # [dW2 | db2]
+FC_SLAB = 92170      # [dW3 | db3]
+
+_F32 = torch.float32
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev(t: torch.Tensor, name: str, shape=None, dtype=_F32) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"splitcnn: {name} is on {t.device}; the split-CNN ops run only on the MI355X HIP kernels "
+            "(move the module and its inputs to a ROCm device). There is no CPU fallback.")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t.data_ptr()
+
+
+def _out(out, shape, like, dtype=_F32, name="out"):
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=like.device)
+    _dev(out, name, shape, dtype)
+    return out
+
+
+def batch_of(x: torch.Tensor, tail: tuple, name: str) -> int:
+    if x.dim() != 1 + len(tail) or tuple(x.shape[1:]) != tail:
+        raise ValueError(f"{name}: expected shape [B,{','.join(map(str, tail))}], got {tuple(x.shape)}")
+    return int(x.shape[0])
+
+
+# ------------------------------------------------------------------------------------ client stage
+def conv1_fwd(x, W1, b1, out=None):
+    B = batch_of(x, (1, 28, 28), "x")
+    act = _out(out, (B, 32, 26, 26), x)
+    _lib.call("slk_conv1_fwd", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)),
+              _dev(b1, "conv1.bias", (32,)), _dev(act, "act"), B, _stream(x))
+    return act
+
+
+def conv1_wgrad_nslab(B: int) -> int:
+    return _lib.query("slk_conv1_wgrad_nslab", B)
+
+
+def conv1_wgrad_slabs(x, act, cut_grad, slabs=None):
+    B = batch_of(x, (1, 28, 28), "x")
+    nslab = conv1_wgrad_nslab(B)
+    slabs = _out(slabs, (nslab, CLIENT_NPARAM), x, name="slabs")
+    _lib.call("slk_conv1_wgrad", _dev(x, "x"), _dev(act, "act", (B, 32, 26, 26)),
+              _dev(cut_grad, "cut_grad", (B, 32, 26, 26)), _dev(slabs, "slabs"), B, _stream(x))
+    return slabs
+
+
+# ------------------------------------------------------------------------------------ server stage
+def conv2_fwd_pool(act, W2, b2, pooled=None, code=None):
+    B = batch_of(act, (32, 26, 26), "act")
+    pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
+    code = _out(code, (B, 64, 12, 12), act, torch.uint8, "code")
+    _lib.call("slk_conv2_fwd_pool", _dev(act, "act"), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+              _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"), _dev(code, "code", dtype=torch.uint8),
+              B, _stream(act))
+    return pooled, code
+
+
+def _pooled_batch(pooled):
+    if pooled.dim() == 2:
+        return batch_of(pooled, (9216,), "pooled")
+    return batch_of(pooled, (64, 12, 12), "pooled")
+
+
+def fc_fwd(pooled, W3, b3, out=None):
+    B = _pooled_batch(pooled)
+    logits = _out(out, (B, 10), pooled)
+    _lib.call("slk_fc_fwd", _dev(pooled, "pooled"), _dev(W3, "fc1.weight", (10, 9216)),
+              _dev(b3, "fc1.bias", (10,)), _dev(logits, "logits"), B, _stream(pooled))
+    return logits
+
+
+def _labels(labels, B):
+    _dev(labels, "labels", (B,), torch.int64)
+    return labels.data_ptr()
+
+
+def xent_fwd_bwd(logits, labels, grad_scale, loss_i=None, dlogits=None, err_flag=None):
+    B = batch_of(logits, (10,), "logits")
+    loss_i = _out(loss_i, (B,), logits, name="loss_i")
+    dlogits = _out(dlogits, (B, 10), logits, name="dlogits")
+    eptr = _dev(err_flag, "err_flag", (1,), torch.int32) if err_flag is not None else None
+    _lib.call("slk_xent_fwd_bwd", _dev(logits, "logits"), _labels(labels, B), _dev(loss_i, "loss_i"),
+              _dev(dlogits, "dlogits"), float(grad_scale), eptr, B, _stream(logits))
+    return loss_i, dlogits
+
+
+def fc_dgrad(dlogits, W3, out=None):
+    B = batch_of(dlogits, (10,), "dlogits")
+    dpooled = _out(out, (B, 9216), dlogits, name="dpooled")
+    _lib.call("slk_fc_dgrad", _dev(dlogits, "dlogits"), _dev(W3, "fc1.weight", (10, 9216)),
+              _dev(dpooled, "dpooled"), B, _stream(dlogits))
+    return dpooled
+
+
+def fc_xent(pooled, W3, b3, labels, grad_scale, logits=None, loss_i=None, dlogits=None,
+            dpooled=None, err_flag=None):
+    B = _pooled_batch(pooled)
+    logits = _out(logits, (B, 10), pooled, name="logits")
+    loss_i = _out(loss_i, (B,), pooled, name="loss_i")
+    dlogits = _out(dlogits, (B, 10), pooled, name="dlogits")
+    dpooled = _out(dpooled, tuple(pooled.shape), pooled, name="dpooled")
+    eptr = _dev(err_flag, "err_flag", (1,), torch.int32) if err_flag is not None else None
+    _lib.call("slk_fc_xent", _dev(pooled, "pooled"), _dev(W3, "fc1.weight", (10, 9216)),
+              _dev(b3, "fc1.bias", (10,)), _labels(labels, B), _dev(logits, "logits"),
+              _dev(loss_i, "loss_i"), _dev(dlogits, "dlogits"), _dev(dpooled, "dpooled"),
+              float(grad_scale), eptr, B, _stream(pooled))
+    return logits, loss_i, dlogits, dpooled
+
+
+def fc_wgrad_nslab(B: int) -> int:
+    return _lib.query("slk_fc_wgrad_nslab", B)
+
+
+def fc_wgrad_slabs(dlogits, pooled, slabs=None):
+    B = batch_of(dlogits, (10,), "dlogits")
+    if _pooled_batch(pooled) != B:
+        raise ValueError("pooled / dlogits batch mismatch")
+    slabs = _out(slabs, (fc_wgrad_nslab(B), FC_SLAB), dlogits, name="slabs")
+    _lib.call("slk_fc_wgrad", _dev(dlogits, "dlogits"), _dev(pooled, "pooled"), _dev(slabs, "slabs"),
+              B, _stream(dlogits))
+    return slabs
+
+
+def _dpooled_batch(dpooled):
+    return _pooled_batch(dpooled)
+
+
+def conv2_dgrad(dpooled, code, W2, out=None):
+    B = _dpooled_batch(dpooled)
+    cut_grad = _out(out, (B, 32, 26, 26), dpooled, name="cut_grad")
+    _lib.call("slk_conv2_dgrad", _dev(dpooled, "dpooled"), _dev(code, "code", (B, 64, 12, 12), torch.uint8),
+              _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(cut_grad, "cut_grad"), B, _stream(dpooled))
+    return cut_grad
+
+
+def conv2_wgrad_nslab(B: int) -> int:
+    return _lib.query("slk_conv2_wgrad_nslab", B)
+
+
+def conv2_wgrad_slabs(act, dpooled, code, slabs=None):
+    B = batch_of(act, (32, 26, 26), "act")
+    if _dpooled_batch(dpooled) != B:
+        raise ValueError("act / dpooled batch mismatch")
+    slabs = _out(slabs, (conv2_wgrad_nslab(B), CONV2_SLAB), act, name="slabs")
+    _lib.call("slk_conv2_wgrad", _dev(act, "act"), _dev(dpooled, "dpooled"),
+              _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(act))
+    return slabs
+
+
+# ------------------------------------------------------------------------------------ reductions
+def reduce_slabs(slabs, out=None):
+    nslab, n = slabs.shape
+    out = _out(out, (n,), slabs, name="out")
+    _lib.call("slk_reduce_slabs", _dev(slabs, "slabs"), nslab, n, _dev(out, "out"), _stream(slabs))
+    return out
+
+
+def sgd_from_slabs(param, grad, slabs, lr):
+    """param -= lr * sum(slabs); grad = sum(slabs) (grad may be None). 1-D flat views."""
+    nslab, n = slabs.shape
+    _dev(param, "param", (n,))
+    gptr = _dev(grad, "grad", (n,)) if grad is not None else None
+    _lib.call("slk_sgd_from_slabs", param.data_ptr(), gptr, _dev(slabs, "slabs"), nslab, n, float(lr),
+              _stream(param))
+
+
+def sgd(param, grad, lr):
+    n = param.numel()
+    _lib.call("slk_sgd", _dev(param, "param"), _dev(grad, "grad", tuple(param.shape)), n, float(lr),
+              _stream(param))
+
+
+def loss_mean(loss_i, out=None, slot=0):
+    B = loss_i.numel()
+    out = _out(out, (1,), loss_i, name="out") if out is None else out
+    _dev(out, "out")
+    if not (0 <= slot < out.numel()):
+        raise IndexError("loss_mean slot out of range")
+    _lib.call("slk_loss_mean", _dev(loss_i, "loss_i"), B, out.data_ptr(), int(slot), _stream(loss_i))
+    return out
+
+
+def loss_log(loss_i, ring, counter):
+    B = loss_i.numel()
+    _lib.call("slk_loss_log", _dev(loss_i, "loss_i"), B, _dev(ring, "ring"), ring.numel(),
+              _dev(counter, "counter", (1,), torch.int32), _stream(loss_i))

@@ -1,0 +1,249 @@
+"""GPU parity: the HIP split step (libslk.so via the C-ABI) against the reference's golden fixtures
+(tests/golden/, generated from the reference src/model_def.py) and the numpy oracle.
+
+Tolerances (SURVEY §8c noise floor: fp32 thread-count drift 9e-6 loss / 7e-5 weights):
+  per-step tensors from identical state  rel_err <= 1e-4  (max|diff| / max|ref|)
+  conv1 activations                      rel_err <= 1e-5
+  loss                                   relative <= 1e-5
+  1k-step loss curve                     relative <= 1e-3 per step
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import FIXTURES, PARAMS, load_fixture, rel_err, weight_ok
+
+pytestmark = pytest.mark.gpu
+
+KEYS = {"W1": ("conv1", "weight"), "b1": ("conv1", "bias"), "W2": ("conv2", "weight"),
+        "b2": ("conv2", "bias"), "W3": ("fc1", "weight"), "b3": ("fc1", "bias")}
+
+
+def make_models(fx, prefix="init_"):
+    from splitcnn.model_def import ModelPartA, ModelPartB
+    a, b = ModelPartA(), ModelPartB()
+    sd_a = {"conv1.weight": torch.from_numpy(fx[prefix + "W1"]), "conv1.bias": torch.from_numpy(fx[prefix + "b1"])}
+    sd_b = {"conv2.weight": torch.from_numpy(fx[prefix + "W2"]), "conv2.bias": torch.from_numpy(fx[prefix + "b2"]),
+            "fc1.weight": torch.from_numpy(fx[prefix + "W3"]), "fc1.bias": torch.from_numpy(fx[prefix + "b3"])}
+    a.load_state_dict(sd_a)
+    b.load_state_dict(sd_b)
+    return a, b
+
+
+def param_of(client, server, k):
+    mod, attr = KEYS[k]
+    m = client.model if k in ("W1", "b1") else server.model
+    return getattr(getattr(m, mod), attr).detach().cpu().numpy()
+
+
+def grad_of(client, server, k):
+    off = {"W1": (0, 288), "b1": (288, 320), "W2": (0, 18432), "b2": (18432, 18496),
+           "W3": (18496, 110656), "b3": (110656, 110666)}[k]
+    g = client.grads if k in ("W1", "b1") else server.grads
+    return g[off[0]:off[1]].cpu().numpy()
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_engine_matches_reference_fixture(gpu, name):
+    from splitcnn.engine import ClientStage, ServerStage
+    fx = load_fixture(name)
+    a, b = make_models(fx)
+    client, server = ClientStage(a, device=gpu), ServerStage(b, device=gpu)
+    prev = {k: fx[f"init_{k}"] for k in PARAMS}
+    for s in range(1, int(fx["nsteps"]) + 1):
+        x = torch.from_numpy(fx[f"x_{s}"]).to(gpu)
+        y = torch.from_numpy(fx[f"y_{s}"]).to(gpu)
+        act = client.forward(x)
+        assert rel_err(act.cpu().numpy(), fx[f"act_{s}"]) <= 1e-5
+        cut_grad, loss_i = server.step(act, y, step=s)
+        logits = server._buf.get("logits", (x.shape[0], 10), torch.float32, gpu)
+        assert rel_err(logits.cpu().numpy(), fx[f"logits_{s}"]) <= 1e-4
+        assert rel_err(cut_grad.cpu().numpy(), fx[f"cut_grad_{s}"]) <= 1e-4
+        client.backward_step(cut_grad)
+        torch.cuda.synchronize()
+        (step, loss), = server.loss_log.flush()
+        assert step == s
+        assert abs(loss - float(fx[f"loss_{s}"])) <= 1e-5 * abs(float(fx[f"loss_{s}"]))
+        if s == 1:
+            for k in PARAMS:
+                assert rel_err(grad_of(client, server, k), fx[f"grad_{k}_1"]) <= 1e-4, k
+        if f"post_W1_{s}" in fx:
+            for k in PARAMS:
+                assert weight_ok(param_of(client, server, k), fx[f"post_{k}_{s}"], prev[k]), (k, s)
+        prev = {k: param_of(client, server, k) for k in PARAMS}
+
+
+@pytest.mark.parametrize("name", ["split_step_b4.npz", "split_step_b13.npz"])
+def test_dropin_modules_reference_code(gpu, name):
+    """The reference's own step code (client_part.py:112-133, server_part.py:45-57) run verbatim on
+    the drop-in modules: autograd, .grad on the received leaf, activations.backward(grad)."""
+    from splitcnn.model_def import CrossEntropyLoss
+    fx = load_fixture(name)
+    client_m, server_m = make_models(fx)
+    client_m, server_m = client_m.to(gpu), server_m.to(gpu)
+    copt = torch.optim.SGD(client_m.parameters(), lr=0.01)
+    sopt = torch.optim.SGD(server_m.parameters(), lr=0.01)
+    criterion = CrossEntropyLoss()
+    x = torch.from_numpy(fx["x_1"]).to(gpu)
+    y = torch.from_numpy(fx["y_1"]).to(gpu)
+    copt.zero_grad()
+    activations = client_m(x)
+    client_activations = activations.clone().detach()
+    client_activations.requires_grad_(True)
+    sopt.zero_grad()
+    outputs = server_m(client_activations)
+    loss = criterion(outputs, y)
+    loss.backward()
+    sopt.step()
+    cut = client_activations.grad.clone().detach()
+    activations.backward(cut)
+    copt.step()
+    assert rel_err(activations.detach().cpu().numpy(), fx["act_1"]) <= 1e-5
+    assert rel_err(outputs.detach().cpu().numpy(), fx["logits_1"]) <= 1e-4
+    assert abs(loss.item() - float(fx["loss_1"])) <= 1e-5 * abs(float(fx["loss_1"]))
+    assert rel_err(cut.cpu().numpy(), fx["cut_grad_1"]) <= 1e-4
+    sd = {**client_m.state_dict(), **server_m.state_dict()}
+    for k, (mod, attr) in KEYS.items():
+        assert weight_ok(sd[f"{mod}.{attr}"].cpu().numpy(), fx[f"post_{k}_1"], fx[f"init_{k}"]), k
+
+
+def test_fullmodel_matches_split(gpu):
+    from splitcnn.data import init_models
+    from splitcnn.model_def import CrossEntropyLoss
+    fx = load_fixture("split_step_b4.npz")
+    full = init_models(seed=0, full=True).to(gpu)
+    x = torch.from_numpy(fx["x_1"]).to(gpu)
+    y = torch.from_numpy(fx["y_1"]).to(gpu)
+    loss = CrossEntropyLoss()(full(x), y)
+    loss.backward()
+    assert abs(loss.item() - float(fx["loss_1"])) <= 1e-5 * float(fx["loss_1"])
+    assert rel_err(full.conv1.weight.grad.cpu().numpy(), fx["grad_W1_1"]) <= 1e-4
+    assert rel_err(full.fc1.weight.grad.cpu().numpy(), fx["grad_W3_1"]) <= 1e-4
+
+
+def test_loss_curve_1k_steps_graph(gpu):
+    """1000 steps at B=64 (HIP-graph replay) follow the reference's curve within 1e-3 per step."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    fx = load_fixture("loss_curve_b64.npz")
+    a, b = init_models(seed=0)
+    tr = SplitTrainer(a, b, device=gpu, graph=True)
+    data = SyntheticMNIST(42)
+    n = int(fx["nsteps"])
+    xs, ys = zip(*(data.batch(64) for _ in range(n)))
+    X = torch.stack(xs).to(gpu)
+    Y = torch.stack(ys).to(gpu)
+    losses = []
+    for s in range(n):
+        tr.step(X[s], Y[s])
+        if (s + 1) % 250 == 0:
+            losses += [l for _, l in tr.loss_log.flush()]
+    losses = np.array(losses)
+    want = fx["losses"].astype(np.float64)
+    rel = np.abs(losses - want) / np.abs(want)
+    assert rel.max() <= 1e-3, (rel.argmax(), rel.max())
+    for k in PARAMS:
+        got = param_of(tr.client, tr.server, k)
+        assert rel_err(got, fx[f"final_{k}"]) <= 1e-3, k
+
+
+def test_graph_equals_eager_and_deterministic(gpu):
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    data = SyntheticMNIST(1)
+    batches = [data.batch(96) for _ in range(4)]
+    results = []
+    for graph in (False, True, True):
+        a, b = init_models(seed=2)
+        tr = SplitTrainer(a, b, device=gpu, graph=graph)
+        for x, y in batches:
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        results.append((tr.client.params.cpu(), tr.server.params.cpu(),
+                        [l for _, l in tr.loss_log.flush()]))
+    for r in results[1:]:
+        assert torch.equal(r[0], results[0][0])
+        assert torch.equal(r[1], results[0][1])
+        assert r[2] == results[0][2]
+
+
+@pytest.mark.parametrize("B", [1, 3, 5, 17, 63, 64, 65])
+def test_ragged_batches_vs_oracle(gpu, B):
+    from oracle.split_step import split_step
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    a, b = init_models(seed=B)
+    P = {"W1": a.conv1.weight, "b1": a.conv1.bias, "W2": b.conv2.weight, "b2": b.conv2.bias,
+         "W3": b.fc1.weight, "b3": b.fc1.bias}
+    P = {k: v.detach().double().numpy() for k, v in P.items()}
+    x, y = SyntheticMNIST(100 + B).batch(B)
+    new, rec = split_step(P, x.double().numpy(), y.numpy())
+    client, server = ClientStage(a, device=gpu), ServerStage(b, device=gpu)
+    act = client.forward(x.to(gpu))
+    cut, _ = server.step(act, y.to(gpu), step=0)
+    client.backward_step(cut)
+    torch.cuda.synchronize()
+    (_, loss), = server.loss_log.flush()
+    assert rel_err(act.cpu().numpy(), rec["act"]) <= 1e-5
+    assert rel_err(cut.cpu().numpy(), rec["cut_grad"]) <= 1e-4
+    assert abs(loss - rec["loss"]) <= 1e-5 * abs(rec["loss"])
+    for k in PARAMS:
+        assert rel_err(grad_of(client, server, k), rec["grads"][k]) <= 1e-4, k
+
+
+def test_b4096_per_sample_independence(gpu):
+    """K2 size (B=4096): rows of a full-batch server pass are bit-identical to the same rows run as
+    a small batch (per-sample work is independent), weight grads are linear over batch chunks, and
+    8 sampled rows match the oracle."""
+    from oracle.split_step import server_step
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    B = 4096
+    a, b = init_models(seed=11)
+    W = {"W2": b.conv2.weight, "b2": b.conv2.bias, "W3": b.fc1.weight, "b3": b.fc1.bias}
+    W = {k: v.detach().double().numpy() for k, v in W.items()}
+    client, server = ClientStage(a, device=gpu), ServerStage(b, device=gpu)
+    x, y = SyntheticMNIST(5).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    act = client.forward(x).clone()
+    cut, loss_i, s2, s3 = server.forward_backward(act, y, 1.0 / B)
+    cut = cut.clone()
+    loss_i = loss_i.clone()
+    server.reduce_grads(s2, s3)
+    g_full = server.grads.clone()
+    rows = torch.tensor([0, 1, 777, 2048, 3001, 4090, 4094, 4095], device=gpu)
+    cut_s, loss_s, _, _ = server.forward_backward(act[rows].contiguous(), y[rows].contiguous(), 1.0 / B)
+    assert torch.equal(cut_s, cut[rows])
+    assert torch.equal(loss_s, loss_i[rows])
+    # linearity of the weight gradient over batch chunks
+    acc = torch.zeros_like(g_full)
+    for c in range(8):
+        sl = slice(c * 512, (c + 1) * 512)
+        _, _, s2c, s3c = server.forward_backward(act[sl].contiguous(), y[sl].contiguous(), 1.0 / B)
+        server.reduce_grads(s2c, s3c)
+        acc += server.grads
+    assert rel_err(acc.cpu().numpy(), g_full.cpu().numpy()) <= 1e-5
+    # oracle on the sampled rows (scaled by the full batch size)
+    r = server_step(act[rows].double().cpu().numpy(), y[rows].cpu().numpy(), W["W2"], W["b2"], W["W3"],
+                    W["b3"], grad_scale_batch=B)
+    assert rel_err(cut_s.cpu().numpy(), r["cut_grad"]) <= 1e-4
+    assert rel_err(loss_s.cpu().numpy(), r["loss_i"]) <= 1e-5
+
+
+def test_bad_label_sets_flag(gpu):
+    from splitcnn.data import init_models
+    from splitcnn.engine import ServerStage
+    _, b = init_models(seed=0)
+    server = ServerStage(b, device=gpu)
+    act = torch.rand(4, 32, 26, 26, device=gpu)
+    y = torch.tensor([0, 1, 10, 2], device=gpu)
+    server.step(act, y)
+    with pytest.raises(IndexError):
+        server.check_labels()
+
+
+def test_cpu_tensors_raise(gpu):
+    from splitcnn.model_def import ModelPartA
+    m = ModelPartA()
+    with pytest.raises(RuntimeError, match="HIP kernels"):
+        m(torch.zeros(2, 1, 28, 28))
