@@ -1,0 +1,273 @@
+"""Throughput benchmark of the MI355X split-CNN step (BASELINE.json metric: training samples/sec).
+
+  python bench.py [--gpus N --steps K --warmup W --batch B --topology T]
+  (N > 1: launched by torch.distributed.run, one process per GPU, RCCL over xGMI)
+
+N = 1 (BASELINE config 2, "K2"): both stages fused on one MI355X, synthetic 1x28x28 batches of 4096,
+fp32, the whole step (client fwd -> cut hand-off -> server fwd/CE/bwd/SGD -> client bwd/SGD)
+replayed as one HIP graph. Inputs are resident in HBM before the timed region (a pool of batches,
+copied into the graph's static input buffers inside each step).
+
+N > 1: --topology replicated (default; SplitFed-V1: each rank one client + one server replica,
+one 444 KB gradient all-reduce per step, weak scaling), pipeline (N=2: client GPU <-> server GPU,
+micro-batched RCCL send/recv) or hub (N-1 client GPUs -> 1 server GPU). With the default topology
+a short second phase runs the exchange topology (pipeline at N=2, hub at N>=3) and reports the
+cut-exchange rate beside a measured RCCL p2p peak ("exchange" object).
+
+One JSON line on rank 0 with the driver's contract plus "roofline" (dominant kernel, measured live
+with HIP events on the launch stream in an eager pass after the timed region) and "cpu_baseline"
+(rank 0, N = 1 only: the reference's client/server loop restated on torch CPU over FastAPI/HTTP +
+pickle, B = 64, timed on this host — oracle/cpu_loop.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "split-learning-k8s_amd"), ROOT]
+
+FLOP_PER_SAMPLE = 65_032_704          # total algorithmic FLOPs per training sample
+CONV2_FLOP_PER_SAMPLE = 21_233_664    # each of conv2 fwd / dgrad / wgrad
+FP32_PEAK_TFLOPS = 157.3              # MI355X_MICROARCH.md: fp32 matrix = vector peak
+HBM_PEAK_GBS = 8000.0
+CUT_BYTES = 86_528                    # fp32 [32,26,26] per sample, each direction
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="per-GPU (per-client) batch")
+    ap.add_argument("--topology", default="auto", choices=["auto", "replicated", "pipeline", "hub"])
+    ap.add_argument("--micro", type=int, default=4, help="micro-batches for the pipeline topology")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-pass", action="store_true")
+    ap.add_argument("--no-exchange-phase", action="store_true")
+    ap.add_argument("--exchange-steps", type=int, default=10)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The reference loop on this host's CPU (child process; runs before this process touches
+    the GPU)."""
+    cmd = [sys.executable, "-m", "oracle.cpu_loop", "--seconds", str(seconds), "--batch", "64"]
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=seconds + 120)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        d = json.loads(line)
+    except Exception as e:  # reported, never fatal
+        return {"value": None, "unit": "samples/s", "error": repr(e)[:300]}
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "?"
+    return {"value": round(d["value"], 1), "unit": "samples/s",
+            "cores": max(d.get("server_threads") or 1, d.get("client_threads") or 1),
+            "kind": "port",
+            "sample": f"{d['steps']} steps x B=64 in {d['seconds']:.1f}s: torch-CPU client+server processes "
+                      f"over FastAPI/uvicorn + requests + pickle on localhost (src/client_part.py:103-138 <-> "
+                      f"src/server_part.py:25-58, MLflow omitted); torch threads server={d.get('server_threads')} "
+                      f"client={d.get('client_threads')}; host nproc={d.get('nproc')} ({model})"}
+
+
+def make_pool(B, n, device, seed=42):
+    import torch
+
+    from splitcnn.data import SyntheticMNIST
+    data = SyntheticMNIST(seed)
+    xs, ys = zip(*(data.batch(B) for _ in range(n)))
+    return torch.stack(xs).to(device), torch.stack(ys).to(device)
+
+
+def timed(fn, K, W, device, group=None):
+    """W warm-up calls, then K timed calls bracketed by barrier + synchronize; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    for i in range(W):
+        fn(i)
+    torch.cuda.synchronize(device)
+    if dist.is_initialized():
+        dist.barrier(group=group)
+    t0 = time.perf_counter()
+    for i in range(K):
+        fn(W + i)
+    torch.cuda.synchronize(device)
+    if dist.is_initialized():
+        dist.barrier(group=group)
+    dt = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dt = float(t.item())
+    return dt
+
+
+def kernel_pass(run_eager, K, device):
+    """Eager steps with HIP events around each launch (on the launch stream)."""
+    from splitcnn.engine import TIMER
+    TIMER.reset()
+    TIMER.enabled = True
+    try:
+        for i in range(K):
+            run_eager(i)
+        return TIMER.summary()
+    finally:
+        TIMER.enabled = False
+
+
+def roofline_from(kern, B):
+    conv = {k: v for k, v in kern.items() if k.startswith("conv2_")}
+    if not conv:
+        return None
+    name = max(conv, key=lambda k: conv[k]["avg_ms"])
+    flops = CONV2_FLOP_PER_SAMPLE * B
+    ach = flops / (conv[name]["avg_ms"] * 1e-3) / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get(name, {}).get(str(B))
+        except Exception:
+            traffic = None
+    return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "flop_per_launch": flops, "avg_ms": round(conv[name]["avg_ms"], 4)}
+
+
+def run_single(args, out):
+    import torch
+
+    from splitcnn.data import init_models
+    from splitcnn.engine import SplitTrainer
+    dev = torch.device("cuda:0")
+    B = args.batch
+    X, Y = make_pool(B, 4, dev)
+    a, b = init_models(seed=0)
+    tr = SplitTrainer(a, b, device=dev, graph=not args.no_graph)
+    step = lambda i: tr.step(X[i % 4], Y[i % 4])  # noqa: E731
+    dt = timed(step, args.steps, args.warmup, dev)
+    losses = tr.loss_log.flush()
+    out.update(value=args.steps * B / dt, ms_per_step=dt / args.steps * 1e3)
+    out["config"] = {"workload": "K2: split CNN (model_def.py ModelPartA+ModelPartB) both stages fused on "
+                                 "1xMI355X, synthetic 1x28x28 MNIST-shape batches, fp32, HIP-graph step",
+                     "global_batch": B, "per_gpu_batch": B, "topology": "fused-1gpu",
+                     "graph": not args.no_graph}
+    out["loss_first_last"] = [round(losses[0][1], 5), round(losses[-1][1], 5)] if losses else None
+    if not args.no_kernel_pass:
+        tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False)
+        kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)
+        out["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
+        out["roofline"] = roofline_from(kern, B)
+    out["step_roofline_frac"] = round(out["value"] * FLOP_PER_SAMPLE / (FP32_PEAK_TFLOPS * 1e12), 4)
+
+
+def run_distributed(args, out, rank, world, local):
+    import torch
+    import torch.distributed as dist
+
+    from splitcnn import dist as sd
+    from splitcnn.data import init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    B = args.batch
+    topo = args.topology if args.topology != "auto" else "replicated"
+    X, Y = make_pool(B, 4, dev, seed=42 + rank)
+    a, b = init_models(seed=0)
+    grp = sd.client_group_for(world) if topo == "hub" or (topo == "replicated" and not args.no_exchange_phase) else None
+
+    def build(topology):
+        a, b = init_models(seed=0)
+        if topology == "replicated":
+            t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev))
+            return (lambda i: t.step(X[i % 4], Y[i % 4])), t, world * B
+        if topology == "pipeline":
+            assert world == 2
+            if rank == 0:
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=args.micro)
+                return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
+            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=args.micro)
+            return (lambda i: t.server_step(B, dev)), t, B
+        if topology == "hub":
+            if rank < world - 1:
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp)
+                return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
+            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp)
+            return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
+        raise ValueError(topology)
+
+    fn, t, global_batch = build(topo)
+    dt = timed(fn, args.steps, args.warmup, dev)
+    out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
+    out["config"] = {"workload": {"replicated": "K4-style SplitFed-V1: every GPU one client + one server "
+                                                "replica, gradient all-reduce per step",
+                                  "pipeline": "K3: 2xMI355X client-stage/server-stage pipeline, micro-batched "
+                                              "RCCL send/recv",
+                                  "hub": "K4: SplitFed N-1 client GPUs + 1 server GPU, client all-reduce"}[topo],
+                     "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
+                     "parallelism": f"{topo}{world}"}
+    out["scaling"] = "weak"
+    if topo in ("pipeline", "hub"):
+        out["exchange"] = {"topology": topo, "bytes_per_step": t.exchange_bytes,
+                           "GBps_effective": round(t.exchange_bytes / (dt / args.steps) / 1e9, 2)}
+    if topo == "replicated" and not args.no_exchange_phase:
+        try:
+            ex = "pipeline" if world == 2 else "hub"
+            fn2, t2, gb2 = build(ex)
+            K2 = args.exchange_steps
+            dt2 = timed(fn2, K2, 2, dev)
+            peak = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
+            pk = torch.tensor([peak or 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+            out["exchange"] = {"topology": ex, "samples_per_s": round(K2 * gb2 / dt2, 1),
+                               "bytes_per_step": t2.exchange_bytes,
+                               "GBps_effective": round(t2.exchange_bytes / (dt2 / K2) / 1e9, 2),
+                               "p2p_peak_GBps_measured": round(float(pk.item()), 2)}
+        except Exception as e:  # the headline number stands on its own
+            out["exchange"] = {"error": repr(e)[:300]}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    out = {"metric": "training samples/sec (node) for split CNN", "value": None, "unit": "samples/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic MNIST-shape batches (class prototypes + noise, normalised (0.1307, 0.3081)), "
+                   "random-init weights (seed 0)"}
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_baseline_seconds)  # before this process touches the GPU
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        run_distributed(args, out, rank, world, local)
+    else:
+        run_single(args, out)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+        if cpu.get("value"):
+            out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

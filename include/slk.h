@@ -111,8 +111,9 @@ int slk_conv2_wgrad_nslab(int B);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 
-/* out[i] = sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed order). */
-int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, void* stream);
+/* out[i] = (accumulate ? out[i] : 0) + sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed slab order).
+ * accumulate = 1 sums micro-batches into one gradient (pipeline topologies). */
+int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, int accumulate, void* stream);
 
 /* Fused deterministic slab reduction + SGD (lr, no momentum, no weight decay):
  * g = sum_s slabs[s*n+i]; grad[i] = g (if grad != NULL); param[i] -= lr * g.
@@ -123,14 +124,16 @@ int slk_sgd_from_slabs(float* param, float* grad, const float* slabs, int nslab,
 /* param[i] -= lr * grad[i]  (flat multi-tensor SGD; torch.optim.SGD semantics, momentum 0). */
 int slk_sgd(float* param, const float* grad, int n, float lr, void* stream);
 
-/* out[slot] = mean(loss_i[0..B))  (fixed-order reduction; the device-side loss log entry that
- * replaces mlflow.log_metric("loss", loss.item(), step) at src/server_part.py:55). */
-int slk_loss_mean(const float* loss_i, int B, float* out, int slot, void* stream);
+/* out[0] = scale * sum(values[0..n))  (fixed-order reduction). With values = per-sample losses and
+ * scale = 1/B this is nn.CrossEntropyLoss()'s mean (src/server_part.py:49). */
+int slk_loss_sum(const float* values, int n, float scale, float* out, void* stream);
 
-/* Loss log ring: ring[*counter % capacity] = mean(loss_i); ++*counter (one device thread).
- * The slot comes from device memory, so a captured HIP graph logs every replay into a new slot;
- * the host flushes the ring every N steps instead of a per-step .item() sync. */
-int slk_loss_log(const float* loss_i, int B, float* ring, int capacity, int* counter, void* stream);
+/* Loss log ring: ring[*counter % capacity] = scale * sum(values[0..n)); ++*counter (one device
+ * thread). This is the device-side replacement of mlflow.log_metric("loss", loss.item(), step)
+ * (src/server_part.py:55): the slot comes from device memory, so a captured HIP graph logs every
+ * replay into a new slot, and the host flushes the ring every N steps instead of syncing per step. */
+int slk_loss_log(const float* values, int n, float scale, float* ring, int capacity, int* counter,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,205 @@
+"""ORACLE / BASELINE HARNESS — TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
+
+A CPU restatement ("port") of the reference's split-learning loop, timed on the host cores:
+  server process: FastAPI app, POST /forward_pass with a pickled {activations, labels, step}
+                  payload; requires_grad_ -> zero_grad -> ModelPartB fwd -> CrossEntropy -> backward
+                  -> SGD(0.01) -> loss logged -> pickled activations.grad back
+                  (src/server_part.py:25-58; uvicorn single worker, k8s/split-learning.yaml:34)
+  client process: ModelPartA fwd -> pickle -> requests.post -> unpickle -> backward -> SGD(0.01)
+                  (src/client_part.py:103-138), batch 64 (client_part.py:98)
+The model is the same architecture written here with torch.nn layers on the CPU (the reference runs
+torch CPU, src/requirements.txt:2); MLflow is replaced by an in-memory list (no tracking server).
+Synthetic MNIST-shape batches replace the S3/torchvision download.
+
+Usage: python -m oracle.cpu_loop --seconds 15 --batch 64   -> prints one JSON line.
+"""
+
+import argparse
+import json
+import os
+import pickle
+import socket
+import subprocess
+import sys
+import time
+
+import torch
+import torch.nn as nn
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if os.path.join(_ROOT, "split-learning-k8s_amd") not in sys.path:
+    sys.path.insert(0, os.path.join(_ROOT, "split-learning-k8s_amd"))
+
+
+class PortPartA(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 32, 3, 1)
+        self.relu = nn.ReLU()
+
+    def forward(self, x):
+        return self.relu(self.conv1(x))
+
+
+class PortPartB(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv2 = nn.Conv2d(32, 64, 3, 1)
+        self.relu = nn.ReLU()
+        self.pool = nn.MaxPool2d(2)
+        self.flatten = nn.Flatten()
+        self.fc1 = nn.Linear(9216, 10)
+
+    def forward(self, x):
+        return self.fc1(self.flatten(self.pool(self.relu(self.conv2(x)))))
+
+
+def make_app():
+    from fastapi import FastAPI, Request, Response
+
+    app = FastAPI()
+    torch.manual_seed(0)
+    PortPartA()  # consume the client's init draws so the server weights match a seeded split init
+    model = PortPartB()
+    opt = torch.optim.SGD(model.parameters(), lr=0.01)
+    crit = nn.CrossEntropyLoss()
+    losses = []
+
+    @app.post("/forward_pass")
+    async def forward_pass(request: Request):
+        data = pickle.loads(await request.body())
+        act, labels, step = data["activations"], data["labels"], data["step"]
+        act.requires_grad_(True)
+        opt.zero_grad()
+        loss = crit(model(act), labels)
+        loss.backward()
+        opt.step()
+        losses.append((step, loss.item()))
+        return Response(content=pickle.dumps(act.grad.clone().detach()), media_type="application/octet-stream")
+
+    @app.get("/health")
+    async def health():
+        return {"status": "healthy", "threads": torch.get_num_threads(), "logged": len(losses)}
+
+    return app
+
+
+app = None
+if os.environ.get("SLK_CPU_LOOP_SERVER") == "1":
+    app = make_app()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_client(url: str, batch: int, seconds: float, warmup: int = 5, max_steps: int = 100000):
+    import requests
+
+    from splitcnn.data import SyntheticMNIST  # seeded CPU batches (no GPU use)
+    torch.manual_seed(0)
+    model = PortPartA()
+    opt = torch.optim.SGD(model.parameters(), lr=0.01)
+    data = SyntheticMNIST(42)
+    pool = [data.batch(batch) for _ in range(16)]
+    sess = requests.Session()
+    step = 0
+    t0 = None
+    timed = 0
+    while step < max_steps:
+        if step == warmup:
+            t0 = time.perf_counter()
+        x, y = pool[step % len(pool)]
+        opt.zero_grad()
+        act = model(x)
+        payload = pickle.dumps({"activations": act.clone().detach(), "labels": y, "step": step})
+        r = sess.post(url + "/forward_pass", data=payload)
+        if r.status_code != 200:
+            raise RuntimeError(f"server returned {r.status_code}")
+        act.backward(pickle.loads(r.content))
+        opt.step()
+        step += 1
+        if t0 is not None:
+            timed += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    dt = time.perf_counter() - t0
+    return timed, dt
+
+
+def compute_only(batch: int, seconds: float):
+    """Same step without HTTP/pickle (for context in the report)."""
+    from splitcnn.data import SyntheticMNIST
+    torch.manual_seed(0)
+    a, b = PortPartA(), PortPartB()
+    oa = torch.optim.SGD(a.parameters(), lr=0.01)
+    ob = torch.optim.SGD(b.parameters(), lr=0.01)
+    crit = nn.CrossEntropyLoss()
+    data = SyntheticMNIST(42)
+    pool = [data.batch(batch) for _ in range(16)]
+    n, t0 = 0, None
+    while True:
+        if n == 3:
+            t0 = time.perf_counter()
+        x, y = pool[n % 16]
+        oa.zero_grad()
+        act = a(x)
+        ad = act.detach().requires_grad_(True)
+        ob.zero_grad()
+        crit(b(ad), y).backward()
+        ob.step()
+        act.backward(ad.grad)
+        oa.step()
+        n += 1
+        if t0 is not None and time.perf_counter() - t0 >= seconds:
+            return (n - 3) * batch / (time.perf_counter() - t0)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=15.0)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--compute-seconds", type=float, default=0.0)
+    args = ap.parse_args(argv)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SLK_CPU_LOOP_SERVER="1",
+               PYTHONPATH=os.pathsep.join([root, os.path.join(root, "split-learning-k8s_amd"),
+                                           os.environ.get("PYTHONPATH", "")]))
+    port = _free_port()
+    srv = subprocess.Popen([sys.executable, "-m", "uvicorn", "oracle.cpu_loop:app", "--host", "127.0.0.1",
+                            "--port", str(port), "--workers", "1", "--log-level", "warning"],
+                           cwd=root, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    url = f"http://127.0.0.1:{port}"
+    try:
+        import requests
+        for _ in range(600):
+            try:
+                h = requests.get(url + "/health", timeout=1).json()
+                break
+            except Exception:
+                if srv.poll() is not None:
+                    raise RuntimeError("cpu_loop server died: " + srv.stderr.read().decode()[-2000:])
+                time.sleep(0.1)
+        else:
+            raise RuntimeError("cpu_loop server did not come up")
+        steps, dt = run_client(url, args.batch, args.seconds)
+    finally:
+        srv.terminate()
+        try:
+            srv.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+    out = {"value": steps * args.batch / dt, "unit": "samples/s", "steps": steps, "seconds": dt,
+           "batch": args.batch, "server_threads": h.get("threads"), "client_threads": torch.get_num_threads(),
+           "nproc": os.cpu_count()}
+    if args.compute_seconds > 0:
+        out["compute_only"] = compute_only(args.batch, args.compute_seconds)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

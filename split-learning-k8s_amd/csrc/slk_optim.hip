@@ -9,9 +9,9 @@
 __global__ __launch_bounds__(256) void sgd_from_slabs_kernel(float* __restrict__ param,
                                                              float* __restrict__ grad,
                                                              const float* __restrict__ slabs,
-                                                             int nslab, int n, float lr) {
+                                                             int nslab, int n, float lr, int acc) {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        float g = 0.f;
+        float g = acc ? grad[i] : 0.f;
         const float* s = slabs + i;
         int k = 0;
         for (; k + 4 <= nslab; k += 4) {  // 4 loads in flight, summed in slab order
@@ -31,29 +31,29 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ param,
         param[i] = param[i] - lr * grad[i];
 }
 
-__global__ __launch_bounds__(256) void loss_mean_kernel(const float* __restrict__ loss_i, int B,
-                                                        float* __restrict__ out) {
+__device__ __forceinline__ float block_sum_256(const float* __restrict__ v, int n) {
     __shared__ float red[4];
     float s = 0.f;
-    for (int i = threadIdx.x; i < B; i += 256) s += loss_i[i];
+    for (int i = threadIdx.x; i < n; i += 256) s += v[i];
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) out[0] = (((red[0] + red[1]) + red[2]) + red[3]) / (float)B;
+    return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ __launch_bounds__(256) void loss_log_kernel(const float* __restrict__ loss_i, int B,
+__global__ __launch_bounds__(256) void loss_sum_kernel(const float* __restrict__ v, int n, float scale,
+                                                       float* __restrict__ out) {
+    const float s = block_sum_256(v, n);
+    if (threadIdx.x == 0) out[0] = s * scale;
+}
+
+__global__ __launch_bounds__(256) void loss_log_kernel(const float* __restrict__ v, int n, float scale,
                                                        float* __restrict__ ring, int capacity,
                                                        int* __restrict__ counter) {
-    __shared__ float red[4];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < B; i += 256) s += loss_i[i];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
+    const float s = block_sum_256(v, n);
     if (threadIdx.x == 0) {
         const int c = *counter;
-        ring[c % capacity] = (((red[0] + red[1]) + red[2]) + red[3]) / (float)B;
+        ring[c % capacity] = s * scale;
         *counter = c + 1;
     }
 }
@@ -63,11 +63,13 @@ static inline int grid_for(int n) {
     return g > 2048 ? 2048 : (g < 1 ? 1 : g);
 }
 
-extern "C" int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, void* stream) {
+extern "C" int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, int accumulate,
+                                void* stream) {
     SLK_CHECK_ARG(nslab >= 0 && n >= 0);
     if (n == 0) return 0;
     SLK_CHECK_ARG(out && (slabs || nslab == 0));
-    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(nullptr, out, slabs, nslab, n, 0.f);
+    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(nullptr, out, slabs, nslab, n, 0.f,
+                                                                        accumulate ? 1 : 0);
     return slk_launch_status();
 }
 
@@ -76,7 +78,7 @@ extern "C" int slk_sgd_from_slabs(float* param, float* grad, const float* slabs,
     SLK_CHECK_ARG(nslab >= 0 && n >= 0);
     if (n == 0) return 0;
     SLK_CHECK_ARG(param && (slabs || nslab == 0));
-    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(param, grad, slabs, nslab, n, lr);
+    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(param, grad, slabs, nslab, n, lr, 0);
     return slk_launch_status();
 }
 
@@ -88,18 +90,18 @@ extern "C" int slk_sgd(float* param, const float* grad, int n, float lr, void* s
     return slk_launch_status();
 }
 
-extern "C" int slk_loss_mean(const float* loss_i, int B, float* out, int slot, void* stream) {
-    SLK_CHECK_ARG(B > 0 && slot >= 0);
-    SLK_CHECK_ARG(loss_i && out);
-    loss_mean_kernel<<<1, 256, 0, slk_stream(stream)>>>(loss_i, B, out + slot);
+extern "C" int slk_loss_sum(const float* values, int n, float scale, float* out, void* stream) {
+    SLK_CHECK_ARG(n > 0);
+    SLK_CHECK_ARG(values && out);
+    loss_sum_kernel<<<1, 256, 0, slk_stream(stream)>>>(values, n, scale, out);
     return slk_launch_status();
 }
 
-extern "C" int slk_loss_log(const float* loss_i, int B, float* ring, int capacity, int* counter,
-                            void* stream) {
-    SLK_CHECK_ARG(B > 0 && capacity > 0);
-    SLK_CHECK_ARG(loss_i && ring && counter);
-    loss_log_kernel<<<1, 256, 0, slk_stream(stream)>>>(loss_i, B, ring, capacity, counter);
+extern "C" int slk_loss_log(const float* values, int n, float scale, float* ring, int capacity,
+                            int* counter, void* stream) {
+    SLK_CHECK_ARG(n > 0 && capacity > 0);
+    SLK_CHECK_ARG(values && ring && counter);
+    loss_log_kernel<<<1, 256, 0, slk_stream(stream)>>>(values, n, scale, ring, capacity, counter);
     return slk_launch_status();
 }
 

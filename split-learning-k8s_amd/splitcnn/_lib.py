@@ -36,11 +36,11 @@ _SIGS = {
     "slk_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad_nslab": [_I],
-    "slk_reduce_slabs": [_P, _I, _I, _P, _P],
+    "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
     "slk_sgd": [_P, _P, _I, _F, _P],
-    "slk_loss_mean": [_P, _I, _P, _I, _P],
-    "slk_loss_log": [_P, _I, _P, _I, _P, _P],
+    "slk_loss_sum": [_P, _I, _F, _P, _P],
+    "slk_loss_log": [_P, _I, _F, _P, _I, _P, _P],
 }
 _RESTYPES = {"slk_error_string": ctypes.c_char_p}
 

@@ -1,0 +1,250 @@
+"""Multi-GPU split-learning topologies over torch.distributed (backend "nccl" = RCCL over xGMI on
+MI355X; "gloo" for the CPU protocol tests). One process per GPU.
+
+The reference has exactly one exchange per step: the client POSTs the cut activations and labels,
+the server answers with the cut gradient (src/client_part.py:117-131, src/server_part.py:38-58),
+and its k8s Deployment runs one client (k8s/split-learning.yaml:49). Its HTTP transport becomes
+device-resident exchange here:
+
+  Replicated (default for N >= 2; "SplitFed-V1" on one node): every rank hosts one client and one
+      server-side replica; the cut tensor is handed over in place on the GPU. After the backward,
+      ONE all-reduce of the [client grads | server grads | loss] bucket (444 KB) averages both
+      sides, so every rank applies the reference's SGD step for the concatenated global batch
+      N*B (mean loss over N*B). Weak scaling: no data-path collective besides that bucket.
+  Pipeline (N = 2): rank 0 = client stage, rank 1 = server stage. The batch is cut into m
+      micro-batches; activations/labels go 0 -> 1 and cut gradients 1 -> 0 by send/recv while the
+      other side computes; both sides accumulate gradients and step once per batch (= the
+      reference step at batch B).
+  Hub (N >= 3; SplitFed with N-1 client GPUs feeding ONE server GPU): each client sends its slice,
+      the server runs every slice as it arrives (accumulating its gradient), returns each client
+      its cut-gradient slice, and the clients all-reduce their 320-float gradient before stepping
+      (= the reference step at batch (N-1)*B on the concatenated inputs).
+
+All three are exactly the reference's step at their global batch (the mean loss scale 1/global is
+applied inside the cross-entropy kernel), so they share the single-process oracle. The stage
+objects only need: client.forward / backward / step / grads / bind_grads and server.compute / step /
+grads / bind_grads / log_loss (engine.ClientStage / engine.ServerStage on GPU; oracle-backed
+stages in the CPU tests).
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+CLIENT_N = 320
+SERVER_N = 110666
+
+
+def _loss_sum(values, scale, out):
+    """scale*sum(values) -> out (the stage's own kernel when it has one)."""
+    if values.device.type == "cuda":
+        from . import ops
+        ops.loss_sum(values, scale, out)
+    else:
+        out.copy_((values.double().sum() * scale).to(out.dtype).reshape(1))
+
+
+class Replicated:
+    def __init__(self, client, server, group=None, device=None):
+        self.client, self.server = client, server
+        self.group = group
+        self.world = dist.get_world_size(group)
+        dev = device if device is not None else client.grads.device
+        self.bucket = torch.zeros(CLIENT_N + SERVER_N + 1, dtype=client.grads.dtype, device=dev)
+        client.bind_grads(self.bucket[:CLIENT_N])
+        server.bind_grads(self.bucket[CLIENT_N:CLIENT_N + SERVER_N])
+        self.loss_slot = self.bucket[-1:]
+        self.global_step = 0
+
+    def step(self, x, y):
+        B = x.shape[0]
+        scale = 1.0 / (self.world * B)
+        act = self.client.forward(x)
+        cut, loss_i = self.server.compute(act, y, scale)
+        self.client.backward(cut)
+        _loss_sum(loss_i, scale, self.loss_slot)
+        dist.all_reduce(self.bucket, group=self.group)
+        self.client.step()
+        self.server.step()
+        self.server.log_loss(self.loss_slot, scale=1.0, step=self.global_step)
+        self.global_step += 1
+
+
+class Pipeline:
+    """2-rank client/server pipeline with m micro-batches. `role` is "client" or "server"."""
+
+    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None):
+        assert role in ("client", "server")
+        self.stage, self.role, self.peer, self.micro, self.group = stage, role, peer, micro, group
+        self.global_step = 0
+        self._bufs = {}
+        self.exchange_bytes = 0
+
+    def _buf(self, name, shape, dtype, device):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != device:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self._bufs[name] = t
+        return t
+
+    def client_step(self, x, y):
+        B = x.shape[0]
+        m = self.micro
+        assert B % m == 0, "batch must be divisible by the micro-batch count"
+        mb = B // m
+        c = self.stage
+        dev = x.device
+        acts = self._buf("acts", (B, 32, 26, 26), torch.float32, dev)
+        cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, dev)
+        sends, recvs = [], []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            c.forward(x[sl], out=acts[sl])
+            sends.append(dist.isend(acts[sl], self.peer, group=self.group))
+            sends.append(dist.isend(y[sl], self.peer, group=self.group))
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            recvs.append(dist.irecv(cuts[sl], self.peer, group=self.group))
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            recvs[k].wait()
+            c.backward(cuts[sl], x=x[sl], act=acts[sl], accumulate=k > 0)
+        for w in sends:
+            w.wait()
+        c.step()
+        self.exchange_bytes = 2 * acts.numel() * 4 + y.numel() * 8
+        self.global_step += 1
+
+    def server_step(self, B: int, device):
+        m = self.micro
+        mb = B // m
+        s = self.stage
+        acts = self._buf("acts", (B, 32, 26, 26), torch.float32, device)
+        labels = self._buf("labels", (B,), torch.int64, device)
+        cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, device)
+        parts = self._buf("loss_parts", (m,), torch.float32, device)
+        recvs = []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            recvs.append((dist.irecv(acts[sl], self.peer, group=self.group),
+                          dist.irecv(labels[sl], self.peer, group=self.group)))
+        sends = []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            recvs[k][0].wait()
+            recvs[k][1].wait()
+            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / B, accumulate=k > 0, cut_grad=cuts[sl])
+            _loss_sum(loss_i, 1.0 / B, parts[k:k + 1])
+            sends.append(dist.isend(cuts[sl], self.peer, group=self.group))
+        s.step()
+        s.log_loss(parts, scale=1.0, step=self.global_step)
+        for w in sends:
+            w.wait()
+        self.exchange_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.global_step += 1
+
+
+class Hub:
+    """N-1 client ranks (0..N-2) feed one server rank (N-1)."""
+
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1):
+        self.stage, self.rank, self.world = stage, rank, world
+        self.server_rank = world - 1
+        self.nclients = world - 1
+        self.client_group = client_group
+        self.micro = micro
+        self.global_step = 0
+        self._bufs = {}
+        self.exchange_bytes = 0
+
+    @property
+    def is_server(self):
+        return self.rank == self.server_rank
+
+    def _buf(self, name, shape, dtype, device):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != device:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self._bufs[name] = t
+        return t
+
+    def client_step(self, x, y):
+        c = self.stage
+        B = x.shape[0]
+        act = self._buf("act", (B, 32, 26, 26), torch.float32, x.device)
+        c.forward(x, out=act)
+        cut = self._buf("cut", (B, 32, 26, 26), torch.float32, x.device)
+        w1 = dist.isend(act, self.server_rank)
+        w2 = dist.isend(y, self.server_rank)
+        r = dist.irecv(cut, self.server_rank)
+        r.wait()
+        c.backward(cut, x=x, act=act)
+        w1.wait()
+        w2.wait()
+        if self.nclients > 1:
+            dist.all_reduce(c.grads, group=self.client_group)
+        c.step()
+        self.exchange_bytes = 2 * act.numel() * 4 + y.numel() * 8
+        self.global_step += 1
+
+    def server_step(self, B: int, device):
+        """B = per-client batch; the server step covers (N-1)*B samples."""
+        s = self.stage
+        G = self.nclients * B
+        acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
+        labels = self._buf("labels", (G,), torch.int64, device)
+        cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
+        parts = self._buf("loss_parts", (self.nclients,), torch.float32, device)
+        recvs = []
+        for c in range(self.nclients):
+            sl = slice(c * B, (c + 1) * B)
+            recvs.append((dist.irecv(acts[sl], c), dist.irecv(labels[sl], c)))
+        sends = []
+        for c in range(self.nclients):
+            sl = slice(c * B, (c + 1) * B)
+            recvs[c][0].wait()
+            recvs[c][1].wait()
+            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=c > 0, cut_grad=cuts[sl])
+            _loss_sum(loss_i, 1.0 / G, parts[c:c + 1])
+            sends.append(dist.isend(cuts[sl], c))
+        s.step()
+        s.log_loss(parts, scale=1.0, step=self.global_step)
+        for w in sends:
+            w.wait()
+        self.exchange_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.global_step += 1
+
+
+def client_group_for(world: int):
+    """The all-reduce group of the hub's client ranks (every rank must call this, in order)."""
+    if world < 3:
+        return None
+    return dist.new_group(list(range(world - 1)))
+
+
+def measure_p2p(nbytes: int, src: int, dst: int, device, iters: int = 5, group=None) -> Optional[float]:
+    """One-directional send/recv bandwidth src -> dst in GB/s (rank-local timing on dst after a
+    barrier-aligned start). Returns the value on dst, None elsewhere."""
+    rank = dist.get_rank(group)
+    n = nbytes // 4
+    t = torch.empty(n, dtype=torch.float32, device=device)
+    if rank == src:
+        t.fill_(1.0)
+    dist.barrier(group=group)
+    for it in range(iters + 1):
+        if it == 1:
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+        if rank == src:
+            dist.send(t, dst, group=group)
+        elif rank == dst:
+            dist.recv(t, src, group=group)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    dist.barrier(group=group)
+    return (iters * nbytes / dt / 1e9) if rank == dst else None

@@ -20,7 +20,9 @@ HIP graph.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Tuple
+import contextlib
+from collections import defaultdict
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -29,6 +31,41 @@ from . import ops
 from .model_def import ModelPartA, ModelPartB
 
 LR = 0.01  # optim.SGD(lr=0.01) on both sides (client_part.py:17, server_part.py:15)
+
+
+class KernelTimer:
+    """HIP-event timing of named launches on the launching (current) stream. Disabled by default;
+    bench.py enables it for its per-kernel pass. Never enable inside graph capture."""
+
+    def __init__(self):
+        self.enabled = False
+        self._ev: Dict[str, list] = defaultdict(list)
+
+    @contextlib.contextmanager
+    def __call__(self, name: str):
+        if not self.enabled:
+            yield
+            return
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        yield
+        e.record()
+        self._ev[name].append((s, e))
+
+    def reset(self):
+        self._ev.clear()
+
+    def summary(self) -> Dict[str, Dict[str, float]]:
+        torch.cuda.synchronize()
+        out = {}
+        for k, v in self._ev.items():
+            ms = [s.elapsed_time(e) for s, e in v]
+            out[k] = {"avg_ms": sum(ms) / len(ms), "min_ms": min(ms), "n": len(ms)}
+        return out
+
+
+TIMER = KernelTimer()
 
 
 def _flatten_params(params: List[nn.Parameter], device) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -100,7 +137,12 @@ class LossLog:
 
 
 class ClientStage:
-    """Client half: ModelPartA on one device + SGD (src/client_part.py:16-17,112-133)."""
+    """Client half: ModelPartA on one device + SGD (src/client_part.py:16-17,112-133).
+
+    forward(x) -> act; then either backward_step(cut_grad) (fused wgrad-slab reduce + SGD, the
+    reference's `activations.backward(grads); optimizer.step()`), or backward(cut_grad,
+    accumulate=...) into the flat gradient block followed by step() (micro-batched / all-reduced
+    topologies)."""
 
     def __init__(self, model: Optional[ModelPartA] = None, lr: float = LR, device="cuda"):
         self.device = torch.device(device)
@@ -120,38 +162,49 @@ class ClientStage:
     def b1(self):
         return self.model.conv1.bias
 
+    def bind_grads(self, view: torch.Tensor):
+        """Use `view` (320 floats, e.g. a slice of an all-reduce bucket) as the gradient block."""
+        view.copy_(self.grads)
+        self.grads = view
+        self.model.conv1.weight.grad = view[:288].view(32, 1, 3, 3)
+        self.model.conv1.bias.grad = view[288:].view(32)
+
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """act = relu(conv1(x)) (client_part.py:114). Keeps x/act for backward_step."""
+        """act = relu(conv1(x)) (client_part.py:114). Keeps x/act for the backward."""
         B = x.shape[0]
         act = out if out is not None else self._buf.get("act", (B, 32, 26, 26), torch.float32, self.device)
-        ops.conv1_fwd(x, self.W1.detach(), self.b1.detach(), out=act)
+        with TIMER("conv1_fwd"):
+            ops.conv1_fwd(x, self.W1.detach(), self.b1.detach(), out=act)
         self._x, self._act = x, act
         return act
+
+    def _slabs(self, cut_grad, x, act, tag="slabs"):
+        x = self._x if x is None else x
+        act = self._act if act is None else act
+        B = x.shape[0]
+        slabs = self._buf.get(tag, (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
+        with TIMER("conv1_wgrad"):
+            ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
+        return slabs
 
     def backward_step(self, cut_grad: torch.Tensor, x: Optional[torch.Tensor] = None,
                       act: Optional[torch.Tensor] = None) -> None:
         """act.backward(cut_grad); optimizer.step() (client_part.py:132-133): relu-bwd + conv1
-        wgrad slabs, then one fused reduce+SGD launch over the 320 client parameters."""
-        x = self._x if x is None else x
-        act = self._act if act is None else act
-        B = x.shape[0]
-        slabs = self._buf.get("slabs", (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
-        ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
-        self.apply_grad_slabs(slabs)
+        wgrad slabs, then ONE fused reduce+SGD launch over the 320 client parameters."""
+        slabs = self._slabs(cut_grad, x, act)
+        with TIMER("sgd_client"):
+            ops.sgd_from_slabs(self.params, self.grads, slabs, self.lr)
 
-    def wgrad_slabs(self, cut_grad, x=None, act=None):
-        x = self._x if x is None else x
-        act = self._act if act is None else act
-        B = x.shape[0]
-        slabs = self._buf.get("slabs", (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
-        return ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
+    def backward(self, cut_grad: torch.Tensor, x: Optional[torch.Tensor] = None,
+                 act: Optional[torch.Tensor] = None, accumulate: bool = False) -> None:
+        """Weight gradient into self.grads (accumulate=True adds: micro-batches)."""
+        slabs = self._slabs(cut_grad, x, act)
+        ops.reduce_slabs(slabs, out=self.grads, accumulate=accumulate)
 
-    def apply_grad_slabs(self, slabs):
-        ops.sgd_from_slabs(self.params, self.grads, slabs, self.lr)
-
-    def apply_grad(self):
+    def step(self):
         """SGD from the (already reduced / all-reduced) flat gradient block."""
-        ops.sgd(self.params, self.grads, self.lr)
+        with TIMER("sgd_client"):
+            ops.sgd(self.params, self.grads, self.lr)
 
 
 class ServerStage:
@@ -169,6 +222,15 @@ class ServerStage:
         self.err_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._buf = _Buffers()
 
+    def bind_grads(self, view: torch.Tensor):
+        view.copy_(self.grads)
+        self.grads = view
+        m = self.model
+        m.conv2.weight.grad = view[:18432].view(64, 32, 3, 3)
+        m.conv2.bias.grad = view[18432:18496].view(64)
+        m.fc1.weight.grad = view[18496:110656].view(10, 9216)
+        m.fc1.bias.grad = view[110656:].view(10)
+
     def _b(self, name, shape, dtype=torch.float32):
         return self._buf.get(name, shape, dtype, self.device)
 
@@ -180,46 +242,62 @@ class ServerStage:
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
         W3, b3 = m.fc1.weight.detach(), m.fc1.bias.detach()
-        pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
-                                          code=self._b("code", (B, 64, 12, 12), torch.uint8))
-        _, loss_i, dlogits, dpooled = ops.fc_xent(
-            pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
-            loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
-            dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag)
+        with TIMER("conv2_fwd_pool"):
+            pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
+                                              code=self._b("code", (B, 64, 12, 12), torch.uint8))
+        with TIMER("fc_xent"):
+            _, loss_i, dlogits, dpooled = ops.fc_xent(
+                pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
+                loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
+                dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag)
         if cut_grad is None:
             cut_grad = self._b("cut_grad", (B, 32, 26, 26))
-        ops.conv2_dgrad(dpooled, code, W2, out=cut_grad)
-        s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
-                                   slabs=self._b("s2", (ops.conv2_wgrad_nslab(B), ops.CONV2_SLAB)))
-        s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+        with TIMER("conv2_dgrad"):
+            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad)
+        with TIMER("conv2_wgrad"):
+            s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
+                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B), ops.CONV2_SLAB)))
+        with TIMER("fc_wgrad"):
+            s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3
 
     def apply_grad_slabs(self, s2, s3):
         """optimizer.step() (server_part.py:52): two fused reduce+SGD launches, one per slab kind."""
-        ops.sgd_from_slabs(self.params[:ops.CONV2_SLAB], self.grads[:ops.CONV2_SLAB], s2, self.lr)
-        ops.sgd_from_slabs(self.params[ops.CONV2_SLAB:], self.grads[ops.CONV2_SLAB:], s3, self.lr)
+        with TIMER("sgd_server"):
+            ops.sgd_from_slabs(self.params[:ops.CONV2_SLAB], self.grads[:ops.CONV2_SLAB], s2, self.lr)
+            ops.sgd_from_slabs(self.params[ops.CONV2_SLAB:], self.grads[ops.CONV2_SLAB:], s3, self.lr)
 
-    def apply_grad(self):
-        ops.sgd(self.params, self.grads, self.lr)
+    def reduce_grads(self, s2, s3, accumulate: bool = False):
+        """Reduce slabs into the flat gradient block without stepping (micro-batches, all-reduce)."""
+        ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB], accumulate=accumulate)
+        ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:], accumulate=accumulate)
 
-    def reduce_grads(self, s2, s3):
-        """Reduce slabs into the flat gradient block without stepping (for all-reduce topologies)."""
-        ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB])
-        ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:])
+    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None):
+        """forward_backward + reduce into self.grads; returns (cut_grad, loss_i)."""
+        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, grad_scale, cut_grad=cut_grad)
+        self.reduce_grads(s2, s3, accumulate=accumulate)
+        return cut_grad, loss_i
 
-    def log_loss(self, loss_i, step: Optional[int] = None):
-        ops.loss_log(loss_i, self.loss_log.ring, self.loss_log.counter)
+    def step(self):
+        with TIMER("sgd_server"):
+            ops.sgd(self.params, self.grads, self.lr)
+
+    def log_loss(self, values, scale: Optional[float] = None, step: Optional[int] = None):
+        """Log scale*sum(values) (default: the mean of per-sample losses) for `step`."""
+        scale = 1.0 / values.numel() if scale is None else scale
+        with TIMER("loss_log"):
+            ops.loss_log(values, scale, self.loss_log.ring, self.loss_log.counter)
         if step is not None:
             self.loss_log.note_step(step)
 
-    def step(self, act: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
-             cut_grad: Optional[torch.Tensor] = None):
-        """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i).
-        The mean loss for `step` lands in the device loss log."""
+    def step_request(self, act: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
+                     cut_grad: Optional[torch.Tensor] = None):
+        """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i). The mean
+        loss for `step` lands in the device loss log."""
         B = act.shape[0]
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad)
         self.apply_grad_slabs(s2, s3)
-        self.log_loss(loss_i, step)
+        self.log_loss(loss_i, step=step)
         return cut_grad, loss_i
 
     def check_labels(self):
@@ -250,7 +328,7 @@ class SplitTrainer:
 
     def _eager(self, x, y):
         act = self.client.forward(x)
-        cut_grad, _ = self.server.step(act, y)
+        cut_grad, _ = self.server.step_request(act, y)
         self.client.backward_step(cut_grad)
 
     def static_inputs(self, B: int):

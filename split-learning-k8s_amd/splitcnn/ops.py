@@ -179,10 +179,12 @@ def conv2_wgrad_slabs(act, dpooled, code, slabs=None):
 
 
 # ------------------------------------------------------------------------------------ reductions
-def reduce_slabs(slabs, out=None):
+def reduce_slabs(slabs, out=None, accumulate=False):
+    """out (+)= sum over slabs (fixed order)."""
     nslab, n = slabs.shape
     out = _out(out, (n,), slabs, name="out")
-    _lib.call("slk_reduce_slabs", _dev(slabs, "slabs"), nslab, n, _dev(out, "out"), _stream(slabs))
+    _lib.call("slk_reduce_slabs", _dev(slabs, "slabs"), nslab, n, _dev(out, "out"), int(bool(accumulate)),
+              _stream(slabs))
     return out
 
 
@@ -201,17 +203,21 @@ def sgd(param, grad, lr):
               _stream(param))
 
 
-def loss_mean(loss_i, out=None, slot=0):
-    B = loss_i.numel()
-    out = _out(out, (1,), loss_i, name="out") if out is None else out
+def loss_sum(values, scale, out=None):
+    """out[0] = scale * sum(values) (fixed order); out may be a 1-element view of a bigger buffer."""
+    n = values.numel()
+    if out is None:
+        out = torch.empty(1, dtype=_F32, device=values.device)
     _dev(out, "out")
-    if not (0 <= slot < out.numel()):
-        raise IndexError("loss_mean slot out of range")
-    _lib.call("slk_loss_mean", _dev(loss_i, "loss_i"), B, out.data_ptr(), int(slot), _stream(loss_i))
+    _lib.call("slk_loss_sum", _dev(values, "values"), n, float(scale), out.data_ptr(), _stream(values))
     return out
 
 
-def loss_log(loss_i, ring, counter):
-    B = loss_i.numel()
-    _lib.call("slk_loss_log", _dev(loss_i, "loss_i"), B, _dev(ring, "ring"), ring.numel(),
-              _dev(counter, "counter", (1,), torch.int32), _stream(loss_i))
+def loss_mean(loss_i, out=None):
+    return loss_sum(loss_i, 1.0 / loss_i.numel(), out)
+
+
+def loss_log(values, scale, ring, counter):
+    n = values.numel()
+    _lib.call("slk_loss_log", _dev(values, "values"), n, float(scale), _dev(ring, "ring"), ring.numel(),
+              _dev(counter, "counter", (1,), torch.int32), _stream(values))

@@ -29,6 +29,9 @@ def rel_err(got, want):
     """max |got - want| / max |want| (norm-free, elementwise worst case scaled by the tensor's range)."""
     got = np.asarray(got, dtype=np.float64)
     want = np.asarray(want, dtype=np.float64)
+    if got.shape != want.shape and got.size == want.size:
+        got = got.reshape(want.shape)
+    assert got.shape == want.shape, (got.shape, want.shape)
     scale = max(np.abs(want).max(), 1e-30)
     return float(np.abs(got - want).max() / scale)
 

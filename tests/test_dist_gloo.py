@@ -1,0 +1,113 @@
+"""Multi-rank protocols of splitcnn/dist.py on the CPU (gloo), driven with oracle-backed stages:
+after two steps every topology must equal the single-process reference step at its global batch
+(Replicated: N*B concatenated; Pipeline: B in micro-batches; Hub: (N-1)*B concatenated)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT, load_fixture
+
+B = 4
+STEPS = 2
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init_params():
+    fx = load_fixture("split_step_b4.npz")
+    return {k: fx["init_" + k].astype(np.float64) for k in ["W1", "b1", "W2", "b2", "W3", "b3"]}
+
+
+def _batches(n_samples):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from splitcnn.data import SyntheticMNIST
+    d = SyntheticMNIST(9)
+    return [d.batch(n_samples) for _ in range(STEPS)]
+
+
+def _worker(rank, world, port, topo, outdir):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from oracle.stages import OracleClient, OracleServer
+    from splitcnn import dist as sd
+    P = _init_params()
+    try:
+        if topo == "replicated":
+            batches = _batches(world * B)
+            t = sd.Replicated(OracleClient(P), OracleServer(P), device=torch.device("cpu"))
+            for x, y in batches:
+                sl = slice(rank * B, (rank + 1) * B)
+                t.step(x[sl].contiguous(), y[sl].contiguous())
+            res = {**t.client.named(), **t.server.named(), "losses": [l for _, l in t.server.losses]}
+        elif topo == "pipeline":
+            batches = _batches(B)
+            if rank == 0:
+                t = sd.Pipeline(OracleClient(P), "client", 1, micro=2)
+                for x, y in batches:
+                    t.client_step(x, y)
+                res = t.stage.named()
+            else:
+                t = sd.Pipeline(OracleServer(P), "server", 0, micro=2)
+                for _ in batches:
+                    t.server_step(B, torch.device("cpu"))
+                res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
+        elif topo == "hub":
+            batches = _batches((world - 1) * B)
+            grp = sd.client_group_for(world)
+            if rank < world - 1:
+                t = sd.Hub(OracleClient(P), rank, world, client_group=grp)
+                for x, y in batches:
+                    sl = slice(rank * B, (rank + 1) * B)
+                    t.client_step(x[sl].contiguous(), y[sl].contiguous())
+                res = t.stage.named()
+            else:
+                t = sd.Hub(OracleServer(P), rank, world, client_group=grp)
+                for _ in batches:
+                    t.server_step(B, torch.device("cpu"))
+                res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), **{k: np.asarray(v) for k, v in res.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def _reference(global_batch):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from oracle.split_step import split_step
+    P = _init_params()
+    losses = []
+    for x, y in _batches(global_batch):
+        P, rec = split_step(P, x.numpy(), y.numpy())
+        losses.append(rec["loss"])
+    return P, losses
+
+
+@pytest.mark.parametrize("topo,world,gb", [("replicated", 2, 2 * B), ("pipeline", 2, B), ("hub", 3, 2 * B)])
+def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
+    mp.spawn(_worker, args=(world, _port(), topo, str(tmp_path)), nprocs=world, join=True)
+    P, losses = _reference(gb)
+    outs = [dict(np.load(tmp_path / f"r{r}.npz")) for r in range(world)]
+    client_ranks = range(world) if topo == "replicated" else range(world - 1)
+    server_ranks = range(world) if topo == "replicated" else [world - 1]
+    for r in client_ranks:
+        for k in ["W1", "b1"]:
+            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
+    for r in server_ranks:
+        for k in ["W2", "b2", "W3", "b3"]:
+            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
+        np.testing.assert_allclose(outs[r]["losses"], losses, rtol=1e-6)
