@@ -6,22 +6,38 @@
 // summed (fixed order, bit-stable) in the same pass that applies the update.
 #include "slk_common.h"
 
-__global__ __launch_bounds__(256) void sgd_from_slabs_kernel(float* __restrict__ param,
-                                                             float* __restrict__ grad,
-                                                             const float* __restrict__ slabs,
-                                                             int nslab, int n, float lr, int acc) {
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        float g = acc ? grad[i] : 0.f;
+// Deterministic slab reduction (+ optional SGD). A 1024-thread block owns 64 columns; wave w sums
+// slabs w, w+16, w+32, ... of those columns in order (8 loads in flight), then wave 0 adds the 16
+// partials in wave order. The result is a fixed function of the inputs (no atomics).
+constexpr int RS_WAVES = 16;
+__global__ __launch_bounds__(1024) void sgd_from_slabs_kernel(float* __restrict__ param,
+                                                              float* __restrict__ grad,
+                                                              const float* __restrict__ slabs,
+                                                              int nslab, int n, float lr, int acc) {
+    __shared__ float part[RS_WAVES][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    float g = 0.f;
+    if (i < n) {
         const float* s = slabs + i;
-        int k = 0;
-        for (; k + 4 <= nslab; k += 4) {  // 4 loads in flight, summed in slab order
-            const float a0 = s[(size_t)k * n], a1 = s[(size_t)(k + 1) * n];
-            const float a2 = s[(size_t)(k + 2) * n], a3 = s[(size_t)(k + 3) * n];
-            g += a0; g += a1; g += a2; g += a3;
+        int k = wave;
+        for (; k + 7 * RS_WAVES < nslab; k += 8 * RS_WAVES) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(k + u * RS_WAVES) * n];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g += v[u];
         }
-        for (; k < nslab; ++k) g += s[(size_t)k * n];
-        if (grad) grad[i] = g;
-        if (param) param[i] = param[i] - lr * g;
+        for (; k < nslab; k += RS_WAVES) g += s[(size_t)k * n];
+    }
+    part[wave][lane] = g;
+    __syncthreads();
+    if (wave == 0 && i < n) {
+        float t = acc ? grad[i] : 0.f;
+#pragma unroll
+        for (int w = 0; w < RS_WAVES; ++w) t += part[w][lane];
+        if (grad) grad[i] = t;
+        if (param) param[i] = param[i] - lr * t;
     }
 }
 
@@ -68,8 +84,8 @@ extern "C" int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out
     SLK_CHECK_ARG(nslab >= 0 && n >= 0);
     if (n == 0) return 0;
     SLK_CHECK_ARG(out && (slabs || nslab == 0));
-    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(nullptr, out, slabs, nslab, n, 0.f,
-                                                                        accumulate ? 1 : 0);
+    sgd_from_slabs_kernel<<<(n + 63) / 64, 1024, 0, slk_stream(stream)>>>(nullptr, out, slabs, nslab, n, 0.f,
+                                                                           accumulate ? 1 : 0);
     return slk_launch_status();
 }
 
@@ -78,7 +94,7 @@ extern "C" int slk_sgd_from_slabs(float* param, float* grad, const float* slabs,
     SLK_CHECK_ARG(nslab >= 0 && n >= 0);
     if (n == 0) return 0;
     SLK_CHECK_ARG(param && (slabs || nslab == 0));
-    sgd_from_slabs_kernel<<<grid_for(n), 256, 0, slk_stream(stream)>>>(param, grad, slabs, nslab, n, lr, 0);
+    sgd_from_slabs_kernel<<<(n + 63) / 64, 1024, 0, slk_stream(stream)>>>(param, grad, slabs, nslab, n, lr, 0);
     return slk_launch_status();
 }
 

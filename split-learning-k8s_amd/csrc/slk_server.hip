@@ -20,216 +20,274 @@
 using namespace slk;
 
 // ============================================================================ conv2 forward + pool
-// One workgroup per sample, 6 waves. The sample's K = 288 is processed as two channel halves
-// (ci 0-15, 16-31) so LDS = 16x676 image + 72x2x64 weights = 80,128 B -> two workgroups per CU, one
-// staging while the other computes.
-// K order inside a half: step s = tap*8 + ci_lo (72 steps), lane half h picks ci = 16*hc + ci_lo + 8h.
-// Pixel tile = 32 pixels = 8 pooling windows x 4 (window-major), so after the MFMA each lane holds
-// the 4 pixels of a pooling window in 4 consecutive accumulator registers: pooling is in-register.
-constexpr int C2F_WAVES = 6;
+// Persistent: one 12-wave workgroup per CU walks samples blockIdx.x, +gridDim.x, ...
+// LDS (160,256 B of the CU's 163,840): W2 resident for the whole launch as [half][s][h][co]
+// (73,728 B, loaded once) + the sample image double-buffered by channel halves (2 x 43,264 B). The
+// next half is fetched by LDS-DMA (global_load_lds_dwordx4) while the current half is on the MFMAs;
+// the end-of-half barrier retires it.
+// K order inside a half: step s = tap*8 + ci_lo (72 steps), MFMA lane half h picks ci = 16*hc +
+// ci_lo + 8h, so both halves of a 32x32x2 MFMA read with one base register + immediate offsets.
+// Pixel tile = 32 pixels = 8 pooling windows x 4; MFMA row i = q + 8g + 4hq (the C/D layout's row
+// order) holds window 4hq + g, position q. After the MFMAs a lane (col = co, half h) therefore owns
+// the 4 pixels of windows 8p+4h .. 8p+4h+3 in its 16 accumulators: bias, ReLU and the 2x2 max-pool
+// are in-register and pooled/code leave as one float4 / one u32 per lane and tile.
+// Work split: 18 pixel tiles x 2 co tiles = 36 tasks per sample; wave w owns co tile (w & 1) and
+// pixel tiles 3*(w >> 1) + {0, 1, 2}.
+constexpr int C2F_WAVES = 12;
 constexpr int C2F_THREADS = C2F_WAVES * 64;
-constexpr int C2F_IMG = 16 * A_PIX;        // 10816 floats
-constexpr int C2F_W = 72 * 2 * 64;         // 9216 floats
-constexpr int C2F_TILES_PER_WAVE = 6;      // 18 pixel tiles x 2 co tiles / 6 waves
+constexpr int C2F_IMG = 16 * A_PIX;        // 10816 floats = 43,264 B per channel half
+constexpr int C2F_WH = 72 * 2 * 64;        // 9216 floats per half
+constexpr int C2F_TPW = 3;                 // pixel tiles per wave
+constexpr int C2F_GRID = 256;              // one workgroup per CU (MI355X)
+constexpr int C2F_CHUNKS = (C2F_IMG * 4 + 1023) / 1024;  // 43 x 1 KiB LDS-DMA pieces per half
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void c2f_dma_half(const float* __restrict__ src, float* dst, int wave, int lane) {
+    // one wave-instruction moves 1 KiB: lane l copies bytes [16l, 16l+16) of the piece
+    const char* s = reinterpret_cast<const char*>(src);
+    char* d = reinterpret_cast<char*>(dst);
+    for (int c = wave; c < C2F_CHUNKS; c += C2F_WAVES) {
+        const int off = c * 1024 + lane * 16;
+        if (off < C2F_IMG * 4)
+            __builtin_amdgcn_global_load_lds((const void*)(s + off), (lds_ptr_t)(d + c * 1024), 16, 0, 0);
+    }
+}
 
 __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
     const float* __restrict__ act, const float* __restrict__ W2, const float* __restrict__ b2,
-    float* __restrict__ pooled, uint8_t* __restrict__ code) {
-    __shared__ __attribute__((aligned(16))) float smem[C2F_IMG + C2F_W];
-    float* img = smem;
-    float* w2s = smem + C2F_IMG;
+    float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * C2F_WH + 2 * C2F_IMG];
+    float* w2s = smem;                    // [hc][s][h][co]
+    float* imgb = smem + 2 * C2F_WH;      // [2][16][676]
 
-    const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, j = lane & 31;
-    const int ct = wave & 1;                       // co tile (32 channels)
-    const int pt0 = (wave >> 1) * C2F_TILES_PER_WAVE;  // first pixel tile of this wave
+    const int ct = wave & 1;
+    const int pt0 = (wave >> 1) * C2F_TPW;
 
-    int pbase[C2F_TILES_PER_WAVE];
+    int pbase[C2F_TPW];
 #pragma unroll
-    for (int t = 0; t < C2F_TILES_PER_WAVE; ++t) {
-        const int win = 8 * (pt0 + t) + (j >> 2);
+    for (int t = 0; t < C2F_TPW; ++t) {
+        const int g = j >> 3, hq = (j >> 2) & 1, q = j & 3;
+        const int win = 8 * (pt0 + t) + 4 * hq + g;
         const int py = win / P_HW, px = win - (win / P_HW) * P_HW;
-        const int q = j & 3;
         const int oy = 2 * py + (q >> 1), ox = 2 * px + (q & 1);
         pbase[t] = h * 8 * A_PIX + oy * A_HW + ox;
     }
-    f32x16 acc[C2F_TILES_PER_WAVE];
-#pragma unroll
-    for (int t = 0; t < C2F_TILES_PER_WAVE; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-    const float* ab = act + (size_t)b * A_SAMPLE;
-#pragma unroll 1
-    for (int hc = 0; hc < 2; ++hc) {
-        if (hc) __syncthreads();
-        // image half: contiguous 16 x 676 floats
-        const float4* src = reinterpret_cast<const float4*>(ab + hc * C2F_IMG);
-        for (int i = tid; i < C2F_IMG / 4; i += C2F_THREADS) reinterpret_cast<float4*>(img)[i] = src[i];
-        // weight half, re-laid as [s][h][co]
-        for (int e = tid; e < C2 * 144; e += C2F_THREADS) {
-            const int co = e / 144, r = e - co * 144;
-            const int ci_l = r / 9, tap = r - ci_l * 9;
-            const int s = tap * 8 + (ci_l & 7);
-            w2s[(s * 2 + (ci_l >> 3)) * 64 + co] = W2[co * K2 + hc * 144 + r];
-        }
-        __syncthreads();
-        const float* wl = w2s + h * 64 + ct * 32 + j;
-#pragma unroll 1
-        for (int tap = 0; tap < 9; ++tap) {
-            const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-            const int toff = ky * A_HW + kx;
-            int tb[C2F_TILES_PER_WAVE];
-#pragma unroll
-            for (int t = 0; t < C2F_TILES_PER_WAVE; ++t) tb[t] = pbase[t] + toff;
-            const float* wt = wl + tap * 8 * 128;
-#pragma unroll
-            for (int ci_lo = 0; ci_lo < 8; ++ci_lo) {
-                const float bv = wt[ci_lo * 128];
-#pragma unroll
-                for (int t = 0; t < C2F_TILES_PER_WAVE; ++t)
-                    acc[t] = mfma32x32x2(img[tb[t] + ci_lo * A_PIX], bv, acc[t]);
-            }
-        }
-    }
-
-    // epilogue: bias + ReLU + 2x2 max-pool (torch CPU order: scan q = 0..3, strict >, first max
-    // wins), staged through LDS for coalesced stores.
-    __syncthreads();
-    float* pl = smem;                                         // [64][144] f32
-    uint8_t* cl = reinterpret_cast<uint8_t*>(smem + P_SAMPLE);  // [64][144] u8
     const int co = ct * 32 + j;
     const float bias = b2[co];
-#pragma unroll
-    for (int t = 0; t < C2F_TILES_PER_WAVE; ++t) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            float m = -__builtin_inff();
-            int idx = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float v = acc[t][4 * g + q] + bias;
-                v = v > 0.f ? v : 0.f;
-                if (v > m) { m = v; idx = q; }
-            }
-            const int win = 8 * (pt0 + t) + 2 * g + h;
-            pl[co * P_WIN + win] = m;
-            cl[co * P_WIN + win] = (uint8_t)(m > 0.f ? idx : CODE_NONE);
-        }
+
+    int b = blockIdx.x;
+    if (b < B) c2f_dma_half(act + (size_t)b * A_SAMPLE, imgb, wave, lane);
+    // W2, once: natural [co][ci][tap] -> [hc][s = tap*8 + (ci_l & 7)][h = ci_l >> 3][co]
+    for (int e = tid; e < W2_N; e += C2F_THREADS) {
+        const int c = e / K2, r = e - c * K2;
+        const int ci = r / 9, tap = r - ci * 9;
+        const int hc = ci >> 4, ci_l = ci & 15;
+        w2s[hc * C2F_WH + ((tap * 8 + (ci_l & 7)) * 2 + (ci_l >> 3)) * 64 + c] = W2[e];
     }
     __syncthreads();
-    float4* pout = reinterpret_cast<float4*>(pooled + (size_t)b * P_SAMPLE);
-    for (int i = tid; i < P_SAMPLE / 4; i += C2F_THREADS) pout[i] = reinterpret_cast<const float4*>(pl)[i];
-    uint4* cout = reinterpret_cast<uint4*>(code + (size_t)b * P_SAMPLE);
-    for (int i = tid; i < P_SAMPLE / 16; i += C2F_THREADS) cout[i] = reinterpret_cast<const uint4*>(cl)[i];
+
+    int buf = 0;
+#pragma unroll 1
+    for (; b < B; b += gridDim.x) {
+        f32x16 acc[C2F_TPW];
+#pragma unroll
+        for (int t = 0; t < C2F_TPW; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll 1
+        for (int hc = 0; hc < 2; ++hc) {
+            // prefetch the next half (this sample's second half, or the next sample's first)
+            const int nb = hc ? b + gridDim.x : b;
+            if (nb < B) c2f_dma_half(act + (size_t)nb * A_SAMPLE + (hc ? 0 : C2F_IMG), imgb + (buf ^ 1) * C2F_IMG,
+                                     wave, lane);
+            const float* img = imgb + buf * C2F_IMG;
+            const float* wl = w2s + hc * C2F_WH + h * 64 + ct * 32 + j;
+#pragma unroll 1
+            for (int tap = 0; tap < 9; ++tap) {
+                const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+                const int toff = ky * A_HW + kx;
+                int tb[C2F_TPW];
+#pragma unroll
+                for (int t = 0; t < C2F_TPW; ++t) tb[t] = pbase[t] + toff;
+                const float* wt = wl + tap * 8 * 128;
+#pragma unroll
+                for (int ci_lo = 0; ci_lo < 8; ++ci_lo) {
+                    const float bv = wt[ci_lo * 128];
+#pragma unroll
+                    for (int t = 0; t < C2F_TPW; ++t)
+                        acc[t] = mfma32x32x2(img[tb[t] + ci_lo * A_PIX], bv, acc[t]);
+                }
+            }
+            __syncthreads();  // all reads of `buf` done; the prefetch into buf^1 has landed
+            buf ^= 1;
+        }
+        // epilogue: bias + ReLU + 2x2 max-pool (torch CPU: scan q = 0..3, strict >, first max wins)
+        float* prow = pooled + (size_t)b * P_SAMPLE + co * P_WIN;
+        uint8_t* crow = code + (size_t)b * P_SAMPLE + co * P_WIN;
+#pragma unroll
+        for (int t = 0; t < C2F_TPW; ++t) {
+            float m4[4];
+            unsigned int c4 = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float m = -__builtin_inff();
+                int idx = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float v = acc[t][4 * g + q] + bias;
+                    v = v > 0.f ? v : 0.f;
+                    if (v > m) { m = v; idx = q; }
+                }
+                m4[g] = m;
+                c4 |= (unsigned int)(m > 0.f ? idx : CODE_NONE) << (8 * g);
+            }
+            const int w0 = 8 * (pt0 + t) + 4 * h;
+            *reinterpret_cast<float4*>(prow + w0) = make_float4(m4[0], m4[1], m4[2], m4[3]);
+            *reinterpret_cast<unsigned int*>(crow + w0) = c4;
+        }
+    }
 }
 
 // ============================================================================ conv2 dgrad (cut grad)
-// g[ci][y][x] = sum_{co,ky,kx} dc[co][y-ky][x-kx] * W2[co][ci][ky][kx], dc = maxpool/relu-routed
-// dpooled. One workgroup per sample, 8 waves, K = 576 in 4 chunks of 16 output channels.
-// LDS: dc chunk expanded to a zero-bordered 28x28 plane per channel (16 x 784 floats) + the W2 chunk
-// as [s][h][ci] (72 x 2 x 32) = 68,608 B -> two workgroups per CU.
-// MFMA roles: A = W2 (rows ci, one 32-row tile), B = dc-im2col (cols = 32 consecutive pixels), so
-// each lane's accumulator column is one pixel and the stores are 128-B coalesced rows of cut_grad.
-constexpr int C2D_WAVES = 8;
+// g[ci][y][x] = sum_{co,ky,kx} dc[co][y-ky][x-kx] * W2[co][ci][ky][kx], dc = max-pool/ReLU-routed
+// dpooled (routing code from the forward). Persistent: one 12-wave workgroup per CU.
+// LDS: W2 resident as [chunk(8)][s(36)][h][ci] (73,728 B) + dc for 8 output channels expanded into
+// zero-bordered 28x28 planes, double-buffered (2 x 25,088 B). K = 576 runs as 8 chunks of 8 channels;
+// the next chunk's dpooled/code are loaded into registers before the current chunk's MFMAs and
+// written (expanded) into the other buffer after them: one barrier per chunk.
+// MFMA roles: A = W2 (rows ci: one 32-row tile), B = dc-im2col (cols = 32 consecutive output
+// pixels), k step s = co_lo*9 + tap with lane half h picking channel co_lo + 4h; every operand read
+// is a ds_read_b32 with a per-lane base and an immediate offset. Each lane's accumulator column is
+// one pixel, so cut_grad leaves in 128-B coalesced rows. 22 pixel tiles (676 -> 704) per sample.
+constexpr int C2D_WAVES = 12;
 constexpr int C2D_THREADS = C2D_WAVES * 64;
 constexpr int C2D_PLANE = 28 * 28;
-constexpr int C2D_DC = 16 * C2D_PLANE;     // 12544 floats
-constexpr int C2D_W = 72 * 2 * 32;         // 4608 floats
-constexpr int C2D_NTILE = 22;              // ceil(676 / 32)
+constexpr int C2D_CO = 8;                        // output channels per chunk
+constexpr int C2D_NCHUNK = C2 / C2D_CO;          // 8
+constexpr int C2D_DC = C2D_CO * C2D_PLANE;       // 6272 floats per buffer
+constexpr int C2D_WC = 36 * 2 * 32;              // 2304 floats of W2 per chunk
+constexpr int C2D_NTILE = 22;                    // ceil(676 / 32)
+constexpr int C2D_GRID = 256;
+constexpr int C2D_STG = (C2D_CO * P_WIN + C2D_THREADS - 1) / C2D_THREADS;  // 2 windows / thread
 
 template <int NT>
-__device__ __forceinline__ void c2d_chunk(const float* __restrict__ dcp, const float* __restrict__ w2d,
-                                          const int (&pbase)[3], f32x16 (&acc)[3], int h, int j) {
-    const float* wl = w2d + h * 32 + j;
-#pragma unroll 1
-    for (int co_lo = 0; co_lo < 8; ++co_lo) {
-        int cb[NT];
+__device__ __forceinline__ void c2d_chunk(const float* __restrict__ dcp, const float* __restrict__ wc,
+                                          const int (&pbase)[2], f32x16 (&acc)[2]) {
 #pragma unroll
-        for (int i = 0; i < NT; ++i) cb[i] = pbase[i] + co_lo * C2D_PLANE;
-        const float* wc = wl + co_lo * 9 * 64;
+    for (int co_lo = 0; co_lo < 4; ++co_lo) {
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int ky = tap / 3, kx = tap % 3;
-            const float av = wc[tap * 64];
-            const int imm = (2 - ky) * 28 + (2 - kx);
+            const float av = wc[(co_lo * 9 + tap) * 64];
+            const int imm = co_lo * C2D_PLANE + (2 - ky) * 28 + (2 - kx);
 #pragma unroll
-            for (int i = 0; i < NT; ++i) acc[i] = mfma32x32x2(av, dcp[cb[i] + imm], acc[i]);
+            for (int i = 0; i < NT; ++i) acc[i] = mfma32x32x2(av, dcp[pbase[i] + imm], acc[i]);
         }
     }
 }
 
-__global__ __launch_bounds__(C2D_THREADS, 4) void conv2_dgrad_kernel(
+__global__ __launch_bounds__(C2D_THREADS, 3) void conv2_dgrad_kernel(
     const float* __restrict__ dpool, const uint8_t* __restrict__ code, const float* __restrict__ W2,
-    float* __restrict__ gcut) {
-    __shared__ __attribute__((aligned(16))) float smem[C2D_DC + C2D_W];
-    float* dcp = smem;
-    float* w2d = smem + C2D_DC;
+    float* __restrict__ gcut, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[C2D_NCHUNK * C2D_WC + 2 * C2D_DC];
+    float* w2d = smem;
+    float* dcb = smem + C2D_NCHUNK * C2D_WC;
 
-    const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, j = lane & 31;
-    const int nt = (wave < C2D_NTILE - 2 * C2D_WAVES) ? 3 : 2;  // waves 0-5: 3 tiles, 6-7: 2
-
-    int pbase[3];
-    int pix[3];
+    // waves 0-9: tiles {w, w+12}; waves 10, 11: tile {w} (22 tiles)
+    const int nt = (wave + C2D_WAVES < C2D_NTILE) ? 2 : 1;
+    int pbase[2], pix[2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int p = 32 * (wave + C2D_WAVES * i) + j;
         pix[i] = p;
         const int pc = p < A_PIX ? p : A_PIX - 1;
         const int y = pc / A_HW, x = pc - (pc / A_HW) * A_HW;
-        pbase[i] = h * 8 * C2D_PLANE + y * 28 + x;
+        pbase[i] = h * 4 * C2D_PLANE + y * 28 + x;
     }
-    f32x16 acc[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 
-    // zero the planes once: the 2-wide border stays zero, the interior is rewritten per chunk
-    for (int i = tid; i < C2D_DC / 4; i += C2D_THREADS)
-        reinterpret_cast<float4*>(dcp)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // W2 once: [co][ci][tap] -> [chunk = co/8][s = (co%4)*9 + tap][h = (co%8)/4][ci]
+    for (int e = tid; e < W2_N; e += C2D_THREADS) {
+        const int c = e / K2, r = e - c * K2;
+        const int ci = r / 9, tap = r - ci * 9;
+        const int cl = c & 7;
+        w2d[(c >> 3) * C2D_WC + (((cl & 3) * 9 + tap) * 2 + (cl >> 2)) * 32 + ci] = W2[e];
+    }
+    for (int i = tid; i < 2 * C2D_DC / 4; i += C2D_THREADS)
+        reinterpret_cast<float4*>(dcb)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-    const float* dpb = dpool + (size_t)b * P_SAMPLE;
-    const uint8_t* cb = code + (size_t)b * P_SAMPLE;
+    // staging registers: window e = tid + 768*i of the chunk (e < 1152): channel e / 144
+    float sv[C2D_STG];
+    int sc[C2D_STG];
+    auto load_chunk = [&](int bb, int ch) {
+#pragma unroll
+        for (int i = 0; i < C2D_STG; ++i) {
+            const int e = tid + C2D_THREADS * i;
+            if (e < C2D_CO * P_WIN && bb < B) {
+                const size_t gi = (size_t)bb * P_SAMPLE + ch * C2D_CO * P_WIN + e;
+                sv[i] = dpool[gi];
+                sc[i] = code[gi];
+            }
+        }
+    };
+    auto write_chunk = [&](float* dst) {
+#pragma unroll
+        for (int i = 0; i < C2D_STG; ++i) {
+            const int e = tid + C2D_THREADS * i;
+            if (e < C2D_CO * P_WIN) {
+                const int col = e / P_WIN, win = e - col * P_WIN;
+                const int py = win / P_HW, px = win - (win / P_HW) * P_HW;
+                const float v = sv[i];
+                const int cd = sc[i];
+                float* d = dst + col * C2D_PLANE + (2 * py + 2) * 28 + 2 * px + 2;
+                *reinterpret_cast<float2*>(d) = make_float2(cd == 0 ? v : 0.f, cd == 1 ? v : 0.f);
+                *reinterpret_cast<float2*>(d + 28) = make_float2(cd == 2 ? v : 0.f, cd == 3 ? v : 0.f);
+            }
+        }
+    };
+
+    int b = blockIdx.x;
+    __syncthreads();  // zeroed planes before the first interior write
+    load_chunk(b, 0);
+    write_chunk(dcb);
+    __syncthreads();
+
+    int buf = 0;
+    f32x16 acc[2];
 #pragma unroll 1
-    for (int chunk = 0; chunk < 4; ++chunk) {
-        __syncthreads();
-        // expand dc for 16 channels: each window writes its 2x2 block (value at the routed position)
-        for (int e = tid; e < 16 * P_WIN; e += C2D_THREADS) {
-            const int col = e / P_WIN, win = e - col * P_WIN;
-            const int gi = (chunk * 16 + col) * P_WIN + win;
-            const int cd = cb[gi];
-            const float v = dpb[gi];
-            const int py = win / P_HW, px = win - (win / P_HW) * P_HW;
-            float* d = dcp + col * C2D_PLANE + (2 * py + 2) * 28 + 2 * px + 2;
-            *reinterpret_cast<float2*>(d) = make_float2(cd == 0 ? v : 0.f, cd == 1 ? v : 0.f);
-            *reinterpret_cast<float2*>(d + 28) = make_float2(cd == 2 ? v : 0.f, cd == 3 ? v : 0.f);
-        }
-        // W2 chunk as [s = co_lo*9 + tap][h = co_l >> 3][ci]
-        for (int e = tid; e < 16 * K2; e += C2D_THREADS) {
-            const int col = e / K2, r = e - col * K2;
-            const int ci = r / 9, tap = r - ci * 9;
-            const int s = (col & 7) * 9 + tap;
-            w2d[(s * 2 + (col >> 3)) * 32 + ci] = W2[(chunk * 16 + col) * K2 + r];
-        }
-        __syncthreads();
-        if (nt == 3) c2d_chunk<3>(dcp, w2d, pbase, acc, h, j);
-        else c2d_chunk<2>(dcp, w2d, pbase, acc, h, j);
-    }
-
-    float* gb = gcut + (size_t)b * A_SAMPLE;
+    for (; b < B; b += gridDim.x) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        if (i < nt && pix[i] < A_PIX) {
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
-                gb[ci * A_PIX + pix[i]] = acc[i][r];
+            for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+        for (int ch = 0; ch < C2D_NCHUNK; ++ch) {
+            const int nb = (ch + 1 < C2D_NCHUNK) ? b : b + gridDim.x;
+            const int nch = (ch + 1 < C2D_NCHUNK) ? ch + 1 : 0;
+            load_chunk(nb, nch);
+            const float* dcp = dcb + buf * C2D_DC;
+            const float* wc = w2d + ch * C2D_WC + h * 32 + j;
+            if (nt == 2) c2d_chunk<2>(dcp, wc, pbase, acc);
+            else c2d_chunk<1>(dcp, wc, pbase, acc);
+            if (nb < B) write_chunk(dcb + (buf ^ 1) * C2D_DC);
+            __syncthreads();
+            buf ^= 1;
+        }
+        float* gb = gcut + (size_t)b * A_SAMPLE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i < nt && pix[i] < A_PIX) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ci = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    gb[ci * A_PIX + pix[i]] = acc[i][r];
+                }
             }
         }
     }
@@ -237,75 +295,114 @@ __global__ __launch_bounds__(C2D_THREADS, 4) void conv2_dgrad_kernel(
 
 // ============================================================================ conv2 wgrad
 // dW2[co][ci][tap] = sum_b sum_{y,x} dc[b][co][y][x] * act[b][ci][y+ky][x+kx];  db2[co] = sum dc.
-// Work unit = (sample, band of 6 pooled rows). K runs window by window: one 16x16x4 MFMA consumes
-// the 4 pixels of one pooling window, and the A operand (dc) is just `code == q ? dpooled : 0`.
-// 6 waves; wave w owns co tiles {2(w&1), 2(w&1)+1} and 6 of the 18 (tap, ci-half) column tiles:
-// 12 tiles = 48 accumulator registers that persist over every unit the workgroup processes. The
-// workgroup then writes one [dW2 | db2] slab; slabs are summed in fixed order by the SGD kernel.
-// LDS: act rows of one band (32 x 14 x 26) + dc band as [win][co] + code band = 70,208 B.
-constexpr int C2W_WAVES = 6;
+// Persistent: one 12-wave workgroup per CU walks work units (sample, band of 6 pooled rows).
+// K runs window by window: one 16x16x4 MFMA consumes the 4 pixels of one pooling window, and its A
+// operand (dc) is `code == q ? dpooled : 0` — the max-pool/ReLU routing is applied in the operand.
+// Wave w owns co tiles {2(w&1), 2(w&1)+1} and column tiles 3*(w>>1) + {0,1,2} of the 18
+// (tap, ci-half) tiles: 6 16x16 accumulators that live across every unit of the launch.
+// LDS, double-buffered per unit: act rows 12*band .. 12*band+13 of all 32 channels (46,592 B, by
+// LDS-DMA with per-lane source addresses) + dc band as [win][co] (18,720 B) + code band (4,896 B);
+// the dc band is register-staged (its transpose happens in the LDS write). db2 is summed in
+// registers while staging (thread t owns channel t % 64). The workgroup finally writes one
+// [dW2 | db2] slab; slabs are summed in a fixed order by the SGD kernel.
+constexpr int C2W_WAVES = 12;
 constexpr int C2W_THREADS = C2W_WAVES * 64;
 constexpr int C2W_ROWS = 14;
-constexpr int C2W_CSTR = C2W_ROWS * A_HW;   // 364
-constexpr int C2W_IMG = C1 * C2W_CSTR;      // 11648 floats
+constexpr int C2W_CSTR = C2W_ROWS * A_HW;   // 364 floats per channel
+constexpr int C2W_IMG = C1 * C2W_CSTR;      // 11648 floats = 46,592 B
 constexpr int C2W_DSTR = 65;                // dc row stride (floats), padded
 constexpr int C2W_CDSTR = 68;               // code row stride (bytes), padded
-constexpr int C2W_MAXSLAB = 512;
+constexpr int C2W_DC = 72 * C2W_DSTR;       // 4680 floats
+constexpr int C2W_CD = 72 * C2W_CDSTR / 4;  // 1224 floats worth of bytes
+constexpr int C2W_BUF = C2W_IMG + C2W_DC + C2W_CD;  // 17552 floats = 70,208 B
+constexpr int C2W_MAXSLAB = 256;
 constexpr int C2W_SLAB = W2_N + C2;         // 18496
+constexpr int C2W_PIECES = (C2W_IMG * 4 + 1023) / 1024;  // 46 LDS-DMA pieces per band
+constexpr int C2W_STG = 72 / (C2W_THREADS / C2);          // 6 windows per thread
+
+__device__ __forceinline__ void c2w_dma_band(const float* __restrict__ ab, float* dst, int wave, int lane) {
+    // LDS image [ci][364] is contiguous; each lane's 16 B come from channel ci's row band.
+    char* d = reinterpret_cast<char*>(dst);
+    for (int c = wave; c < C2W_PIECES; c += C2W_WAVES) {
+        const int o = c * 1024 + lane * 16;
+        if (o < C2W_IMG * 4) {
+            const int ci = o / (C2W_CSTR * 4), r = o - ci * (C2W_CSTR * 4);
+            const char* src = reinterpret_cast<const char*>(ab + ci * A_PIX) + r;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(d + c * 1024), 16, 0, 0);
+        }
+    }
+}
 
 __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
     const float* __restrict__ act, const float* __restrict__ dpool, const uint8_t* __restrict__ code,
     float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(16))) float img[C2W_IMG];
-    __shared__ float dcb[72 * C2W_DSTR];
-    __shared__ uint8_t cdb[72 * C2W_CDSTR];
+    __shared__ __attribute__((aligned(16))) float smem[2 * C2W_BUF];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int g4 = lane >> 4, c = lane & 15;
-    const int cp = wave & 1;            // co tiles 2cp, 2cp+1
-    const int ntb = 6 * (wave >> 1);    // column tiles ntb .. ntb+5
+    const int cp = wave & 1;
+    const int ntb = 3 * (wave >> 1);
 
-    int base[6];
+    int base[3];
 #pragma unroll
-    for (int tt = 0; tt < 6; ++tt) {
+    for (int tt = 0; tt < 3; ++tt) {
         const int ntile = ntb + tt, tap = ntile >> 1, chalf = ntile & 1;
         const int ky = tap / 3, kx = tap % 3;
         base[tt] = (chalf * 16 + c) * C2W_CSTR + ((g4 >> 1) + ky) * A_HW + (g4 & 1) + kx;
     }
-    f32x4 acc[2][6];
+    f32x4 acc[2][3];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int tt = 0; tt < 6; ++tt) acc[m][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float db_acc = 0.f;
+        for (int tt = 0; tt < 3; ++tt) acc[m][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // dc staging: thread t owns channel sco = t % 64 and windows t/64 + 12*i
+    const int sco = tid & 63, sw0 = tid >> 6;
+    float sv[C2W_STG];
+    int sc[C2W_STG];
+    float db_acc = 0.f;
     const int nunit = 2 * B;
+    auto load_dc = [&](int u) {
+        if (u < nunit) {
+            const int bb = u >> 1, band = u & 1;
+            const size_t g0 = (size_t)bb * P_SAMPLE + sco * P_WIN + band * 72;
+#pragma unroll
+            for (int i = 0; i < C2W_STG; ++i) {
+                sv[i] = dpool[g0 + sw0 + 12 * i];
+                sc[i] = code[g0 + sw0 + 12 * i];
+            }
+        }
+    };
+    auto write_dc = [&](float* bufp) {
+        float* dcb = bufp + C2W_IMG;
+        uint8_t* cdb = reinterpret_cast<uint8_t*>(bufp + C2W_IMG + C2W_DC);
+#pragma unroll
+        for (int i = 0; i < C2W_STG; ++i) {
+            const int w = sw0 + 12 * i;
+            dcb[w * C2W_DSTR + sco] = sv[i];
+            cdb[w * C2W_CDSTR + sco] = (uint8_t)sc[i];
+            db_acc += (sc[i] != CODE_NONE) ? sv[i] : 0.f;
+        }
+    };
+
+    int u = blockIdx.x;
+    if (u < nunit) c2w_dma_band(act + (size_t)(u >> 1) * A_SAMPLE + (u & 1) * 12 * A_HW, smem, wave, lane);
+    load_dc(u);
+    if (u < nunit) write_dc(smem);
+    __syncthreads();
+
+    int buf = 0;
 #pragma unroll 1
-    for (int u = blockIdx.x; u < nunit; u += gridDim.x) {
-        const int b = u >> 1, band = u & 1;
-        __syncthreads();
-        // act rows 12*band .. 12*band+13 of every channel (364 contiguous floats per channel)
-        const float* ab = act + (size_t)b * A_SAMPLE + band * 12 * A_HW;
-        for (int i = tid; i < C1 * (C2W_CSTR / 4); i += C2W_THREADS) {
-            const int ci = i / (C2W_CSTR / 4), r4 = i - ci * (C2W_CSTR / 4);
-            reinterpret_cast<float4*>(img + ci * C2W_CSTR)[r4] =
-                reinterpret_cast<const float4*>(ab + ci * A_PIX)[r4];
-        }
-        const float* dpb = dpool + (size_t)b * P_SAMPLE + band * 72;
-        const uint8_t* cbb = code + (size_t)b * P_SAMPLE + band * 72;
-        for (int e = tid; e < C2 * 72; e += C2W_THREADS) {
-            const int co = e / 72, w = e - co * 72;
-            dcb[w * C2W_DSTR + co] = dpb[co * P_WIN + w];
-            cdb[w * C2W_CDSTR + co] = cbb[co * P_WIN + w];
-        }
-        __syncthreads();
-        if (tid < C2) {  // db2: fixed-order sum over the band's routed windows
-            float s = 0.f;
-            for (int w = 0; w < 72; ++w)
-                s += (cdb[w * C2W_CDSTR + tid] != CODE_NONE) ? dcb[w * C2W_DSTR + tid] : 0.f;
-            db_acc += s;
-        }
+    for (; u < nunit; u += gridDim.x) {
+        const int nu = u + gridDim.x;
+        float* cur = smem + buf * C2W_BUF;
+        float* nxt = smem + (buf ^ 1) * C2W_BUF;
+        if (nu < nunit) c2w_dma_band(act + (size_t)(nu >> 1) * A_SAMPLE + (nu & 1) * 12 * A_HW, nxt, wave, lane);
+        load_dc(nu);
+        const float* img = cur;
+        const float* dcb = cur + C2W_IMG;
+        const uint8_t* cdb = reinterpret_cast<const uint8_t*>(cur + C2W_IMG + C2W_DC);
 #pragma unroll 1
         for (int pyl = 0; pyl < 6; ++pyl) {
             const float* dr = dcb + pyl * P_HW * C2W_DSTR + cp * 32 + c;
@@ -321,20 +418,32 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
                     av[m] = (cd == g4) ? dv : 0.f;
                 }
 #pragma unroll
-                for (int tt = 0; tt < 6; ++tt) {
+                for (int tt = 0; tt < 3; ++tt) {
                     const float bv = ir[base[tt] + 2 * px];
                     acc[0][tt] = mfma16x16x4(av[0], bv, acc[0][tt]);
                     acc[1][tt] = mfma16x16x4(av[1], bv, acc[1][tt]);
                 }
             }
         }
+        if (nu < nunit) write_dc(nxt);
+        __syncthreads();
+        buf ^= 1;
     }
 
+    // db2: 12 partials per channel (threads co, co+64, ...) summed in fixed order via LDS
+    float* red = smem;  // all units done (last barrier passed)
+    red[tid] = db_acc;
+    __syncthreads();
     float* slab = slabs + (size_t)blockIdx.x * C2W_SLAB;
+    if (tid < C2) {
+        float s = 0.f;
+        for (int k = 0; k < C2W_THREADS / C2; ++k) s += red[k * C2 + tid];
+        slab[W2_N + tid] = s;
+    }
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int tt = 0; tt < 6; ++tt) {
+        for (int tt = 0; tt < 3; ++tt) {
             const int ntile = ntb + tt, tap = ntile >> 1, chalf = ntile & 1;
             const int ci = chalf * 16 + c;
 #pragma unroll
@@ -343,7 +452,6 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
                 slab[co * K2 + ci * 9 + tap] = acc[m][tt][r];
             }
         }
-    if (tid < C2) slab[W2_N + tid] = db_acc;
 }
 
 extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
@@ -518,7 +626,8 @@ extern "C" int slk_conv2_fwd_pool(const float* act, const float* W2, const float
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(act && W2 && b2 && pooled && code);
-    conv2_fwd_pool_kernel<<<B, C2F_THREADS, 0, slk_stream(stream)>>>(act, W2, b2, pooled, code);
+    conv2_fwd_pool_kernel<<<B < C2F_GRID ? B : C2F_GRID, C2F_THREADS, 0, slk_stream(stream)>>>(
+        act, W2, b2, pooled, code, B);
     return slk_launch_status();
 }
 
@@ -527,7 +636,8 @@ extern "C" int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const 
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(dpooled && code && W2 && cut_grad);
-    conv2_dgrad_kernel<<<B, C2D_THREADS, 0, slk_stream(stream)>>>(dpooled, code, W2, cut_grad);
+    conv2_dgrad_kernel<<<B < C2D_GRID ? B : C2D_GRID, C2D_THREADS, 0, slk_stream(stream)>>>(
+        dpooled, code, W2, cut_grad, B);
     return slk_launch_status();
 }
 
