@@ -10,107 +10,145 @@
 
 using namespace slk;
 
-// One workgroup per sample. Thread t produces float4 chunks of the NCHW output; 676 % 4 == 0, so a
-// chunk never straddles two channels.
+// One workgroup per sample; thread t owns pixels t, t+256, t+512 (< 676). Its 3x3 input windows
+// are read once from LDS (consecutive lanes -> consecutive addresses) into registers, then it walks
+// the 32 channels with wave-uniform (broadcast) weights: every store is a 256-B coalesced row
+// segment of one channel plane. HBM-bound on the 86,528-B/sample write.
+constexpr int C1F_PPT = 3;  // pixels per thread
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ W1,
                                                         const float* __restrict__ b1,
                                                         float* __restrict__ act) {
     __shared__ float xs[IN_HW * IN_HW];
-    __shared__ float ws[C1 * 9];
-    __shared__ float bs[C1];
+    __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const float* xb = x + (size_t)b * IN_HW * IN_HW;
     for (int i = tid; i < IN_HW * IN_HW / 4; i += 256)
         reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xb)[i];
-    for (int i = tid; i < C1 * 9; i += 256) ws[i] = W1[i];
-    if (tid < C1) bs[tid] = b1[tid];
+    for (int i = tid; i < C1 * 9; i += 256) ws[(i / 9) * 10 + i % 9] = W1[i];
+    if (tid < C1) ws[tid * 10 + 9] = b1[tid];
     __syncthreads();
 
-    float4* out = reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE);
-    for (int i4 = tid; i4 < A_SAMPLE / 4; i4 += 256) {
-        const int e = i4 * 4;
-        const int c = e / A_PIX;
-        const int p0 = e - c * A_PIX;
-        const float* w = ws + c * 9;
-        float r[4];
+    float xv[C1F_PPT][9];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int p = p0 + u;
-            const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
-            const float* src = xs + y * IN_HW + xx;
-            // same tap order as the reference conv (ky, kx row-major), bias added last
+    for (int u = 0; u < C1F_PPT; ++u) {
+        const int p = tid + 256 * u;
+        const int pc = p < A_PIX ? p : A_PIX - 1;
+        const int y = pc / A_HW, xx = pc - (pc / A_HW) * A_HW;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
+    }
+    float* out = act + (size_t)b * A_SAMPLE;
+#pragma unroll 4
+    for (int c = 0; c < C1; ++c) {
+        const float* w = ws + c * 10;
+        float wk[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) wk[k] = w[k];
+#pragma unroll
+        for (int u = 0; u < C1F_PPT; ++u) {
+            const int p = tid + 256 * u;
+            // tap order (ky, kx) row-major, bias added last — as the reference conv
             float s = 0.f;
 #pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) s = fmaf(src[ky * IN_HW + kx], w[ky * 3 + kx], s);
-            s += bs[c];
-            r[u] = s > 0.f ? s : 0.f;
+            for (int k = 0; k < 9; ++k) s = fmaf(xv[u][k], wk[k], s);
+            s += wk[9];
+            if (p < A_PIX) out[c * A_PIX + p] = s > 0.f ? s : 0.f;
         }
-        out[i4] = make_float4(r[0], r[1], r[2], r[3]);
     }
 }
 
-// conv1 weight gradient. Grid (ngroups, 32 channels); a workgroup owns one channel c and a group of
-// G samples, so its 676*G-long reduction stays in registers + one LDS tree: fixed order, bit-stable.
-// Output slab row (per group): [dW1 c*9+tap (288) | db1 c (32)] = the client flat layout.
-constexpr int C1W_G = 8;
+// conv1 weight gradient. Grid (ngroups of 16 samples, 8 channel groups of 4). Thread t owns pixels
+// t, t+256, t+512; per sample it loads its 3x3 input windows once and, for each of the block's 8
+// channels, the cut gradient and the activation (relu-bwd mask act > 0) as coalesced rows, keeping
+// 8 x 10 accumulators. A fixed-order block reduction writes the group's slab row
+// [dW1 c*9+tap (288) | db1 c (32)] (the client flat layout) for those 8 channels.
+constexpr int C1W_G = 16;
+constexpr int C1W_CG = 4;
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ act,
                                                           const float* __restrict__ gcut,
                                                           float* __restrict__ slabs, int B) {
-    __shared__ float xs[C1W_G * IN_HW * IN_HW];
-    __shared__ float red[4][10];
+    __shared__ float red[4][C1W_CG * 10];
     const int grp = blockIdx.x;
-    const int c = blockIdx.y;
+    const int c0 = blockIdx.y * C1W_CG;
     const int tid = threadIdx.x;
     const int b0 = grp * C1W_G;
     const int nb = min(C1W_G, B - b0);
-    for (int i = tid; i < nb * IN_HW * IN_HW / 4; i += 256)
-        reinterpret_cast<float4*>(xs)[i] =
-            reinterpret_cast<const float4*>(x + (size_t)b0 * IN_HW * IN_HW)[i];
-    __syncthreads();
 
-    float acc[10];
+    float acc[C1W_CG][10];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-    constexpr int P4 = A_PIX / 4;  // 169 float4 per channel plane
-    for (int i4 = tid; i4 < nb * P4; i4 += 256) {
-        const int bl = i4 / P4;
-        const int p0 = (i4 - bl * P4) * 4;
-        const size_t off = ((size_t)(b0 + bl) * C1 + c) * A_PIX + p0;
-        const float4 g4 = *reinterpret_cast<const float4*>(gcut + off);
-        const float4 a4 = *reinterpret_cast<const float4*>(act + off);
-        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float* xi = xs + bl * IN_HW * IN_HW;
+    for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float gm = av[u] > 0.f ? gv[u] : 0.f;  // threshold_backward: grad where relu out > 0
-            const int p = p0 + u;
-            const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
-            const float* src = xi + y * IN_HW + xx;
+        for (int k = 0; k < 10; ++k) acc[c][k] = 0.f;
+    // pixel slots: loads always use a clamped (valid) pixel; invalid slots are zeroed by `valid`
+    // (a per-load branch would make hipcc wait vmcnt(0) around every load)
+    int pix[C1F_PPT], xo[C1F_PPT];
+    float valid[C1F_PPT];
 #pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
+    for (int u = 0; u < C1F_PPT; ++u) {
+        const int p = tid + 256 * u;
+        const int pc = p < A_PIX ? p : A_PIX - 1;
+        pix[u] = pc;
+        valid[u] = p < A_PIX ? 1.f : 0.f;
+        xo[u] = (pc / A_HW) * IN_HW + pc % A_HW;
+    }
+#pragma unroll 1
+    for (int bl = 0; bl < nb; ++bl) {
+        const int bb = b0 + bl;
+        const float* xi = x + (size_t)bb * IN_HW * IN_HW;
+        const float* ab = act + ((size_t)bb * C1 + c0) * A_PIX;
+        const float* gb = gcut + ((size_t)bb * C1 + c0) * A_PIX;
+        // issue every load of this sample first, then pin them (an empty asm that "uses" each value
+        // keeps hipcc from sinking gv's load into a branch on av > 0 with a vmcnt(0) per element)
+        float gv[C1W_CG][C1F_PPT], av[C1W_CG][C1F_PPT];
 #pragma unroll
-                for (int kx = 0; kx < 3; ++kx) acc[ky * 3 + kx] = fmaf(gm, src[ky * IN_HW + kx], acc[ky * 3 + kx]);
-            acc[9] += gm;
-        }
+        for (int c = 0; c < C1W_CG; ++c)
+#pragma unroll
+            for (int u = 0; u < C1F_PPT; ++u) {
+                gv[c][u] = gb[c * A_PIX + pix[u]];
+                av[c][u] = ab[c * A_PIX + pix[u]];
+            }
+#pragma unroll
+        for (int c = 0; c < C1W_CG; ++c)
+#pragma unroll
+            for (int u = 0; u < C1F_PPT; ++u) asm volatile("" : "+v"(gv[c][u]), "+v"(av[c][u]));
+        float gm[C1W_CG][C1F_PPT];
+#pragma unroll
+        for (int c = 0; c < C1W_CG; ++c)
+#pragma unroll
+            for (int u = 0; u < C1F_PPT; ++u)
+                gm[c][u] = av[c][u] > 0.f ? gv[c][u] * valid[u] : 0.f;  // threshold_backward mask
+        float xv[C1F_PPT][9];
+#pragma unroll
+        for (int u = 0; u < C1F_PPT; ++u)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) xv[u][k] = xi[xo[u] + (k / 3) * IN_HW + k % 3];
+#pragma unroll
+        for (int c = 0; c < C1W_CG; ++c)
+#pragma unroll
+            for (int u = 0; u < C1F_PPT; ++u) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc[c][k] = fmaf(gm[c][u], xv[u][k], acc[c][k]);
+                acc[c][9] += gm[c][u];
+            }
     }
     const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        const float v = wave_sum(acc[k]);
-        if (lane == 0) red[wave][k] = v;
-    }
+    for (int c = 0; c < C1W_CG; ++c)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            const float v = wave_sum(acc[c][k]);
+            if (lane == 0) red[wave][c * 10 + k] = v;
+        }
     __syncthreads();
-    if (tid < 10) {
+    if (tid < C1W_CG * 10) {
+        const int c = tid / 10, k = tid - c * 10;
         const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
         float* slab = slabs + (size_t)grp * SLK_CLIENT_NPARAM;
-        if (tid < 9) slab[c * 9 + tid] = v;
-        else slab[C1 * 9 + c] = v;
+        if (k < 9) slab[(c0 + c) * 9 + k] = v;
+        else slab[C1 * 9 + c0 + c] = v;
     }
 }
 
@@ -130,7 +168,7 @@ extern "C" int slk_conv1_wgrad(const float* x, const float* act, const float* cu
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(x && act && cut_grad && slabs);
-    dim3 grid(slk_conv1_wgrad_nslab(B), C1);
+    dim3 grid(slk_conv1_wgrad_nslab(B), C1 / C1W_CG);
     conv1_wgrad_kernel<<<grid, 256, 0, slk_stream(stream)>>>(x, act, cut_grad, slabs, B);
     return slk_launch_status();
 }

@@ -457,18 +457,19 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
 extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
 
 // ============================================================================ fc1 + cross-entropy
-// 4 samples per 256-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy fwd+bwd,
-// 4 = fc input gradient (dpooled = dlogits @ W3). W3 (368 KB) is L2/MALL-resident and is re-read
-// once per 4 samples per phase; pooled is streamed from HBM once.
-constexpr int FC_S = 4;
+// 8 samples per 512-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy
+// fwd+bwd, 4 = fc input gradient (dpooled = dlogits @ W3). W3 (368 KB) is L2/MALL-resident and is
+// re-read once per 8 samples per phase; pooled is streamed from HBM once.
+constexpr int FC_S = 8;
+constexpr int FC_T = 512;
 constexpr int FC_K4 = P_SAMPLE / 4;  // 2304
 
 template <int MODE>
-__global__ __launch_bounds__(256) void fc_head_kernel(
+__global__ __launch_bounds__(FC_T) void fc_head_kernel(
     const float* __restrict__ pooled, const float* __restrict__ W3, const float* __restrict__ b3,
     const int64_t* __restrict__ labels, float* __restrict__ logits, float* __restrict__ loss_i,
     float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B) {
-    __shared__ float red[4][FC_S * NCLS];
+    __shared__ float red[FC_T / 64][FC_S * NCLS];
     __shared__ float zl[FC_S][NCLS];
     __shared__ float dl[FC_S][NCLS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -483,7 +484,7 @@ __global__ __launch_bounds__(256) void fc_head_kernel(
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) acc[s][jj] = 0.f;
         const float4* P4 = reinterpret_cast<const float4*>(pooled + (size_t)b0 * P_SAMPLE);
-        for (int k4 = tid; k4 < FC_K4; k4 += 256) {
+        for (int k4 = tid; k4 < FC_K4; k4 += FC_T) {
             float4 w[NCLS];
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) w[jj] = W34[jj * FC_K4 + k4];
@@ -507,7 +508,10 @@ __global__ __launch_bounds__(256) void fc_head_kernel(
         __syncthreads();
         if (tid < FC_S * NCLS) {
             const int s = tid / NCLS, jj = tid - s * NCLS;
-            const float v = (((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]) + b3[jj];
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < FC_T / 64; ++w) v += red[w][tid];
+            v += b3[jj];
             zl[s][jj] = v;
             if (s < ns) logits[(size_t)(b0 + s) * NCLS + jj] = v;
         }
@@ -559,57 +563,75 @@ __global__ __launch_bounds__(256) void fc_head_kernel(
 
     if (MODE & 4) {
         float4* D4 = reinterpret_cast<float4*>(dpooled + (size_t)b0 * P_SAMPLE);
-        for (int k4 = tid; k4 < FC_K4; k4 += 256) {
+        for (int k4 = tid; k4 < FC_K4; k4 += FC_T) {
             float4 w[NCLS];
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) w[jj] = W34[jj * FC_K4 + k4];
+#pragma unroll 2
+            for (int s = 0; s < ns; ++s) {
+                float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int s = 0; s < FC_S; ++s) {
-                if (s < ns) {
-                    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                    for (int jj = 0; jj < NCLS; ++jj) {
-                        const float d = dl[s][jj];
-                        o.x = fmaf(d, w[jj].x, o.x); o.y = fmaf(d, w[jj].y, o.y);
-                        o.z = fmaf(d, w[jj].z, o.z); o.w = fmaf(d, w[jj].w, o.w);
-                    }
-                    D4[s * FC_K4 + k4] = o;
+                for (int jj = 0; jj < NCLS; ++jj) {
+                    const float d = dl[s][jj];  // LDS broadcast
+                    o.x = fmaf(d, w[jj].x, o.x); o.y = fmaf(d, w[jj].y, o.y);
+                    o.z = fmaf(d, w[jj].z, o.z); o.w = fmaf(d, w[jj].w, o.w);
                 }
+                D4[s * FC_K4 + k4] = o;
             }
         }
     }
 }
 
-// fc1 weight gradient partials. Grid (36 column blocks of 256, nsplit batch slices). Thread t owns
-// column k and sums its slice of the batch in order; db3 comes from column block 0.
-constexpr int FCW_MAXSPLIT = 32;
+// fc1 weight gradient partials. Grid (9 column blocks of 1024, nsplit batch slices). Thread t owns
+// the 4 columns 4*(blockIdx.x*256 + t) .. +3 and sums its slice of the batch in order, 8 samples'
+// float4 rows in flight; db3 comes from column block 0. dlogits are wave-uniform scalar loads.
+constexpr int FCW_MAXSPLIT = 64;
 constexpr int FCW_SLAB = W3_N + NCLS;  // 92170
 __global__ __launch_bounds__(256) void fc_wgrad_kernel(const float* __restrict__ dlogits,
                                                        const float* __restrict__ pooled,
                                                        float* __restrict__ slabs, int B, int per) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int k4 = blockIdx.x * 256 + threadIdx.x;  // float4 column index (< 2304)
     const int sp = blockIdx.y;
     const int bs = sp * per, be = min(B, bs + per);
-    float acc[NCLS];
+    float4 acc[NCLS];
 #pragma unroll
-    for (int jj = 0; jj < NCLS; ++jj) acc[jj] = 0.f;
-    for (int b = bs; b < be; ++b) {
-        const float p = pooled[(size_t)b * P_SAMPLE + k];
+    for (int jj = 0; jj < NCLS; ++jj) acc[jj] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* P4 = reinterpret_cast<const float4*>(pooled);
+    int b = bs;
+    for (; b + 8 <= be; b += 8) {
+        float4 p[8];
 #pragma unroll
-        for (int jj = 0; jj < NCLS; ++jj) acc[jj] = fmaf(dlogits[b * NCLS + jj], p, acc[jj]);
+        for (int u = 0; u < 8; ++u) p[u] = P4[(size_t)(b + u) * FC_K4 + k4];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int jj = 0; jj < NCLS; ++jj) {
+                const float d = dlogits[(b + u) * NCLS + jj];
+                acc[jj].x = fmaf(d, p[u].x, acc[jj].x); acc[jj].y = fmaf(d, p[u].y, acc[jj].y);
+                acc[jj].z = fmaf(d, p[u].z, acc[jj].z); acc[jj].w = fmaf(d, p[u].w, acc[jj].w);
+            }
+    }
+    for (; b < be; ++b) {
+        const float4 p = P4[(size_t)b * FC_K4 + k4];
+#pragma unroll
+        for (int jj = 0; jj < NCLS; ++jj) {
+            const float d = dlogits[b * NCLS + jj];
+            acc[jj].x = fmaf(d, p.x, acc[jj].x); acc[jj].y = fmaf(d, p.y, acc[jj].y);
+            acc[jj].z = fmaf(d, p.z, acc[jj].z); acc[jj].w = fmaf(d, p.w, acc[jj].w);
+        }
     }
     float* slab = slabs + (size_t)sp * FCW_SLAB;
 #pragma unroll
-    for (int jj = 0; jj < NCLS; ++jj) slab[jj * P_SAMPLE + k] = acc[jj];
+    for (int jj = 0; jj < NCLS; ++jj) reinterpret_cast<float4*>(slab + jj * P_SAMPLE)[k4] = acc[jj];
     if (blockIdx.x == 0 && threadIdx.x < NCLS) {
         float s = 0.f;
-        for (int b = bs; b < be; ++b) s += dlogits[b * NCLS + threadIdx.x];
+        for (int bb = bs; bb < be; ++bb) s += dlogits[bb * NCLS + threadIdx.x];
         slab[W3_N + threadIdx.x] = s;
     }
 }
 
 static inline int fcw_per(int B) {
-    int ns = (B + 127) / 128;
+    int ns = (B + 63) / 64;
     if (ns > FCW_MAXSPLIT) ns = FCW_MAXSPLIT;
     if (ns < 1) ns = 1;
     return (B + ns - 1) / ns;
@@ -656,7 +678,7 @@ extern "C" int slk_fc_fwd(const float* pooled, const float* W3, const float* b3,
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(pooled && W3 && b3 && logits);
-    fc_head_kernel<1><<<(B + FC_S - 1) / FC_S, 256, 0, slk_stream(stream)>>>(
+    fc_head_kernel<1><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
         pooled, W3, b3, nullptr, logits, nullptr, nullptr, nullptr, 0.f, nullptr, B);
     return slk_launch_status();
 }
@@ -666,7 +688,7 @@ extern "C" int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, floa
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(logits && labels && loss_i && dlogits);
-    fc_head_kernel<2><<<(B + FC_S - 1) / FC_S, 256, 0, slk_stream(stream)>>>(
+    fc_head_kernel<2><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
         nullptr, nullptr, nullptr, labels, const_cast<float*>(logits), loss_i, dlogits, nullptr,
         grad_scale, err_flag, B);
     return slk_launch_status();
@@ -677,7 +699,7 @@ extern "C" int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpoole
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(dlogits && W3 && dpooled);
-    fc_head_kernel<4><<<(B + FC_S - 1) / FC_S, 256, 0, slk_stream(stream)>>>(
+    fc_head_kernel<4><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
         nullptr, W3, nullptr, nullptr, nullptr, nullptr, const_cast<float*>(dlogits), dpooled, 0.f,
         nullptr, B);
     return slk_launch_status();
@@ -689,7 +711,7 @@ extern "C" int slk_fc_xent(const float* pooled, const float* W3, const float* b3
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits && dpooled);
-    fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, 256, 0, slk_stream(stream)>>>(
+    fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
         pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B);
     return slk_launch_status();
 }
@@ -700,7 +722,7 @@ extern "C" int slk_fc_wgrad(const float* dlogits, const float* pooled, float* sl
     if (B == 0) return 0;
     SLK_CHECK_ARG(dlogits && pooled && slabs);
     const int per = fcw_per(B);
-    dim3 grid(P_SAMPLE / 256, (B + per - 1) / per);
+    dim3 grid(FC_K4 / 256, (B + per - 1) / per);
     fc_wgrad_kernel<<<grid, 256, 0, slk_stream(stream)>>>(dlogits, pooled, slabs, B, per);
     return slk_launch_status();
 }
