@@ -91,6 +91,12 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
     __syncthreads();
 
     int buf = 0;
+    float slk_abl_reg = (float)lane;
+    slk_keep(slk_abl_reg);
+#if SLK_ABL & 16
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+    const int b_first = b;
+#endif
 #pragma unroll 1
     for (; b < B; b += gridDim.x) {
         f32x16 acc[C2F_TPW];
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
         for (int hc = 0; hc < 2; ++hc) {
             // prefetch the next half (this sample's second half, or the next sample's first)
             const int nb = hc ? b + gridDim.x : b;
-            if (nb < B) c2f_dma_half(act + (size_t)nb * A_SAMPLE + (hc ? 0 : C2F_IMG), imgb + (buf ^ 1) * C2F_IMG,
+            if (!(SLK_ABL & 4) && nb < B) c2f_dma_half(act + (size_t)nb * A_SAMPLE + (hc ? 0 : C2F_IMG), imgb + (buf ^ 1) * C2F_IMG,
                                      wave, lane);
             const float* img = imgb + buf * C2F_IMG;
             const float* wl = w2s + hc * C2F_WH + h * 64 + ct * 32 + j;
@@ -116,10 +122,10 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
                 const float* wt = wl + tap * 8 * 128;
 #pragma unroll
                 for (int ci_lo = 0; ci_lo < 8; ++ci_lo) {
-                    const float bv = wt[ci_lo * 128];
+                    const float bv = SLK_LDS(wt[ci_lo * 128]);
 #pragma unroll
                     for (int t = 0; t < C2F_TPW; ++t)
-                        acc[t] = mfma32x32x2(img[tb[t] + ci_lo * A_PIX], bv, acc[t]);
+                        acc[t] = mfma32x32x2(SLK_LDS(img[tb[t] + ci_lo * A_PIX]), bv, acc[t]);
                 }
             }
             __syncthreads();  // all reads of `buf` done; the prefetch into buf^1 has landed
@@ -150,6 +156,12 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
             *reinterpret_cast<unsigned int*>(crow + w0) = c4;
         }
     }
+#if SLK_ABL & 16
+    // diagnostic: in-kernel clock (GHz) of this workgroup into pooled[blockIdx.x] (output is garbage)
+    __syncthreads();
+    const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && b_first < B) pooled[blockIdx.x] = (float)((double)(clk_t1 - clk_t0) / (double)(clk_r1 - clk_r0) * 0.1);
+#endif
 }
 
 // ============================================================================ conv2 dgrad (cut grad)
@@ -177,16 +189,30 @@ constexpr int C2D_STG = (C2D_CO * P_WIN + C2D_THREADS - 1) / C2D_THREADS;  // 2 
 template <int NT>
 __device__ __forceinline__ void c2d_chunk(const float* __restrict__ dcp, const float* __restrict__ wc,
                                           const int (&pbase)[2], f32x16 (&acc)[2]) {
+    float slk_abl_reg = (float)threadIdx.x;
+    slk_keep(slk_abl_reg);
 #pragma unroll
     for (int co_lo = 0; co_lo < 4; ++co_lo) {
+        // gather this channel's 9 taps of operands, then 9*NT MFMAs back to back
+        float av[9], bv[9][NT];
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int ky = tap / 3, kx = tap % 3;
-            const float av = wc[(co_lo * 9 + tap) * 64];
+            av[tap] = SLK_LDS(wc[(co_lo * 9 + tap) * 64]);
             const int imm = co_lo * C2D_PLANE + (2 - ky) * 28 + (2 - kx);
 #pragma unroll
-            for (int i = 0; i < NT; ++i) acc[i] = mfma32x32x2(av, dcp[pbase[i] + imm], acc[i]);
+            for (int i = 0; i < NT; ++i) bv[tap][i] = SLK_LDS(dcp[pbase[i] + imm]);
         }
+#if SLK_PIN_PHASES
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+            for (int i = 0; i < NT; ++i) acc[i] = mfma32x32x2(av[tap], bv[tap][i], acc[i]);
+#if SLK_PIN_PHASES
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
@@ -270,12 +296,12 @@ __global__ __launch_bounds__(C2D_THREADS, 3) void conv2_dgrad_kernel(
         for (int ch = 0; ch < C2D_NCHUNK; ++ch) {
             const int nb = (ch + 1 < C2D_NCHUNK) ? b : b + gridDim.x;
             const int nch = (ch + 1 < C2D_NCHUNK) ? ch + 1 : 0;
-            load_chunk(nb, nch);
+            if (!(SLK_ABL & 4)) load_chunk(nb, nch);
             const float* dcp = dcb + buf * C2D_DC;
             const float* wc = w2d + ch * C2D_WC + h * 32 + j;
             if (nt == 2) c2d_chunk<2>(dcp, wc, pbase, acc);
             else c2d_chunk<1>(dcp, wc, pbase, acc);
-            if (nb < B) write_chunk(dcb + (buf ^ 1) * C2D_DC);
+            if (!(SLK_ABL & 4) && nb < B) write_chunk(dcb + (buf ^ 1) * C2D_DC);
             __syncthreads();
             buf ^= 1;
         }
@@ -296,40 +322,40 @@ __global__ __launch_bounds__(C2D_THREADS, 3) void conv2_dgrad_kernel(
 // ============================================================================ conv2 wgrad
 // dW2[co][ci][tap] = sum_b sum_{y,x} dc[b][co][y][x] * act[b][ci][y+ky][x+kx];  db2[co] = sum dc.
 // Persistent: one 12-wave workgroup per CU walks work units (sample, band of 6 pooled rows).
-// K runs window by window: one 16x16x4 MFMA consumes the 4 pixels of one pooling window, and its A
-// operand (dc) is `code == q ? dpooled : 0` — the max-pool/ReLU routing is applied in the operand.
-// Wave w owns co tiles {2(w&1), 2(w&1)+1} and column tiles 3*(w>>1) + {0,1,2} of the 18
-// (tap, ci-half) tiles: 6 16x16 accumulators that live across every unit of the launch.
-// LDS, double-buffered per unit: act rows 12*band .. 12*band+13 of all 32 channels (46,592 B, by
-// LDS-DMA with per-lane source addresses) + dc band as [win][co] (18,720 B) + code band (4,896 B);
-// the dc band is register-staged (its transpose happens in the LDS write). db2 is summed in
-// registers while staging (thread t owns channel t % 64). The workgroup finally writes one
-// [dW2 | db2] slab; slabs are summed in a fixed order by the SGD kernel.
+// GEMM view: M = 64 co, N = 288 (tap, ci), K = pixels. 32x32x2 MFMAs: a tile is [32 co][32 ci] of
+// one tap; a k step is 2 pixels of one pooling window (lane half h: q = 2t + h, t = 0, 1), so the A
+// operand (dc) of a lane is `code == q ? dpooled : 0` — the max-pool/ReLU routing applied in the
+// operand — and one dc read serves 2 k steps x 3 taps = 6 MFMAs.
+// Waves: w = kh + 2*(ct + 2*tg): co tile ct (32 channels), tap group tg (taps 3tg..3tg+2) and
+// K half kh (windows of even / odd px). The two K halves of each tile are summed in LDS at the end
+// in a fixed order; 48 accumulator registers per wave live across every unit of the launch.
+// LDS, double-buffered per unit: act rows 12*band .. 12*band+13 of all 32 channels at an ODD channel
+// stride of 369 floats (conflict-free B reads; filled by 4-byte LDS-DMA with per-lane sources) +
+// the dc band as [win][co] + code band; the dc band is register-staged (transposed on the LDS
+// write). db2 is summed in registers while staging (thread t owns channel t % 64). The workgroup
+// writes one [dW2 | db2] slab; slabs are summed in a fixed order by the SGD kernel.
 constexpr int C2W_WAVES = 12;
 constexpr int C2W_THREADS = C2W_WAVES * 64;
 constexpr int C2W_ROWS = 14;
-constexpr int C2W_CSTR = C2W_ROWS * A_HW;   // 364 floats per channel
-constexpr int C2W_IMG = C1 * C2W_CSTR;      // 11648 floats = 46,592 B
+constexpr int C2W_BAND = C2W_ROWS * A_HW;   // 364 floats of one channel per band
+constexpr int C2W_CSTR = 369;               // odd LDS channel stride
+constexpr int C2W_IMG = C1 * C2W_CSTR;      // 11808 floats = 47,232 B
 constexpr int C2W_DSTR = 65;                // dc row stride (floats), padded
 constexpr int C2W_CDSTR = 68;               // code row stride (bytes), padded
 constexpr int C2W_DC = 72 * C2W_DSTR;       // 4680 floats
 constexpr int C2W_CD = 72 * C2W_CDSTR / 4;  // 1224 floats worth of bytes
-constexpr int C2W_BUF = C2W_IMG + C2W_DC + C2W_CD;  // 17552 floats = 70,208 B
+constexpr int C2W_BUF = C2W_IMG + C2W_DC + C2W_CD;  // 17712 floats = 70,848 B
 constexpr int C2W_MAXSLAB = 256;
 constexpr int C2W_SLAB = W2_N + C2;         // 18496
-constexpr int C2W_PIECES = (C2W_IMG * 4 + 1023) / 1024;  // 46 LDS-DMA pieces per band
-constexpr int C2W_STG = 72 / (C2W_THREADS / C2);          // 6 windows per thread
+constexpr int C2W_PIECES = (C2W_IMG + 63) / 64;  // 185 four-byte LDS-DMA pieces per band
+constexpr int C2W_STG = 72 / (C2W_THREADS / C2);  // 6 windows per thread
 
 __device__ __forceinline__ void c2w_dma_band(const float* __restrict__ ab, float* dst, int wave, int lane) {
-    // LDS image [ci][364] is contiguous; each lane's 16 B come from channel ci's row band.
-    char* d = reinterpret_cast<char*>(dst);
     for (int c = wave; c < C2W_PIECES; c += C2W_WAVES) {
-        const int o = c * 1024 + lane * 16;
-        if (o < C2W_IMG * 4) {
-            const int ci = o / (C2W_CSTR * 4), r = o - ci * (C2W_CSTR * 4);
-            const char* src = reinterpret_cast<const char*>(ab + ci * A_PIX) + r;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(d + c * 1024), 16, 0, 0);
-        }
+        const int o = c * 64 + lane;  // LDS float index
+        const int ci = o / C2W_CSTR, r = o - ci * C2W_CSTR;
+        if (ci < C1 && r < C2W_BAND)
+            __builtin_amdgcn_global_load_lds((const void*)(ab + ci * A_PIX + r), (lds_ptr_t)(dst + c * 64), 4, 0, 0);
     }
 }
 
@@ -340,37 +366,40 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int g4 = lane >> 4, c = lane & 15;
-    const int cp = wave & 1;
-    const int ntb = 3 * (wave >> 1);
+    const int h = lane >> 5, j = lane & 31;
+    const int kh = wave & 1, ct = (wave >> 1) & 1, tg = wave >> 2;
 
+    // B operand base per tap: channel j, window row offset (t + ky), column (h + kx) + 2px
     int base[3];
 #pragma unroll
     for (int tt = 0; tt < 3; ++tt) {
-        const int ntile = ntb + tt, tap = ntile >> 1, chalf = ntile & 1;
-        const int ky = tap / 3, kx = tap % 3;
-        base[tt] = (chalf * 16 + c) * C2W_CSTR + ((g4 >> 1) + ky) * A_HW + (g4 & 1) + kx;
+        const int tap = 3 * tg + tt, ky = tap / 3, kx = tap % 3;
+        base[tt] = j * C2W_CSTR + ky * A_HW + h + kx;
     }
-    f32x4 acc[2][3];
+    f32x16 acc[3];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int tt = 0; tt < 3; ++tt)
 #pragma unroll
-        for (int tt = 0; tt < 3; ++tt) acc[m][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 16; ++r) acc[tt][r] = 0.f;
 
-    // dc staging: thread t owns channel sco = t % 64 and windows t/64 + 12*i
-    const int sco = tid & 63, sw0 = tid >> 6;
+    // dc staging, coalesced: element e = tid + 768*i of the band's [64 co][72 win] block (consecutive
+    // lanes = consecutive windows of one channel row); the transpose to [win][co] happens in the LDS
+    // write (stride 65 floats / 68 bytes: conflict-free).
     float sv[C2W_STG];
     int sc[C2W_STG];
-    float db_acc = 0.f;
+    float db_acc = 0.f;  // db2 partial: channel (tid & 63), windows 6*(tid >> 6) .. +5 of every band
     const int nunit = 2 * B;
     auto load_dc = [&](int u) {
         if (u < nunit) {
             const int bb = u >> 1, band = u & 1;
-            const size_t g0 = (size_t)bb * P_SAMPLE + sco * P_WIN + band * 72;
+            const float* dp0 = dpool + (size_t)bb * P_SAMPLE + band * 72;
+            const uint8_t* cd0 = code + (size_t)bb * P_SAMPLE + band * 72;
 #pragma unroll
             for (int i = 0; i < C2W_STG; ++i) {
-                sv[i] = dpool[g0 + sw0 + 12 * i];
-                sc[i] = code[g0 + sw0 + 12 * i];
+                const int e = tid + C2W_THREADS * i;
+                const int co = e / 72, w = e - co * 72;
+                sv[i] = dp0[co * P_WIN + w];
+                sc[i] = cd0[co * P_WIN + w];
             }
         }
     };
@@ -379,11 +408,19 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
         uint8_t* cdb = reinterpret_cast<uint8_t*>(bufp + C2W_IMG + C2W_DC);
 #pragma unroll
         for (int i = 0; i < C2W_STG; ++i) {
-            const int w = sw0 + 12 * i;
-            dcb[w * C2W_DSTR + sco] = sv[i];
-            cdb[w * C2W_CDSTR + sco] = (uint8_t)sc[i];
-            db_acc += (sc[i] != CODE_NONE) ? sv[i] : 0.f;
+            const int e = tid + C2W_THREADS * i;
+            const int co = e / 72, w = e - co * 72;
+            dcb[w * C2W_DSTR + co] = sv[i];
+            cdb[w * C2W_CDSTR + co] = (uint8_t)sc[i];
         }
+    };
+    auto db_accum = [&](const float* bufp) {  // fixed (channel, windows) per thread: deterministic
+        const float* dcb = bufp + C2W_IMG;
+        const uint8_t* cdb = reinterpret_cast<const uint8_t*>(bufp + C2W_IMG + C2W_DC);
+        const int co = tid & 63, w0 = 6 * (tid >> 6);
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            db_acc += (cdb[(w0 + k) * C2W_CDSTR + co] != CODE_NONE) ? dcb[(w0 + k) * C2W_DSTR + co] : 0.f;
     };
 
     int u = blockIdx.x;
@@ -392,66 +429,90 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
     if (u < nunit) write_dc(smem);
     __syncthreads();
 
+    const int q0 = h, q1 = 2 + h;  // pixel of this lane half in k steps t = 0, 1
+    float slk_abl_reg = (float)lane;
+    slk_keep(slk_abl_reg);
     int buf = 0;
 #pragma unroll 1
     for (; u < nunit; u += gridDim.x) {
         const int nu = u + gridDim.x;
         float* cur = smem + buf * C2W_BUF;
         float* nxt = smem + (buf ^ 1) * C2W_BUF;
-        if (nu < nunit) c2w_dma_band(act + (size_t)(nu >> 1) * A_SAMPLE + (nu & 1) * 12 * A_HW, nxt, wave, lane);
-        load_dc(nu);
+        if (!(SLK_ABL & 4) && nu < nunit) c2w_dma_band(act + (size_t)(nu >> 1) * A_SAMPLE + (nu & 1) * 12 * A_HW, nxt, wave, lane);
+        if (!(SLK_ABL & 36)) load_dc(nu);
+        db_accum(cur);
         const float* img = cur;
         const float* dcb = cur + C2W_IMG;
         const uint8_t* cdb = reinterpret_cast<const uint8_t*>(cur + C2W_IMG + C2W_DC);
 #pragma unroll 1
         for (int pyl = 0; pyl < 6; ++pyl) {
-            const float* dr = dcb + pyl * P_HW * C2W_DSTR + cp * 32 + c;
-            const uint8_t* cr = cdb + pyl * P_HW * C2W_CDSTR + cp * 32 + c;
+            const float* dr = dcb + pyl * P_HW * C2W_DSTR + ct * 32 + j;
+            const uint8_t* cr = cdb + pyl * P_HW * C2W_CDSTR + ct * 32 + j;
             const float* ir = img + 2 * pyl * A_HW;
+            // this wave's 6 windows of the row (px = 2i + kh): gather, then 36 MFMAs
+            float dv[6], bv[6][2][3];
+            int cd[6];
 #pragma unroll
-            for (int px = 0; px < P_HW; ++px) {
-                float av[2];
+            for (int i = 0; i < 6; ++i) {
+                const int px = 2 * i + kh;
+                dv[i] = SLK_LDS(dr[px * C2W_DSTR]);
+                cd[i] = SLK_LDS(cr[px * C2W_CDSTR]);
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const float dv = dr[px * C2W_DSTR + m * 16];
-                    const int cd = cr[px * C2W_CDSTR + m * 16];
-                    av[m] = (cd == g4) ? dv : 0.f;
-                }
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int tt = 0; tt < 3; ++tt) bv[i][t][tt] = SLK_LDS(ir[base[tt] + t * A_HW + 2 * px]);
+            }
+#if SLK_PIN_PHASES
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const float a0 = (cd[i] == q0) ? dv[i] : 0.f;
+                const float a1 = (cd[i] == q1) ? dv[i] : 0.f;
 #pragma unroll
                 for (int tt = 0; tt < 3; ++tt) {
-                    const float bv = ir[base[tt] + 2 * px];
-                    acc[0][tt] = mfma16x16x4(av[0], bv, acc[0][tt]);
-                    acc[1][tt] = mfma16x16x4(av[1], bv, acc[1][tt]);
+                    acc[tt] = mfma32x32x2(a0, bv[i][0][tt], acc[tt]);
+                    acc[tt] = mfma32x32x2(a1, bv[i][1][tt], acc[tt]);
                 }
             }
+#if SLK_PIN_PHASES
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
-        if (nu < nunit) write_dc(nxt);
+        if (!(SLK_ABL & 36) && nu < nunit) write_dc(nxt);
         __syncthreads();
         buf ^= 1;
     }
 
-    // db2: 12 partials per channel (threads co, co+64, ...) summed in fixed order via LDS
-    float* red = smem;  // all units done (last barrier passed)
+    // combine: K-half 1 waves park their tiles in LDS, K-half 0 waves add them (fixed order)
+    float* park = smem;  // 6 waves x 3 tiles x 16 regs x 64 lanes = 18432 floats
+    float* red = smem + 18432;
+    const int pw = wave >> 1;  // (ct, tg) pair index 0..5
+    if (kh == 1) {
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) park[((pw * 3 + tt) * 16 + r) * 64 + lane] = acc[tt][r];
+    }
     red[tid] = db_acc;
     __syncthreads();
     float* slab = slabs + (size_t)blockIdx.x * C2W_SLAB;
-    if (tid < C2) {
+    if (tid < C2) {  // the 12 window groups of channel tid, in order
         float s = 0.f;
         for (int k = 0; k < C2W_THREADS / C2; ++k) s += red[k * C2 + tid];
         slab[W2_N + tid] = s;
     }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
+    if (kh == 0) {
 #pragma unroll
         for (int tt = 0; tt < 3; ++tt) {
-            const int ntile = ntb + tt, tap = ntile >> 1, chalf = ntile & 1;
-            const int ci = chalf * 16 + c;
+            const int tap = 3 * tg + tt;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int co = (2 * cp + m) * 16 + g4 * 4 + r;
-                slab[co * K2 + ci * 9 + tap] = acc[m][tt][r];
+            for (int r = 0; r < 16; ++r) {
+                const int co = ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                slab[co * K2 + j * 9 + tap] = acc[tt][r] + park[((pw * 3 + tt) * 16 + r) * 64 + lane];
             }
         }
+    }
 }
 
 extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
