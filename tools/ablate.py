@@ -49,7 +49,17 @@ s = torch.cuda.current_stream().cuda_stream
 p = lambda t: P(t.data_ptr())  # noqa: E731
 
 def calls(L):
-    return {
+    extra = {}
+    if hasattr(L, "slk_conv2_dgrad_fc"):
+        L.slk_conv2_dgrad_fc.restype = ctypes.c_int
+        L.slk_conv2_wgrad_fc.restype = ctypes.c_int
+        extra = {
+            "fc_xent_nodp": lambda: L.slk_fc_xent(p(pooled), p(W3), p(b3), p(y), p(logits), p(loss_i), p(dl), None,
+                                                  ctypes.c_float(1.0 / B), None, B, P(s)),
+            "conv2_dgrad_fc": lambda: L.slk_conv2_dgrad_fc(p(dl), p(W3), p(code), p(W2), p(gcut), B, P(s)),
+            "conv2_wgrad_fc": lambda: L.slk_conv2_wgrad_fc(p(act), p(dl), p(W3), p(code), p(slabs), B, P(s)),
+        }
+    return {**extra,
         "conv2_fwd_pool": lambda: L.slk_conv2_fwd_pool(p(act), p(W2), p(b2), p(pooled), p(code), B, P(s)),
         "fc_xent": lambda: L.slk_fc_xent(p(pooled), p(W3), p(b3), p(y), p(logits), p(loss_i), p(dl), p(dp2),
                                          ctypes.c_float(1.0 / B), None, B, P(s)),
