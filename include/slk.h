@@ -135,6 +135,14 @@ int slk_loss_sum(const float* values, int n, float scale, float* out, void* stre
 int slk_loss_log(const float* values, int n, float scale, float* ring, int capacity, int* counter,
                  void* stream);
 
+/* MNIST batch from the HBM-resident u8 dataset (replaces DataLoader(batch_size=64, shuffle=True)
+ * over torchvision MNIST + ToTensor + Normalize((0.1307,),(0.3081,)), src/client_part.py:61-64,98):
+ * x[s] = ((float)images[idx[s]] / 255 - mean) / std as f32 [B,1,28,28], y[s] = labels[idx[s]] (i64).
+ * images: [n_images][784] u8 (4-byte aligned); x 16-byte aligned. An idx outside [0, n_images)
+ * sets *err_flag (if non-null) and reads image 0. Bit-identical to the torchvision transform. */
+int slk_mnist_batch(const uint8_t* images, const uint8_t* labels, int n_images, const int64_t* idx,
+                    int B, float mean, float std, float* x, int64_t* y, int* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

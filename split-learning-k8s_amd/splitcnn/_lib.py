@@ -41,6 +41,7 @@ _SIGS = {
     "slk_sgd": [_P, _P, _I, _F, _P],
     "slk_loss_sum": [_P, _I, _F, _P, _P],
     "slk_loss_log": [_P, _I, _F, _P, _I, _P, _P],
+    "slk_mnist_batch": [_P, _P, _I, _P, _I, _F, _F, _P, _P, _P, _P],
 }
 _RESTYPES = {"slk_error_string": ctypes.c_char_p}
 

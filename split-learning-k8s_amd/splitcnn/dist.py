@@ -19,8 +19,10 @@ device-resident exchange here:
       the server runs every slice as it arrives (accumulating its gradient), returns each client
       its cut-gradient slice, and the clients all-reduce their 320-float gradient before stepping
       (= the reference step at batch (N-1)*B on the concatenated inputs).
+  FedAvg (the reference's LEARNING_MODE=federated): full-model local training per
+      rank, then one all-reduce of the sample-weighted parameters per round.
 
-All three are exactly the reference's step at their global batch (the mean loss scale 1/global is
+The first three are exactly the reference's step at their global batch (the mean loss scale 1/global is
 applied inside the cross-entropy kernel), so they share the single-process oracle. The stage
 objects only need: client.forward / backward / step / grads / bind_grads and server.compute / step /
 grads / bind_grads / log_loss (engine.ClientStage / engine.ServerStage on GPU; oracle-backed
@@ -216,6 +218,58 @@ class Hub:
             w.wait()
         self.exchange_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
         self.global_step += 1
+
+
+class FedAvg:
+    """Federated learning round: each rank trains the FULL model locally on its own
+    batches (src/client_part.py:143-170: forward, CE, backward, SGD per batch — on one GPU that is the
+    split step with the cut in place), then `aggregate()` replaces the reference's state_dict POST +
+    identity `load_state_dict` (client_part.py:172-195, server_part.py:81-93) by ONE all-reduce of
+    [n_k * params | n_k | n_k * mean local loss] and a device-side divide: sample-weighted FedAvg,
+    no host sync. With one rank it is exactly the reference's single-client round.
+
+    The aggregated client loss is logged for `step` like server_part.py:84 (mlflow.log_metric)."""
+
+    def __init__(self, client, server, group=None, device=None):
+        self.client, self.server = client, server
+        self.group = group
+        dev = device if device is not None else client.params.device
+        self.n = CLIENT_N + SERVER_N
+        self.bucket = torch.zeros(self.n + 2, dtype=client.params.dtype, device=dev)
+        self.loss_acc = torch.zeros(1, dtype=client.params.dtype, device=dev)
+        self._loss_tmp = torch.zeros(1, dtype=client.params.dtype, device=dev)
+        self.samples = 0   # n_k of the current round (host count: no sync)
+        self.batches = 0
+
+    def local_step(self, x, y):
+        B = x.shape[0]
+        act = self.client.forward(x)
+        cut, loss_i = self.server.compute(act, y, 1.0 / B)
+        self.client.backward(cut)
+        self.client.step()
+        self.server.step()
+        _loss_sum(loss_i, 1.0 / B, self._loss_tmp)
+        self.loss_acc += self._loss_tmp     # epoch_loss += loss.item() without the per-step sync
+        self.samples += B
+        self.batches += 1
+
+    def aggregate(self, step: Optional[int] = None, weight: Optional[float] = None):
+        """All-reduce the sample-weighted parameters; every rank leaves with the FedAvg model."""
+        w = float(self.samples if weight is None else weight)
+        C = CLIENT_N
+        b = self.bucket
+        torch.mul(self.client.params, w, out=b[:C])
+        torch.mul(self.server.params, w, out=b[C:self.n])
+        b[self.n].fill_(w)
+        torch.mul(self.loss_acc, w / max(self.batches, 1), out=b[self.n + 1:])
+        dist.all_reduce(b, group=self.group)
+        wsum = b[self.n:self.n + 1]
+        torch.div(b[:C], wsum, out=self.client.params)
+        torch.div(b[C:self.n], wsum, out=self.server.params)
+        torch.div(b[self.n + 1:], wsum, out=self._loss_tmp)
+        self.server.log_loss(self._loss_tmp, scale=1.0, step=step)
+        self.loss_acc.zero_()
+        self.samples = self.batches = 0
 
 
 def client_group_for(world: int):

@@ -133,6 +133,8 @@ class LossLog:
                 self.sink(step, loss)
         self._flushed = count
         self.history.extend(out)
+        if self.sink is not None and hasattr(self.sink, "flush"):
+            self.sink.flush()  # batching sinks (splitcnn.sinks) send once per flush
         return out
 
 

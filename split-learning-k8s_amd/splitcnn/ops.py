@@ -221,3 +221,22 @@ def loss_log(values, scale, ring, counter):
     n = values.numel()
     _lib.call("slk_loss_log", _dev(values, "values"), n, float(scale), _dev(ring, "ring"), ring.numel(),
               _dev(counter, "counter", (1,), torch.int32), _stream(values))
+
+
+# ------------------------------------------------------------------------------------ data
+MNIST_MEAN, MNIST_STD = 0.1307, 0.3081   # client_part.py:63
+
+
+def mnist_batch(images, labels, idx, x=None, y=None, err_flag=None, mean=MNIST_MEAN, std=MNIST_STD):
+    """Gather + ToTensor + Normalize one batch from the HBM-resident u8 dataset (slk_mnist_batch)."""
+    n = batch_of(images, (28, 28), "images")
+    if labels.shape != (n,):
+        raise ValueError(f"labels: expected shape ({n},), got {tuple(labels.shape)}")
+    B = int(idx.shape[0])
+    x = _out(x, (B, 1, 28, 28), images, name="x")
+    y = _out(y, (B,), images, dtype=torch.int64, name="y")
+    _lib.call("slk_mnist_batch", _dev(images, "images", dtype=torch.uint8),
+              _dev(labels, "labels", dtype=torch.uint8), n, _dev(idx, "idx", (B,), torch.int64), B,
+              float(mean), float(std), x.data_ptr(), y.data_ptr(),
+              None if err_flag is None else _dev(err_flag, "err_flag", (1,), torch.int32), _stream(x))
+    return x, y

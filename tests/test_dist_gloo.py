@@ -111,3 +111,73 @@ def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
         for k in ["W2", "b2", "W3", "b3"]:
             np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
         np.testing.assert_allclose(outs[r]["losses"], losses, rtol=1e-6)
+
+
+FED_B = (4, 2)     # unequal local batches: FedAvg weights must follow the sample counts
+FED_ROUNDS = (2, 1)  # local steps per round
+
+
+def _fed_batches(rank):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from splitcnn.data import SyntheticMNIST
+    d = SyntheticMNIST(100 + rank)
+    return [d.batch(FED_B[rank]) for _ in range(sum(FED_ROUNDS))]
+
+
+def _fed_worker(rank, world, port, outdir):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from oracle.stages import OracleClient, OracleServer
+    from splitcnn import dist as sd
+    try:
+        P = _init_params()
+        fed = sd.FedAvg(OracleClient(P), OracleServer(P), device=torch.device("cpu"))
+        it = iter(_fed_batches(rank))
+        step = 0
+        for r, nloc in enumerate(FED_ROUNDS):
+            for _ in range(nloc):
+                fed.local_step(*next(it))
+                step += 1
+            fed.aggregate(step=step - 1)
+        res = {**fed.client.named(), **fed.server.named(), "losses": [l for _, l in fed.server.losses],
+               "steps": [s for s, _ in fed.server.losses]}
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), **{k: np.asarray(v) for k, v in res.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fedavg_round_equals_weighted_average_of_local_training(tmp_path):
+    """client_part.py:143-195 per rank (full-model local SGD), then sample-weighted averaging in
+    place of server_part.py:81's identity load_state_dict; equal to the oracle run rank by rank."""
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from oracle.split_step import split_step
+    world = 2
+    mp.spawn(_fed_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    P = _init_params()
+    data = [iter(_fed_batches(r)) for r in range(world)]
+    want_losses = []
+    for nloc in FED_ROUNDS:
+        locals_, lsum = [], 0.0
+        for r in range(world):
+            Q = dict(P)
+            ls = []
+            for _ in range(nloc):
+                x, y = next(data[r])
+                Q, rec = split_step(Q, x.numpy(), y.numpy())
+                ls.append(rec["loss"])
+            locals_.append(Q)
+            lsum += FED_B[r] * nloc * np.mean(ls)
+        wts = np.array([FED_B[r] * nloc for r in range(world)], dtype=np.float64)
+        P = {k: sum(w * Q[k] for w, Q in zip(wts, locals_)) / wts.sum() for k in P}
+        want_losses.append(lsum / wts.sum())
+    outs = [dict(np.load(tmp_path / f"r{r}.npz")) for r in range(world)]
+    for r in range(world):
+        for k in P:
+            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-9 * np.abs(P[k]).max())
+        np.testing.assert_allclose(outs[r]["losses"], want_losses, rtol=1e-9)
+        assert list(outs[r]["steps"]) == [FED_ROUNDS[0] - 1, sum(FED_ROUNDS) - 1]
