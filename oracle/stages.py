@@ -101,3 +101,65 @@ class OracleServer:
 
     def named(self):
         return _unflat(self.params, KEYS_S)
+
+
+class OracleUServer:
+    """conv2 trunk of the U-shape (splitcnn/ushaped.py UServerStage) in float64."""
+
+    def __init__(self, params, lr=O.LR):
+        self.params = _flat(params, ["W2", "b2"])
+        self.lr = lr
+        self._act = self._code = self._relu = None
+
+    def forward(self, act):
+        p = _unflat(self.params, ["W2", "b2"])
+        a = act.double().numpy()
+        r = O.relu(O.conv3x3(a, p["W2"], p["b2"]))
+        pooled, idx = O.maxpool2(r)
+        self._act, self._relu, self._code = a, r, O.route_code(pooled, idx)
+        return torch.from_numpy(pooled)
+
+    def backward_step(self, dpooled):
+        p = _unflat(self.params, ["W2", "b2"])
+        code = self._code
+        dpool = np.where(code < O.CODE_NONE, dpooled.double().numpy(), 0.0)
+        dc = O.maxpool2_bwd(dpool, np.minimum(code, 3), self._relu.shape)
+        dW2, db2 = O.conv3x3_wgrad(self._act, dc)
+        cut = O.conv3x3_dgrad(dc, p["W2"])
+        self.params -= self.lr * torch.from_numpy(np.concatenate([dW2.reshape(-1), db2]))
+        return torch.from_numpy(cut)
+
+    def named(self):
+        return _unflat(self.params, ["W2", "b2"])
+
+
+class OracleUClient:
+    """conv1 + fc1 head + CE of the U-shape (splitcnn/ushaped.py UClientStage) in float64."""
+
+    def __init__(self, params, lr=O.LR):
+        self.conv = OracleClient(params, lr)
+        self.params = _flat(params, ["W3", "b3"])
+        self.lr = lr
+        self.losses = []
+
+    def forward(self, x):
+        return self.conv.forward(x)
+
+    def head_step(self, pooled, labels, step=None):
+        p = _unflat(self.params, ["W3", "b3"])
+        pl = pooled.double().numpy()
+        B = pl.shape[0]
+        flat = pl.reshape(B, -1)
+        loss, _, dlogits = O.cross_entropy(flat @ p["W3"].T + p["b3"], labels.numpy())
+        dflat = dlogits @ p["W3"]
+        g = np.concatenate([(dlogits.T @ flat).reshape(-1), dlogits.sum(axis=0)])
+        self.params -= self.lr * torch.from_numpy(g)
+        self.losses.append((step, float(loss)))
+        return torch.from_numpy(dflat.reshape(pl.shape))
+
+    def backward_step(self, cut_grad):
+        self.conv.backward(cut_grad)
+        self.conv.step()
+
+    def named(self):
+        return {**self.conv.named(), **_unflat(self.params, ["W3", "b3"])}

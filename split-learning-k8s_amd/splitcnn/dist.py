@@ -272,6 +272,53 @@ class FedAvg:
         self.samples = self.batches = 0
 
 
+class UShaped:
+    """Label-private U-shape on 2 ranks (splitcnn/ushaped.py): rank `client` holds conv1 + fc1 +
+    labels, rank `server` the conv2 trunk. Four tensors cross per step — act and dpooled
+    client -> server, pooled and cut_grad server -> client; labels never leave the client."""
+
+    def __init__(self, stage, role: str, peer: int, group=None):
+        assert role in ("client", "server")
+        self.stage, self.role, self.peer, self.group = stage, role, peer, group
+        self.global_step = 0
+        self._bufs = {}
+        self.exchange_bytes = 0
+
+    def _buf(self, name, shape, dtype, device):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != device:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self._bufs[name] = t
+        return t
+
+    def client_step(self, x, y):
+        B, dev, c = x.shape[0], x.device, self.stage
+        act = c.forward(x)
+        dist.send(act, self.peer, group=self.group)
+        pooled = self._buf("pooled", (B, 64, 12, 12), act.dtype, dev)
+        dist.recv(pooled, self.peer, group=self.group)
+        dpooled = c.head_step(pooled, y, step=self.global_step)
+        dist.send(dpooled, self.peer, group=self.group)
+        cut = self._buf("cut", (B, 32, 26, 26), act.dtype, dev)
+        dist.recv(cut, self.peer, group=self.group)
+        c.backward_step(cut)
+        self.exchange_bytes = 2 * (act.numel() + pooled.numel()) * act.element_size()
+        self.global_step += 1
+
+    def server_step(self, B: int, device, dtype=torch.float32):
+        s = self.stage
+        act = self._buf("act", (B, 32, 26, 26), dtype, device)
+        dist.recv(act, self.peer, group=self.group)
+        pooled = s.forward(act)
+        dist.send(pooled, self.peer, group=self.group)
+        dpooled = self._buf("dpooled", (B, 64, 12, 12), dtype, device)
+        dist.recv(dpooled, self.peer, group=self.group)
+        cut = s.backward_step(dpooled)
+        dist.send(cut, self.peer, group=self.group)
+        self.exchange_bytes = 2 * (act.numel() + pooled.numel()) * act.element_size()
+        self.global_step += 1
+
+
 def client_group_for(world: int):
     """The all-reduce group of the hub's client ranks (every rank must call this, in order)."""
     if world < 3:

@@ -66,6 +66,19 @@ def _worker(rank, world, port, topo, outdir):
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"))
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
+        elif topo == "ushaped":
+            from oracle.stages import OracleUClient, OracleUServer
+            batches = _batches(B)
+            if rank == 0:
+                t = sd.UShaped(OracleUClient(P), "client", 1)
+                for x, y in batches:
+                    t.client_step(x, y)
+                res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
+            else:
+                t = sd.UShaped(OracleUServer(P), "server", 0)
+                for _ in batches:
+                    t.server_step(B, torch.device("cpu"), dtype=torch.float64)
+                res = t.stage.named()
         elif topo == "hub":
             batches = _batches((world - 1) * B)
             grp = sd.client_group_for(world)
@@ -97,21 +110,28 @@ def _reference(global_batch):
     return P, losses
 
 
-@pytest.mark.parametrize("topo,world,gb", [("replicated", 2, 2 * B), ("pipeline", 2, B), ("hub", 3, 2 * B)])
+@pytest.mark.parametrize("topo,world,gb", [("replicated", 2, 2 * B), ("pipeline", 2, B), ("hub", 3, 2 * B),
+                                           ("ushaped", 2, B)])
 def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
     mp.spawn(_worker, args=(world, _port(), topo, str(tmp_path)), nprocs=world, join=True)
     P, losses = _reference(gb)
     outs = [dict(np.load(tmp_path / f"r{r}.npz")) for r in range(world)]
-    client_ranks = range(world) if topo == "replicated" else range(world - 1)
-    server_ranks = range(world) if topo == "replicated" else [world - 1]
-    for r in client_ranks:
-        for k in ["W1", "b1"]:
-            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
-    for r in server_ranks:
-        for k in ["W2", "b2", "W3", "b3"]:
-            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
-        np.testing.assert_allclose(outs[r]["losses"], losses, rtol=1e-6)
-
+    if topo == "ushaped":   # labels, fc1 and the loss live on the client (rank 0)
+        want = {0: ["W1", "b1", "W3", "b3", "losses"], 1: ["W2", "b2"]}
+    else:
+        client_ranks = range(world) if topo == "replicated" else range(world - 1)
+        server_ranks = range(world) if topo == "replicated" else [world - 1]
+        want = {r: [] for r in range(world)}
+        for r in client_ranks:
+            want[r] += ["W1", "b1"]
+        for r in server_ranks:
+            want[r] += ["W2", "b2", "W3", "b3", "losses"]
+    for r, keys in want.items():
+        for k in keys:
+            if k == "losses":
+                np.testing.assert_allclose(outs[r]["losses"], losses, rtol=1e-6)
+            else:
+                np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
 
 FED_B = (4, 2)     # unequal local batches: FedAvg weights must follow the sample counts
 FED_ROUNDS = (2, 1)  # local steps per round
