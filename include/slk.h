@@ -143,6 +143,70 @@ int slk_loss_log(const float* values, int n, float scale, float* ring, int capac
 int slk_mnist_batch(const uint8_t* images, const uint8_t* labels, int n_images, const int64_t* idx,
                     int B, float mean, float std, float* x, int64_t* y, int* err_flag, void* stream);
 
+
+/* ================================================================ widened split CNN (BASELINE config 5)
+ * The reference has no such model: these entry points run the north star's
+ * widened config — client conv1 3->64 (32x32) + ReLU, conv2 64->128 + ReLU + pool, conv3 128->256 +
+ * ReLU + pool (the cut, [B,256,8,8]); server Dropout(0.25) + Linear(16384,10) + cross-entropy; Adam —
+ * behind the same step contract (client_part.py:110-138 <-> server_part.py:25-58). Oracle:
+ * oracle/wide_step.py. Activations are bf16 in the "C8" layout [B][C/8][H][W][8] (8 channels of one
+ * pixel = one 16-byte chunk); routing codes are u8 in the same layout (0..3 = argmax position in the
+ * 2x2 window, first max wins; 4 = ReLU-blocked). Weight masters are f32 in torch layout; the MFMA
+ * convolutions read bf16 shadows built by slk_wide_shadows:
+ *   w2f [tap][ci/8][co][8] (128x64)   w2d [8-tap][co/8][ci][8]
+ *   w3f [co/128][tap][ci/8][co%128][8] (256x128)   w3d [8-tap][co/8][ci][8]
+ * Client flat block: [W1 1728 | b1 64 | W2 73728 | b2 128 | W3 294912 | b3 256]; server: [Wf | bf]. */
+#define SLK_WIDE_CLIENT_NPARAM 370816
+#define SLK_WIDE_SERVER_NPARAM 163850
+
+/* a1 = bf16(relu(conv1(x))), x f32 NCHW [B,3,32,32]; f32 VALU (K = 27). */
+int slk_wide_conv1_fwd(const float* x, const float* W1, const float* b1, uint16_t* a1, int B, void* stream);
+/* p2, code2 = pool(relu(conv2(a1) + b2)) — bf16 MFMA implicit GEMM, f32 accumulation. */
+int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2, uint16_t* p2, uint8_t* code2,
+                       int B, void* stream);
+/* cut, code3 = pool(relu(conv3(p2) + b3)). The cut is what the client sends (client_part.py:117-125). */
+int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const float* b3, uint16_t* cut, uint8_t* code3,
+                       int B, void* stream);
+/* Server: dropout (hash of seed, *step, sample, feature; keep iff hash >= keep_threshold, kept values
+ * scaled by keep_scale), fc forward, cross-entropy forward+backward (dlogits scaled by grad_scale) and
+ * the cut gradient dcut = keep * keep_scale * dlogits @ Wf (bf16, C8). wf8 = slk_wide_fc_shadow(Wf).
+ * Replaces server_part.py:48-51 + the cut-gradient return (:57) for the widened model. */
+int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
+                  unsigned seed, unsigned keep_threshold, float keep_scale, float grad_scale, float* logits,
+                  float* loss_i, float* dlogits, uint16_t* dcut, int* err_flag, int B, void* stream);
+/* fc weight-gradient slabs [slk_wide_fc_wgrad_nslab(B)][163850] = [dWf (torch layout) | dbf]. */
+int slk_wide_fc_wgrad(const uint16_t* cut, const float* dlogits, const int* step, unsigned seed,
+                      unsigned keep_threshold, float keep_scale, float* slabs, int B, void* stream);
+int slk_wide_fc_wgrad_nslab(int B);
+/* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
+ * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
+ * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs
+ * [nslab][1728 + 64]. Slabs are [dW (torch layout) | db] and reduce in fixed order. */
+int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream);
+int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream);
+int slk_wide_conv3_wgrad_nslab(int B);
+int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, const uint8_t* code2, uint16_t* dc2, int B,
+                         void* stream);
+int slk_wide_conv2_wgrad(const uint16_t* dc2, const uint16_t* a1, float* slabs, int B, void* stream);
+int slk_wide_conv2_wgrad_nslab(int B);
+int slk_wide_conv2_dgrad(const uint16_t* dc2, const uint16_t* w2d, const uint16_t* a1, uint16_t* da1m, int B,
+                         void* stream);
+int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream);
+int slk_wide_conv1_wgrad_nslab(int B);
+
+/* Fixed-order slab reduction + torch.optim.Adam step (amsgrad off, no weight decay) on n floats:
+ * t = *step + 1; grad (if non-null) receives the reduced gradient. Replaces optimizer.step() for the
+ * widened config (the north star's "fused SGD/Adam"). */
+int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab, int n,
+                        float lr, float beta1, float beta2, float eps, const int* step, void* stream);
+/* Rebuild the bf16 conv weight shadows from the f32 masters W2 [128,64,3,3], W3 [256,128,3,3]. */
+int slk_wide_shadows(const float* W2, const float* W3, uint16_t* w2f, uint16_t* w2d, uint16_t* w3f, uint16_t* w3d,
+                     void* stream);
+/* wf8[j][(plane*64+pix)*8+k] = Wf[j][(plane*8+k)*64+pix]: the fc weight in the cut's C8 order. */
+int slk_wide_fc_shadow(const float* wf, float* wf8, void* stream);
+/* ++*counter on the device (the per-stage step counter a captured HIP graph advances). */
+int slk_tick(int* counter, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

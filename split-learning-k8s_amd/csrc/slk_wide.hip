@@ -1,0 +1,738 @@
+// slk_wide.hip — the WIDENED split CNN (BASELINE.json config 5, "K5") on gfx950 bf16 MFMA.
+//
+// Model (oracle/wide_step.py restates it): client conv1 3->64 (32x32) + ReLU, conv2 64->128 + ReLU +
+// pool, conv3 128->256 + ReLU + pool -> cut [B,256,8,8]; server Dropout(0.25) + Linear(16384,10) +
+// cross-entropy; Adam on both sides. The reference has no such model: it keeps
+// the reference's step contract (src/client_part.py:110-138 <-> src/server_part.py:25-58) with the
+// channel widths at which a 3x3 convolution is a real contraction (K = 9*Cin = 576 .. 2304).
+//
+// Activation layout in HBM ("C8"): bf16 [B][C/8][H][W][8] — eight channels of one pixel are one
+// 16-byte chunk, and a chunk plane [H][W][8] is contiguous, so an image row of one chunk is one
+// coalesced run and a 16x16x32 MFMA operand fragment (8 consecutive K = channels) is one 16-byte read.
+//
+// conv3x3 (pad 1) forward and input-gradient ("dgrad") are one implicit-GEMM kernel:
+//   out[m][px] = sum_{tap, c} A[tap][c][m] * In[c][px + off(tap)]
+// with A = the bf16 weight shadow (forward: W[co][ci][tap]; dgrad: W[co][ci][8 - tap], m = ci) and In
+// the activation (forward) or the unpooled output gradient (dgrad). A workgroup (4 waves, 2 per CU)
+// owns MT output channels x NPX pixels (TR whole image rows); each wave a 64 x 64 sub-tile as
+// 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators. The input tile of one 32-channel group is staged in
+// LDS with its 1-pixel halo as [4 chunks][(TR+2)*(W+2) pixels][16 B] by LDS-DMA (halo lanes read a
+// static zero block), so all 9 taps read it with a constant offset and every fragment read is a
+// conflict-free ds_read_b128 (16 consecutive pixels of one chunk = 256 contiguous bytes). The weight
+// slice of each (group, tap) step [4 chunks][MT][16 B] streams through a 3-slot LDS ring two steps
+// ahead; the next group's input tile streams into the other input slot during the current group.
+// One counted `s_waitcnt vmcnt` + one barrier per step; the stream continues across tiles.
+// Epilogues: forward = bias + ReLU + 2x2 max-pool in registers (vertical pairs are sibling
+// accumulators, horizontal pairs neighbouring lanes) -> pooled bf16 + routing code; dgrad of conv3 =
+// max-pool backward of conv2 (route to the code's position, bf16) -> conv2's unpooled output gradient;
+// dgrad of conv2 = ReLU mask of a1 -> the gradient conv1's wgrad consumes.
+#include "slk_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+namespace wide {
+constexpr int IMG = 32;                 // input 3 x 32 x 32
+constexpr int C1 = 64, C2 = 128, C3 = 256;
+constexpr int CUT = C3 * 8 * 8;         // 16384 features per sample
+constexpr int NCLS = 10;
+constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_UNPOOL = 1, MODE_DGRAD_MASK = 2;
+}  // namespace wide
+
+__device__ __attribute__((aligned(64))) uint32_t slk_wide_zero[64];  // zero source for halo lanes
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    const __bf16 x = (__bf16)a, y = (__bf16)b;
+    return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+__device__ __forceinline__ float dpp_xor1(float v) {
+    // quad_perm [1,0,3,2]: lane l reads lane l^1
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// ----------------------------------------------------------------------------- conv geometry
+template <int CI_, int CO_, int HW_, int MT_, int MODE_>
+struct ConvCfg {
+    static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = MT_, MODE = MODE_;
+    static constexpr int NPX = MT == 128 ? 128 : 256;       // pixels per tile (4 waves of 64 x 64)
+    static constexpr int WN = NPX / 64;                     // waves along pixels
+    static constexpr int TR = NPX / HW;                     // image rows per tile
+    static constexpr int PW = HW + 2;                       // LDS row pitch (pixels, with halo)
+    static constexpr int NP = (TR + 2) * PW;
+    static constexpr int NPP = (NP + 63) / 64 * 64;         // pixels per chunk plane in LDS
+    static constexpr int ND = NPP / 64;                     // LDS-DMA instructions per chunk plane
+    static constexpr int G = CI / 32;                       // 32-channel groups (one MFMA K each)
+    static constexpr int S = G * 9;                         // steps per tile
+    static constexpr int IN_SLOT = NPP * 64;                // bytes: 4 chunks x NPP x 16
+    static constexpr int W_SLOT = MT * 64;                  // bytes: 4 chunks x MT x 16
+    static constexpr int NW = W_SLOT / 1024 / 4;            // weight DMA instructions per wave per step
+    static constexpr int L = 2;                             // weight lookahead (steps)
+    static constexpr int RW = L + 1;                        // weight ring slots
+    static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
+    static constexpr int RB = HW / TR;                      // row blocks per image
+    static constexpr int NCB = CO / MT;                     // output-channel blocks
+    static constexpr int FPR = HW / 16;                     // 16-pixel fragments per image row
+    static_assert(MT == 128 || MT == 64, "MT");
+    static_assert(HW % TR == 0 && TR % 2 == 0 && (64 % HW == 0 || HW == 64), "tile rows");
+    static_assert(NW >= 1 && (W_SLOT % 4096) == 0, "weight slot must split over 4 waves");
+    static_assert(NCB == 1 || NCB == 2, "NCB");
+};
+
+struct TileState {
+    int valid, n, rb, cob;
+};
+
+template <class C>
+__device__ __forceinline__ TileState tile_state(int t, int B) {
+    // XCD-aware: with NCB = 2 the two channel blocks of a pixel tile are tiles t and t + 8, i.e.
+    // blocks b and b + 8 of a grid that is a multiple of 16 — the same XCD under round-robin
+    // placement, so the second reads the input tile from L2. (Speed only; any placement is correct.)
+    TileState s;
+    int pt;
+    if (C::NCB == 2) {
+        s.cob = (t >> 3) & 1;
+        pt = ((t >> 4) << 3) | (t & 7);
+    } else {
+        s.cob = 0;
+        pt = t;
+    }
+    s.valid = pt < B * C::RB;
+    s.n = pt / C::RB;
+    s.rb = pt - s.n * C::RB;
+    return s;
+}
+
+template <class C>
+__device__ __forceinline__ void tile_poff(const TileState& s, int lane, int (&poff)[C::ND]) {
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) {
+        const int P = d * 64 + lane;
+        const int ry = P / C::PW, rx = P - (P / C::PW) * C::PW;
+        const int y = s.rb * C::TR - 1 + ry, x = rx - 1;
+        const bool ok = P < C::NP && y >= 0 && y < C::HW && x >= 0 && x < C::HW;
+        poff[d] = ok ? y * C::HW + x : -1;
+    }
+}
+
+// input tile of group g (chunks 4g .. 4g+3) -> LDS slot; wave w moves chunk plane w
+template <class C>
+__device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, const TileState& s,
+                                            const int (&poff)[C::ND], int g, char* slot, int wave, int lane) {
+    const char* plane = reinterpret_cast<const char*>(in) +
+                        ((size_t)(s.n * (C::CI / 8) + g * 4 + wave) * (C::HW * C::HW)) * 16;
+    const char* zero = reinterpret_cast<const char*>(slk_wide_zero);
+    char* dst = slot + wave * C::NPP * 16;
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) {
+        const char* src = poff[d] >= 0 ? plane + (size_t)poff[d] * 16 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + d * 1024), 16, 0, 0);
+    }
+}
+
+// weight slice of step (cob, g, tap) -> LDS slot; wave w moves NW consecutive KiB
+template <class C>
+__device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, int cob, int sl, char* slot,
+                                             int wave, int lane) {
+    const int g = sl / 9, tap = sl - (sl / 9) * 9;
+    const char* src = reinterpret_cast<const char*>(wsh) +
+                      ((size_t)((cob * 9 + tap) * (C::CI / 8) + g * 4) * C::MT) * 16;
+#pragma unroll
+    for (int i = 0; i < C::NW; ++i) {
+        const int j = wave * C::NW + i;
+        __builtin_amdgcn_global_load_lds((const void*)(src + j * 1024 + lane * 16), (lds_ptr_t)(slot + j * 1024), 16, 0, 0);
+    }
+}
+
+// aux: forward = bias (f32 [CO]); dgrad-unpool = code2 (u8, C8 [B][CO/8][HW][HW][8]);
+//      dgrad-mask = a1 (bf16, C8 [B][CO/8][HW][HW][8]).
+// out: forward = pooled bf16 C8 [B][CO/8][HW/2][HW/2][8] (+ code u8 same layout in out2);
+//      dgrad-unpool = bf16 C8 [B][CO/8][2HW][2HW][8]; dgrad-mask = bf16 C8 [B][CO/8][HW][HW][8].
+template <class C>
+__global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __restrict__ in,
+                                                           const uint16_t* __restrict__ wsh,
+                                                           const void* __restrict__ aux,
+                                                           uint16_t* __restrict__ out,
+                                                           uint8_t* __restrict__ out2, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+    char* islot0 = smem;
+    char* wslot0 = smem + 2 * C::IN_SLOT;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave - (wave / C::WN) * C::WN;
+    const int grid = gridDim.x;
+
+    int t = blockIdx.x;
+    TileState cur = tile_state<C>(t, B);
+    if (!cur.valid) return;
+    int tn = t + grid;
+    TileState nxt = tile_state<C>(tn, B);
+    int pcur[C::ND], pnxt[C::ND];
+    tile_poff<C>(cur, lane, pcur);
+    tile_poff<C>(nxt, lane, pnxt);
+
+    // per-lane fragment read offsets (bytes, relative to the slot)
+    const int a_off = ((lane >> 4) * C::MT + wm * 64 + (lane & 15)) * 16;
+    int b_off[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int q = wn * 64 + f * 16 + (lane & 15);
+        const int r = q / C::HW, x = q - (q / C::HW) * C::HW;
+        b_off[f] = ((lane >> 4) * C::NPP + (r + 1) * C::PW + x + 1) * 16;
+    }
+
+    float bias[4][4];
+    if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+        const float* b = reinterpret_cast<const float*>(aux);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[i][r] = b[cur.cob * C::MT + wm * 64 + i * 16 + 4 * (lane >> 4) + r];
+    }
+
+    // prologue: input group 0 of the first tile, then weight steps 0 .. L-1
+    issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
+#pragma unroll
+    for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
+
+    int wslot = 0;   // ring slot of the current step
+    int islot = 0;   // input slot of the current group
+#pragma unroll 1
+    while (true) {
+        const bool tail = !nxt.valid;
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+        for (int g = 0; g < C::G; ++g) {
+            const char* ib = islot0 + islot * C::IN_SLOT;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                // this step's weight slice (and, at tap 0, this group's input tile) has landed
+                if (tail) wait_vmcnt<0>();
+                else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::ND>();
+                else wait_vmcnt<(C::L - 1) * C::NW>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                // lookahead: weight step +L (ring slot of step -1, free since the barrier), then at
+                // tap 0 the next group's input tile (slot of group -1)
+                {
+                    const int sl = g * 9 + tap + C::L;
+                    int ws = wslot + C::L;
+                    ws = ws >= C::RW ? ws - C::RW : ws;
+                    if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                    else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
+                }
+                if (tap == 0) {
+                    char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
+                    if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
+                    else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
+                }
+                const char* wb = wslot0 + wslot * C::W_SLOT;
+                const int toff = ((tap / 3 - 1) * C::PW + (tap % 3 - 1)) * 16;
+                bf16x8 av[4], bv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const bf16x8*>(wb + a_off + i * 256);
+#pragma unroll
+                for (int f = 0; f < 4; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                        acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
+                wslot = wslot + 1 == C::RW ? 0 : wslot + 1;
+            }
+            islot ^= 1;
+        }
+
+        // ------------------------------------------------------------------ epilogue
+        const int ch_base = cur.cob * C::MT + wm * 64 + 4 * (lane >> 4);
+        if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+            constexpr int PH = C::HW / 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ch0 = ch_base + i * 16;
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    if ((f / C::FPR) & 1) continue;       // bottom row of a window pair
+                    const int fb = f + C::FPR;
+                    float pv[4];
+                    uint32_t cw = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float v0 = acc[i][f][r] + bias[i][r];
+                        const float v2 = acc[i][fb][r] + bias[i][r];
+                        const float v1 = dpp_xor1(v0), v3 = dpp_xor1(v2);
+                        // torch CPU max-pool over relu(c): strict > scan, first max wins
+                        float best = v0 > 0.f ? v0 : 0.f;
+                        int idx = 0;
+                        const float r1 = v1 > 0.f ? v1 : 0.f, r2 = v2 > 0.f ? v2 : 0.f, r3 = v3 > 0.f ? v3 : 0.f;
+                        if (r1 > best) { best = r1; idx = 1; }
+                        if (r2 > best) { best = r2; idx = 2; }
+                        if (r3 > best) { best = r3; idx = 3; }
+                        pv[r] = best;
+                        cw |= (uint32_t)(best > 0.f ? idx : slk::CODE_NONE) << (8 * r);
+                    }
+                    if ((lane & 1) == 0) {
+                        const int q = wn * 64 + f * 16 + (lane & 15);
+                        const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
+                        const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * PH + (y >> 1)) * PH + (x >> 1)) * 8 + (ch0 & 7);
+                        *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+                        *reinterpret_cast<uint32_t*>(out2 + o) = cw;
+                    }
+                }
+            }
+        } else if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL) {
+            const uint8_t* code = reinterpret_cast<const uint8_t*>(aux);
+            constexpr int FH = 2 * C::HW;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ch0 = ch_base + i * 16;
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    const int q = wn * 64 + f * 16 + (lane & 15);
+                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
+                    const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
+                    const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + ((plane * C::HW + y) * C::HW + x) * 8 + (ch0 & 7));
+#pragma unroll
+                    for (int pos = 0; pos < 4; ++pos) {
+                        float v[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = ((cw >> (8 * r)) & 0xFF) == (uint32_t)pos ? acc[i][f][r] : 0.f;
+                        const size_t o = ((plane * FH + 2 * y + (pos >> 1)) * FH + 2 * x + (pos & 1)) * 8 + (ch0 & 7);
+                        *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                    }
+                }
+            }
+        } else {
+            const uint16_t* a1 = reinterpret_cast<const uint16_t*>(aux);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ch0 = ch_base + i * 16;
+#pragma unroll
+                for (int f = 0; f < 4; ++f) {
+                    const int q = wn * 64 + f * 16 + (lane & 15);
+                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
+                    const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
+                    const uint2 m = *reinterpret_cast<const uint2*>(a1 + o);
+                    // a1 > 0 (bf16): sign bit clear and not +0
+                    const float v0 = (int)(m.x << 16) > 0 ? acc[i][f][0] : 0.f;
+                    const float v1 = (int)(m.x & 0xFFFF0000u) > 0 ? acc[i][f][1] : 0.f;
+                    const float v2 = (int)(m.y << 16) > 0 ? acc[i][f][2] : 0.f;
+                    const float v3 = (int)(m.y & 0xFFFF0000u) > 0 ? acc[i][f][3] : 0.f;
+                    *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                }
+            }
+        }
+
+        if (tail) break;
+        cur = nxt;
+#pragma unroll
+        for (int d = 0; d < C::ND; ++d) pcur[d] = pnxt[d];
+        tn += grid;
+        nxt = tile_state<C>(tn, B);
+        tile_poff<C>(nxt, lane, pnxt);
+    }
+}
+
+using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL>;
+using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL>;
+using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK>;
+
+template <class C>
+static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux, uint16_t* out, uint8_t* out2,
+                       int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && in && wsh && aux && out);
+    if (C::MODE == wide::MODE_FWD_POOL) SLK_CHECK_ARG(out2 != nullptr);
+    if (B == 0) return 0;
+    const long ntiles = (long)B * C::RB * C::NCB;
+    long grid = 512;                                   // 2 workgroups per CU (256 CUs)
+    if (ntiles < grid) grid = C::NCB == 2 ? ((ntiles + 15) / 16) * 16 : ntiles;
+    hipLaunchKernelGGL(wide_conv_kernel<C>, dim3((unsigned)grid), dim3(256), 0, slk_stream(stream), in, wsh, aux,
+                       out, out2, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2, uint16_t* p2,
+                                  uint8_t* code2, int B, void* stream) {
+    return launch_conv<CfgConv2Fwd>(a1, w2f, b2, p2, code2, B, stream);
+}
+extern "C" int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const float* b3, uint16_t* cut,
+                                  uint8_t* code3, int B, void* stream) {
+    return launch_conv<CfgConv3Fwd>(p2, w3f, b3, cut, code3, B, stream);
+}
+extern "C" int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, const uint8_t* code2, uint16_t* dc2,
+                                    int B, void* stream) {
+    return launch_conv<CfgConv3Dgrad>(dc3, w3d, code2, dc2, nullptr, B, stream);
+}
+extern "C" int slk_wide_conv2_dgrad(const uint16_t* dc2, const uint16_t* w2d, const uint16_t* a1, uint16_t* da1m,
+                                    int B, void* stream) {
+    return launch_conv<CfgConv2Dgrad>(dc2, w2d, a1, da1m, nullptr, B, stream);
+}
+
+// ============================================================================ conv3x3 weight gradient
+// dW[co][ci][tap] = sum_{n,y,x} dC[n][co][y][x] * In[n][ci][y+ky-1][x+kx-1];  db[co] = sum dC.
+// GEMM M = co, N = (tap, ci), K = pixels. A workgroup (8 waves, 1 per CU) owns a 128-co x 64-ci block
+// of dW (all 9 taps) and a K-split share of the batch's (image, row-block) tiles; each wave holds
+// 64 co x (9 taps x 16 ci) = 4 x 9 accumulators of v_mfma_f32_16x16x32_bf16 (144 VGPRs). Both operands
+// need 8 consecutive PIXELS per lane while the C8 layout stores 8 consecutive CHANNELS per 16 bytes, so
+// the fragments come from LDS by ds_read_b64_tr_b16 (the hardware transpose read): dC tile
+// [16 chunks][TR*W pixels] and the input halo tile [8 chunks][(TR+2)*(W+2) pixels], chunk planes
+// padded to a stride of 64 mod 256 bytes so every 32-lane half of a transposed read hits 64 distinct
+// banks. The whole next tile streams in by LDS-DMA while the current one is on the MFMAs (2 buffers,
+// one wait + barrier per tile). db rides along as one MFMA per step against a ones fragment. Each
+// workgroup writes its partial dW/db into its own slab (torch layout [co][ci][3][3] | db), reduced in
+// fixed order by slk_reduce_slabs / slk_adam_from_slabs.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int CI_, int CO_, int HW_, int TR_>
+struct WgCfg {
+    static constexpr int CI = CI_, CO = CO_, HW = HW_, TR = TR_;
+    static constexpr int COB = 128, CIB = 64;
+    static constexpr int NCOB = CO / COB, NCIB = CI / CIB, NBLK = NCOB * NCIB;
+    static constexpr int NPX = TR * HW;                  // pixels per tile (K per tile)
+    static constexpr int NPXP = NPX + 4;                 // dC plane stride (pixels): 64 mod 256 bytes
+    static constexpr int PW = HW + 2;
+    static constexpr int NP = (TR + 2) * PW;
+    static constexpr int ND = (NP + 63) / 64;
+    static constexpr int NPI = ND * 64 + 4;              // input plane stride (pixels)
+    static constexpr int DC_BYTES = (COB / 8) * NPXP * 16;
+    static constexpr int IN_BYTES = (CIB / 8) * NPI * 16;
+    static constexpr int BUF = DC_BYTES + IN_BYTES;
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int KS = NPX / 32;                  // MFMA k-steps per tile
+    static constexpr int RB = HW / TR;
+    static constexpr int SLAB = CO * CI * 9 + CO;
+    static constexpr int KSPLIT = 256 / NBLK;            // one workgroup per CU
+    static_assert(NPX % 32 == 0 && (HW == 32 || HW == 16), "tile");
+    static_assert(DC_BYTES % 16 == 0 && ((NPX * 16) % 1024) == 0, "dC rows move in whole KiB");
+};
+
+template <class C>
+__global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __restrict__ dc,
+                                                            const uint16_t* __restrict__ in,
+                                                            float* __restrict__ slabs, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    // XCD-aware block placement: the NBLK blocks of one K-split share sit 8 workgroups apart
+    const int w = blockIdx.x;
+    int blk, ks;
+    if (C::NBLK == 1) { blk = 0; ks = w; }
+    else { blk = (w >> 3) % C::NBLK; ks = ((w >> 3) / C::NBLK) * 8 + (w & 7); }
+    const int cob = blk / C::NCIB, cib = blk - (blk / C::NCIB) * C::NCIB;
+    const int NT = B * C::RB;
+
+    // per-lane transposed-read bases (bytes within a buffer)
+    const int q = lane >> 4, ig = lane & 15, a = ig >> 2, p = ig & 3;
+    const int a_base = (((wm * 64 + 4 * p) >> 3) * C::NPXP + 8 * q + a) * 16 + (p & 1) * 8;
+    const int pl = 8 * q + a, r0 = pl / C::HW, x0 = pl % C::HW;
+    // wave wn owns input channels cib*64 + 16*wn .. +15 (chunks 2wn, 2wn+1) for all 9 taps
+    const int b_base = C::DC_BYTES + (((2 * wn + (p >> 1)) * C::NPI) + (r0 + 1) * C::PW + x0 + 1) * 16 + (p & 1) * 8;
+    const bool do_db = cib == 0;
+    const short one = 0x3F80;  // bf16 1.0
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(8))) short){one, one, one, one, one, one, one, one});
+
+    f32x4 acc[4][9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int u = 0; u < 9; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue_tile = [&](int t, char* buf) {
+        const int n = t / C::RB, rb = t - (t / C::RB) * C::RB;
+        // dC rows: 16 chunk planes x (NPX*16/1024) KiB, 4 pieces per wave
+        constexpr int PPC = C::NPX * 16 / 1024;
+#pragma unroll
+        for (int k = 0; k < (16 * PPC) / 8; ++k) {
+            const int piece = wave * ((16 * PPC) / 8) + k;
+            const int c = piece / PPC, part = piece - (piece / PPC) * PPC;
+            const char* src = reinterpret_cast<const char*>(dc) +
+                              (((size_t)(n * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
+                              part * 1024 + lane * 16;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + c * C::NPXP * 16 + part * 1024), 16, 0, 0);
+        }
+        // input halo tile: wave w moves chunk plane w (ND pieces), halo lanes read zeros
+        const char* plane = reinterpret_cast<const char*>(in) +
+                            ((size_t)(n * (C::CI / 8) + cib * 8 + wave) * (C::HW * C::HW)) * 16;
+#pragma unroll
+        for (int d = 0; d < C::ND; ++d) {
+            const int P = d * 64 + lane;
+            const int ry = P / C::PW, rx = P - (P / C::PW) * C::PW;
+            const int y = rb * C::TR - 1 + ry, x = rx - 1;
+            const bool ok = P < C::NP && y >= 0 && y < C::HW && x >= 0 && x < C::HW;
+            const char* src = ok ? plane + (size_t)(y * C::HW + x) * 16 : reinterpret_cast<const char*>(slk_wide_zero);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (lds_ptr_t)(buf + C::DC_BYTES + wave * C::NPI * 16 + d * 1024), 16, 0, 0);
+        }
+    };
+
+    int t = ks, b = 0;
+    if (t < NT) issue_tile(t, smem);
+#pragma unroll 1
+    for (; t < NT; t += C::KSPLIT) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + C::KSPLIT < NT) issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
+        const char* buf = smem + b * C::BUF;
+#pragma unroll
+        for (int j = 0; j < C::KS; ++j) {
+            typedef __attribute__((address_space(3))) bf16x4* lp4;
+            bf16x8 av[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const char* pa = buf + a_base + i * 2 * C::NPXP * 16 + j * 32 * 16;
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)pa);
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(pa + 64));
+                av[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+            if (do_db) {  // wave (wm, wn) sums co fragment wn
+                bf16x8 adb = av[0];
+#pragma unroll
+                for (int i = 1; i < 4; ++i) adb = wn == i ? av[i] : adb;
+                accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(adb, ones, accb, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 9; ++u) {               // u = tap
+                const int toff = ((u / 3 - 1) * C::PW + (u % 3 - 1)) * 16;
+                const char* pb = buf + b_base + toff + j * (32 / C::HW) * C::PW * 16;
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)pb);
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(pb + 64));
+                const bf16x8 bv = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][u], 0, 0, 0);
+            }
+        }
+        b ^= 1;
+    }
+
+    // partial dW / db -> slab ks (torch layout)
+    float* slab = slabs + (size_t)ks * C::SLAB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+            const int tap = u;
+            const int ci = cib * C::CIB + wn * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = cob * C::COB + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+                slab[((size_t)co * C::CI + ci) * 9 + tap] = acc[i][u][r];
+            }
+        }
+    }
+    if (do_db && (lane & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slab[C::CO * C::CI * 9 + cob * C::COB + wm * 64 + wn * 16 + 4 * (lane >> 4) + r] = accb[r];
+    }
+}
+
+using CfgWg2 = WgCfg<64, 128, 32, 4>;
+using CfgWg3 = WgCfg<128, 256, 16, 8>;
+
+template <class C>
+static int launch_wgrad(const uint16_t* dc, const uint16_t* in, float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && dc && in && slabs);
+    hipLaunchKernelGGL(wide_wgrad_kernel<C>, dim3(256), dim3(512), 0, slk_stream(stream), dc, in, slabs, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_wide_conv2_wgrad_nslab(int B) { return B >= 0 ? CfgWg2::KSPLIT : 0; }
+extern "C" int slk_wide_conv3_wgrad_nslab(int B) { return B >= 0 ? CfgWg3::KSPLIT : 0; }
+extern "C" int slk_wide_conv2_wgrad(const uint16_t* dc2, const uint16_t* a1, float* slabs, int B, void* stream) {
+    return launch_wgrad<CfgWg2>(dc2, a1, slabs, B, stream);
+}
+extern "C" int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream) {
+    return launch_wgrad<CfgWg3>(dc3, p2, slabs, B, stream);
+}
+
+// ============================================================================ conv1 (3 -> 64), f32
+// conv1 has K = 27, no real contraction: f32 VALU. One 256-thread workgroup per image stages the
+// image with its zero halo in LDS ([3][34][34] f32); each thread owns 4 pixels (tid + 256k) and loops
+// over the 64 output channels with that channel's 27 weights + bias in SGPRs (wave-uniform loop,
+// scalar loads), 108 FMAs per channel; each 8-channel chunk leaves as one 16-byte bf16 store per pixel.
+constexpr int C1P = 34;  // padded image pitch
+
+__device__ __forceinline__ void stage_image(const float* __restrict__ x, float* xs) {
+    // xs[ci][34][34] with zero border
+    for (int e = threadIdx.x; e < 3 * C1P * C1P; e += 256) {
+        const int ci = e / (C1P * C1P), r = e - ci * (C1P * C1P);
+        const int yy = r / C1P - 1, xx = r % C1P - 1;
+        xs[e] = (yy >= 0 && yy < 32 && xx >= 0 && xx < 32) ? x[(ci * 32 + yy) * 32 + xx] : 0.f;
+    }
+}
+
+__global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W1,
+                                                             const float* __restrict__ b1, uint16_t* __restrict__ a1) {
+    __shared__ float xs[3 * C1P * C1P];
+    const int n = blockIdx.x;
+    stage_image(x + (size_t)n * 3 * 1024, xs);
+    __syncthreads();
+    float xv[4][27];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = threadIdx.x + 256 * k, y = p >> 5, xx = p & 31;
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) xv[k][ci * 9 + t] = xs[(ci * C1P + y + t / 3) * C1P + xx + t % 3];
+    }
+#pragma unroll 1
+    for (int c = 0; c < 8; ++c) {
+        uint32_t pk[4][4];
+#pragma unroll 1
+        for (int u = 0; u < 8; u += 2) {  // one channel pair per iteration; shift it into pk
+            float o[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int co = c * 8 + u + h;
+                const float* w = W1 + co * 27;
+                const float bb = b1[co];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float acc = bb;
+#pragma unroll
+                    for (int i = 0; i < 27; ++i) acc = __builtin_fmaf(w[i], xv[k][i], acc);
+                    o[h][k] = acc > 0.f ? acc : 0.f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pk[k][0] = pk[k][1];
+                pk[k][1] = pk[k][2];
+                pk[k][2] = pk[k][3];
+                pk[k][3] = pack_bf16x2(o[0][k], o[1][k]);
+            }
+        }
+        uint16_t* dst = a1 + ((size_t)(n * 8 + c) * 1024) * 8;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<uint4*>(dst + (threadIdx.x + 256 * k) * 8) = make_uint4(pk[k][0], pk[k][1], pk[k][2], pk[k][3]);
+    }
+}
+
+// conv1 weight gradient from the ReLU-masked bf16 gradient da1m (conv2 dgrad's epilogue applied the
+// mask) and the f32 image: dW1[co][ci][tap] = sum_px da1m[co][px] * xpad[ci][px + off(tap)].
+// Grid = 16 channel quads x C1W_SPLIT batch slices; a thread owns 4 channels x 27 taps (+4 bias sums)
+// for 4 pixels of each image; the image is staged in LDS. Fixed-order wave/LDS reduction at the end;
+// one slab [1792] = [dW1 (torch layout) | db1] per batch slice.
+constexpr int C1W_SPLIT = 128;
+
+__global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __restrict__ x, const uint16_t* __restrict__ da1m,
+                                                               float* __restrict__ slabs, int B) {
+    __shared__ float xs[3 * C1P * C1P];
+    __shared__ float red[4][112];
+    const int cq = blockIdx.x & 15, split = blockIdx.x >> 4;
+    const int co0 = cq * 4;
+    float acc[4][27], accb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        accb[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 27; ++i) acc[j][i] = 0.f;
+    }
+#pragma unroll 1
+    for (int n = split; n < B; n += C1W_SPLIT) {
+        __syncthreads();
+        stage_image(x + (size_t)n * 3 * 1024, xs);
+        uint2 dv[4];
+        const uint16_t* src = da1m + ((size_t)(n * 8 + (co0 >> 3)) * 1024) * 8 + (co0 & 7);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[k] = *reinterpret_cast<const uint2*>(src + (threadIdx.x + 256 * k) * 8);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = threadIdx.x + 256 * k, y = p >> 5, xx = p & 31;
+            const float d[4] = {bf16_lo(dv[k].x), bf16_hi(dv[k].x), bf16_lo(dv[k].y), bf16_hi(dv[k].y)};
+            float xv[27];
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) xv[ci * 9 + t] = xs[(ci * C1P + y + t / 3) * C1P + xx + t % 3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                accb[j] += d[j];
+#pragma unroll
+                for (int i = 0; i < 27; ++i) acc[j][i] = __builtin_fmaf(d[j], xv[i], acc[j][i]);
+            }
+        }
+    }
+    // reduce 112 values over the workgroup: wave sums, then waves 0..3 in order
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int i = 0; i < 27; ++i) {
+            const float s = wave_sum(acc[j][i]);
+            if (lane == 0) red[wave][j * 27 + i] = s;
+        }
+        const float s = wave_sum(accb[j]);
+        if (lane == 0) red[wave][108 + j] = s;
+    }
+    __syncthreads();
+    float* slab = slabs + (size_t)split * 1792;
+    for (int e = threadIdx.x; e < 112; e += 256) {
+        const float s = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+        if (e < 108) slab[co0 * 27 + e] = s;          // [co][ci][ky][kx] = co*27 + ci*9 + tap
+        else slab[1728 + co0 + (e - 108)] = s;
+    }
+}
+
+extern "C" int slk_wide_conv1_fwd(const float* x, const float* W1, const float* b1, uint16_t* a1, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && x && W1 && b1 && a1);
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(wide_conv1_fwd_kernel, dim3(B), dim3(256), 0, slk_stream(stream), x, W1, b1, a1);
+    return slk_launch_status();
+}
+extern "C" int slk_wide_conv1_wgrad_nslab(int B) { return B >= 0 ? C1W_SPLIT : 0; }
+extern "C" int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && x && da1m && slabs);
+    hipLaunchKernelGGL(wide_conv1_wgrad_kernel, dim3(16 * C1W_SPLIT), dim3(256), 0, slk_stream(stream), x, da1m, slabs, B);
+    return slk_launch_status();
+}
+
+// ============================================================================ unpool of the cut gradient
+// dc3[b][c][2y+dy][2x+dx] = dcut[b][c][y][x] if code3 == 2dy+dx else 0 (max-pool backward of conv3's
+// pool with the ReLU folded into code 4). One thread per 8-channel chunk of one pooled pixel.
+__global__ __launch_bounds__(256) void wide_unpool_kernel(const uint16_t* __restrict__ dcut, const uint8_t* __restrict__ code,
+                                                          uint16_t* __restrict__ dc3, int nchunk) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nchunk) return;
+    const int plane = i >> 6, pix = i & 63, y = pix >> 3, xx = pix & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(dcut + (size_t)i * 8);
+    const uint2 c = *reinterpret_cast<const uint2*>(code + (size_t)i * 8);
+    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t cw[2] = {c.x, c.y};
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c0 = (cw[k >> 1] >> (16 * (k & 1))) & 0xFF, c1 = (cw[k >> 1] >> (16 * (k & 1) + 8)) & 0xFF;
+            o[k] = (c0 == (uint32_t)pos ? (vw[k] & 0xFFFFu) : 0u) | (c1 == (uint32_t)pos ? (vw[k] & 0xFFFF0000u) : 0u);
+        }
+        const size_t off = (((size_t)plane * 16 + 2 * y + (pos >> 1)) * 16 + 2 * xx + (pos & 1)) * 8;
+        *reinterpret_cast<uint4*>(dc3 + off) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+extern "C" int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && dcut && code3 && dc3);
+    if (B == 0) return 0;
+    const int nchunk = B * 32 * 64;
+    hipLaunchKernelGGL(wide_unpool_kernel, dim3((nchunk + 255) / 256), dim3(256), 0, slk_stream(stream), dcut, code3, dc3, nchunk);
+    return slk_launch_status();
+}

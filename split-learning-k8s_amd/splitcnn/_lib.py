@@ -18,6 +18,7 @@ _c_float_p = ctypes.c_void_p  # device pointers travel as integers
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
+_U = ctypes.c_uint
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 _SIGS = {
@@ -42,6 +43,26 @@ _SIGS = {
     "slk_loss_sum": [_P, _I, _F, _P, _P],
     "slk_loss_log": [_P, _I, _F, _P, _I, _P, _P],
     "slk_mnist_batch": [_P, _P, _I, _P, _I, _F, _F, _P, _P, _P, _P],
+    # widened split CNN (BASELINE config 5)
+    "slk_wide_conv1_fwd": [_P, _P, _P, _P, _I, _P],
+    "slk_wide_conv2_fwd": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_wide_conv3_fwd": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_wide_head": [_P, _P, _P, _P, _P, _U, _U, _F, _F, _P, _P, _P, _P, _P, _I, _P],
+    "slk_wide_fc_wgrad": [_P, _P, _P, _U, _U, _F, _P, _I, _P],
+    "slk_wide_fc_wgrad_nslab": [_I],
+    "slk_wide_unpool": [_P, _P, _P, _I, _P],
+    "slk_wide_conv3_wgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv3_wgrad_nslab": [_I],
+    "slk_wide_conv3_dgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_wide_conv2_wgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv2_wgrad_nslab": [_I],
+    "slk_wide_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_wide_conv1_wgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv1_wgrad_nslab": [_I],
+    "slk_adam_from_slabs": [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _P, _P],
+    "slk_wide_shadows": [_P, _P, _P, _P, _P, _P, _P],
+    "slk_wide_fc_shadow": [_P, _P, _P],
+    "slk_tick": [_P, _P],
 }
 _RESTYPES = {"slk_error_string": ctypes.c_char_p}
 

@@ -15,7 +15,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include")
 LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
-SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip"]
+SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip", "slk_wide.hip",
+           "slk_wide_head.hip"]
 ARCH = "gfx950"
 
 

@@ -1,0 +1,217 @@
+"""GPU parity of the widened split CNN (BASELINE config 5) against oracle/wide_step.py.
+
+Tolerances (the north star's "stated looser bound for bf16"):
+  * bf16 tensors (activations, pooled maps, cut gradient, unpooled/masked gradients): every element
+    equal to the oracle's bf16 rounding of the same math, except rare elements where the f32
+    accumulation order of the GPU and the oracle's float64 land on opposite sides of a bf16 rounding
+    boundary: those may differ by one bf16 ulp (<= 2^-7 relative) plus the f32 accumulation floor
+    (4e-6 x the tensor's max), and must be < 0.1 % of elements;
+  * max-pool routing codes: equal except numerical ties (the two candidates within 1e-5 of the
+    window's scale), as in the fp32 path (oracle.split_step.tie_discrepancies);
+  * weight gradients (f32 sums of exact bf16 x bf16 products): 1e-5 of the gradient's max;
+  * Adam (f32 tensor math, torch formula): 1e-6 of the update's max + 2 f32 ulp;
+  * loss curve over 30 steps: 2e-2 relative per step (SURVEY.md §8c's bf16 bound).
+Each kernel is checked on the GPU's own inputs of that layer (layer-isolated), so a rounding flip
+upstream cannot cascade into a false failure downstream.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import wide_step as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def _nchw(t):
+    from splitcnn.wide import c8_to_nchw
+    return _np(c8_to_nchw(t))
+
+
+def bf16_close(got, want, frac=1e-3, acc_floor=4e-6):
+    """One bf16 ulp where the rounding flipped, on top of the f32 accumulation noise floor
+    (acc_floor x the tensor's max: f32 sums of O(1) terms carry absolute, not relative, error)."""
+    got, want = np.asarray(got), np.asarray(want)
+    assert got.shape == want.shape, (got.shape, want.shape)
+    bad = got != want
+    if not bad.any():
+        return
+    d = np.abs(got - want)[bad]
+    lim = 2.0 ** -7 * np.abs(want)[bad] + acc_floor * np.abs(want).max() + 1e-30
+    assert (d <= lim * 1.0001).all(), f"max rel diff {np.max(d / np.maximum(np.abs(want[bad]), 1e-30)):.3g}"
+    assert bad.mean() <= frac, f"{bad.mean():.2e} of elements differ by one bf16 ulp"
+
+
+def codes_close(c_pre, code_got, code_want, rtol=1e-5):
+    """Routing differences must be numerical ties of the f32/f64 pre-pool values c_pre."""
+    diff = code_got != code_want
+    if not diff.any():
+        return
+    B, C, H, Wd = c_pre.shape
+    win = c_pre.reshape(B, C, H // 2, 2, Wd // 2, 2).transpose(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, Wd // 2, 4)
+    win = np.maximum(win, 0.0)[diff]
+    scale = max(np.abs(c_pre).max(), 1e-30)
+
+    def val(code):
+        return np.where(code < 4, np.take_along_axis(win, np.minimum(code, 3)[:, None], axis=1)[:, 0], 0.0)
+    va, vb = val(code_got[diff]), val(code_want[diff])
+    assert (np.abs(va - vb) <= rtol * scale).all(), f"{diff.sum()} non-tie routing differences"
+    assert diff.mean() < 1e-3
+
+
+def grad_close(got, want, rtol=1e-5):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    err = np.abs(got - want).max() / max(np.abs(want).max(), 1e-30)
+    assert err <= rtol, err
+
+
+def _params(client, server):
+    P = {}
+    for k, v in client.model.state_dict().items():
+        P[k] = _np(v)
+    for k, v in server.model.state_dict().items():
+        P[k] = _np(v)
+    return P
+
+
+def test_wide_step_layer_by_layer_vs_oracle(gpu):
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    A, Bm = init_wide_models(seed=0)
+    tr = WideTrainer(A, Bm, device=gpu, graph=False)
+    B = 5  # ragged: not a multiple of any tile
+    x, y = SyntheticCIFAR(42).batch(B)
+    c, s = tr.client, tr.server
+    P0 = _params(c, s)
+    cut = c.forward(x.to(gpu))
+    dcut, loss_i = s.step_request(cut, y.to(gpu))
+    grads_s = s.grads.clone()
+    c.backward_step(dcut)
+    torch.cuda.synchronize()
+    xs = x.double().numpy()
+    bf = lambda a: W.bf16(a).astype(np.float64)  # noqa: E731
+
+    # conv1 (f32 VALU) -> a1 bf16
+    a1 = _nchw(c._a1)
+    bf16_close(a1, bf(np.maximum(W.conv3x3p1(xs, P0["conv1.weight"], P0["conv1.bias"]), 0)))
+    # conv2 + pool on the GPU's a1
+    W2b, W3b = bf(P0["conv2.weight"]), bf(P0["conv3.weight"])
+    c2 = W.conv3x3p1(a1, W2b, P0["conv2.bias"])
+    p2f, code2 = W.relu_pool_code(c2)
+    code2_gpu = _nchw(c._code2).astype(np.int64)
+    codes_close(c2, code2_gpu, code2)
+    p2 = _nchw(c._p2)
+    p2f_g = np.take_along_axis(np.maximum(c2, 0).reshape(B, 128, 16, 2, 16, 2).transpose(0, 1, 2, 4, 3, 5)
+                               .reshape(B, 128, 16, 16, 4), np.minimum(code2_gpu, 3)[..., None], -1)[..., 0]
+    bf16_close(p2, bf(np.where(code2_gpu < 4, p2f_g, 0.0)))
+    # conv3 + pool on the GPU's p2 -> the cut
+    c3 = W.conv3x3p1(p2, W3b, P0["conv3.bias"])
+    _, code3 = W.relu_pool_code(c3)
+    code3_gpu = _nchw(c._code3).astype(np.int64)
+    codes_close(c3, code3_gpu, code3)
+    cut_g = _nchw(cut)
+    p3_g = np.take_along_axis(np.maximum(c3, 0).reshape(B, 256, 8, 2, 8, 2).transpose(0, 1, 2, 4, 3, 5)
+                              .reshape(B, 256, 8, 8, 4), np.minimum(code3_gpu, 3)[..., None], -1)[..., 0]
+    bf16_close(cut_g, bf(np.where(code3_gpu < 4, p3_g, 0.0)))
+    # server on the GPU's cut: dropout mask of step 0, seed 0
+    keep = W.dropout_keep(0, 0, B)
+    sv = W.server_step(P0, cut_g, y.numpy(), keep)
+    np.testing.assert_allclose(_np(loss_i), sv["loss_i"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(_np(s._dlogits), sv["dlogits"], rtol=0, atol=2e-7)
+    bf16_close(_nchw(dcut), sv["dcut"])
+    grad_close(_np(grads_s[:163840]).reshape(10, -1), sv["grads"]["fc.weight"])
+    grad_close(_np(grads_s[163840:]), sv["grads"]["fc.bias"])
+    # client backward on the GPU's tensors
+    dcut_g = _nchw(dcut)
+    dc3 = W.unpool(dcut_g, code3_gpu)
+    assert np.array_equal(_nchw(c._dc3), dc3)                        # bit-exact routing
+    dc2 = W.unpool(W.conv3x3p1_dgrad(dc3, W3b), code2_gpu)
+    bf16_close(_nchw(c._dc2), bf(dc2))
+    dc2_g = _nchw(c._dc2)
+    da1 = W.conv3x3p1_dgrad(dc2_g, W2b)
+    bf16_close(_nchw(c._da1m), bf(np.where(a1 > 0, da1, 0.0)))
+    g = _np(c.grads)
+    dW3, db3 = W.conv3x3p1_wgrad(p2, dc3)
+    grad_close(g[75648:370560].reshape(256, 128, 3, 3), dW3)
+    grad_close(g[370560:], db3)
+    dW2, db2 = W.conv3x3p1_wgrad(a1, dc2_g)
+    grad_close(g[1792:75520].reshape(128, 64, 3, 3), dW2)
+    grad_close(g[75520:75648], db2)
+    dW1, db1 = W.conv3x3p1_wgrad(xs, _nchw(c._da1m))
+    grad_close(g[:1728].reshape(64, 3, 3, 3), dW1)
+    grad_close(g[1728:1792], db1)
+    # Adam (t = 1) on the GPU's own gradients
+    flat0 = np.concatenate([P0[k].ravel() for k in W.CLIENT_KEYS])
+    want, _, _ = W.adam(flat0, g, np.zeros_like(g), np.zeros_like(g), 1)
+    got = _np(c.params)
+    tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
+    assert (np.abs(got - want) <= tol).all()
+    assert int(c.step_ctr.item()) == 1 and int(s.step_ctr.item()) == 1
+
+
+def test_wide_large_batch_per_sample_rows_and_linearity(gpu):
+    """B = 520 exercises the persistent multi-tile pipelines of every kernel (each workgroup walks
+    several tiles). Size-independent properties: per-sample forward and input-gradient rows are
+    bit-identical to small-batch runs (per-element K order does not depend on the tile mapping);
+    weight gradients are linear in the batch (1e-5)."""
+    from splitcnn.wide import SyntheticCIFAR, WideClientStage, init_wide_models
+    A, _ = init_wide_models(seed=0)
+    c = WideClientStage(A, device=gpu)
+    B = 520
+    x, _ = SyntheticCIFAR(7).batch(B)
+    x = x.to(gpu)
+    gen = torch.Generator().manual_seed(3)
+    dcut = (torch.randn(B, 32, 8, 8, 8, generator=gen) * 1e-3).to(torch.bfloat16).to(gpu)
+    cut = c.forward(x).clone()
+    s1, s2, s3 = (t.sum(0) for t in c.backward_slabs(dcut))
+    dc2, da1m = c._dc2.clone(), c._da1m.clone()
+    parts = []
+    for lo, hi in ((0, 4), (4, 260), (260, 516), (516, 520)):
+        cut_p = c.forward(x[lo:hi].contiguous()).clone()
+        assert torch.equal(cut_p, cut[lo:hi]), (lo, hi)
+        t1, t2, t3 = (t.sum(0) for t in c.backward_slabs(dcut[lo:hi].contiguous()))
+        assert torch.equal(c._dc2, dc2[lo:hi]) and torch.equal(c._da1m, da1m[lo:hi]), (lo, hi)
+        parts.append((t1, t2, t3))
+    for k, tot in enumerate((s1, s2, s3)):
+        acc = sum(p[k].double() for p in parts)
+        grad_close(_np(tot), _np(acc))
+    torch.cuda.synchronize()
+
+
+def test_wide_graph_replay_equals_eager_and_is_deterministic(gpu):
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    runs = []
+    for graph in (True, False, True):
+        A, Bm = init_wide_models(seed=0)
+        tr = WideTrainer(A, Bm, device=gpu, graph=graph)
+        data = SyntheticCIFAR(42)
+        for _ in range(3):
+            x, y = data.batch(64)
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        runs.append((tr.client.params.clone(), tr.server.params.clone(), [l for _, l in tr.loss_log.flush()]))
+    for r in runs[1:]:
+        assert torch.equal(r[0], runs[0][0]) and torch.equal(r[1], runs[0][1])
+        assert r[2] == runs[0][2]
+
+
+def test_wide_loss_curve_vs_oracle(gpu):
+    """30 Adam steps at B = 8 through the HIP graph vs the bf16 oracle chained on its own state."""
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    A, Bm = init_wide_models(seed=0)
+    P = {k: v.detach().double().numpy() for k, v in list(A.state_dict().items()) + list(Bm.state_dict().items())}
+    tr = WideTrainer(A, Bm, device=gpu, graph=True)
+    data = SyntheticCIFAR(11)
+    opt, want = {}, []
+    for t in range(1, 31):
+        x, y = data.batch(8)
+        tr.step(x.to(gpu), y.to(gpu))
+        P, opt, rec = W.wide_step(P, opt, t, x.numpy(), y.numpy(), seed=0)
+        want.append(rec["loss"])
+    got = [l for _, l in tr.loss_log.flush()]
+    rel = np.abs(np.array(got) - np.array(want)) / np.abs(np.array(want))
+    assert rel.max() <= 2e-2, rel
+    assert np.mean(got[-5:]) < np.mean(got[:5])   # it learns
