@@ -36,6 +36,11 @@ CONV2_FLOP_PER_SAMPLE = 21_233_664    # each of conv2 fwd / dgrad / wgrad
 FP32_PEAK_TFLOPS = 157.3              # MI355X_MICROARCH.md: fp32 matrix = vector peak
 HBM_PEAK_GBS = 8000.0
 CUT_BYTES = 86_528                    # fp32 [32,26,26] per sample, each direction
+# widened split CNN (BASELINE config 5, splitcnn/wide.py): algorithmic FLOPs per training sample
+WIDE_CONV_FLOP = {"wide_conv2_fwd": 150_994_944, "wide_conv3_fwd": 150_994_944, "wide_conv3_dgrad": 150_994_944,
+                  "wide_conv2_dgrad": 150_994_944, "wide_conv3_wgrad": 150_994_944, "wide_conv2_wgrad": 150_994_944}
+WIDE_FLOP_PER_SAMPLE = 914_030_592    # 6 x 150,994,944 (conv2/conv3) + 2 x 3,538,944 (conv1) + 3 x 327,680 (fc)
+BF16_PEAK_TFLOPS = 2500.0             # MI355X_MICROARCH.md: dense bf16 MFMA peak
 
 
 def parse():
@@ -52,6 +57,10 @@ def parse():
     ap.add_argument("--no-kernel-pass", action="store_true")
     ap.add_argument("--no-exchange-phase", action="store_true")
     ap.add_argument("--exchange-steps", type=int, default=10)
+    ap.add_argument("--config", default="k2", choices=["k2", "k5"],
+                    help="k2 = reference split CNN fp32 (headline); k5 = widened bf16 split CNN")
+    ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
+    ap.add_argument("--k5-batch", type=int, default=4096)
     return ap.parse_args()
 
 
@@ -169,6 +178,39 @@ def run_single(args, out):
     out["step_roofline_frac"] = round(out["value"] * FLOP_PER_SAMPLE / (FP32_PEAK_TFLOPS * 1e12), 4)
 
 
+def run_wide(args, B, steps, warmup, kernel_pass_on=True):
+    """BASELINE config 5: widened split CNN (bf16 MFMA convs, dropout, Adam) fused on one GPU."""
+    import torch
+
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    dev = torch.device("cuda:0")
+    data = SyntheticCIFAR(42)
+    xs, ys = zip(*(data.batch(B) for _ in range(4)))
+    X, Y = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
+    tr = WideTrainer(*init_wide_models(seed=0), device=dev, graph=not args.no_graph)
+    dt = timed(lambda i: tr.step(X[i % 4], Y[i % 4]), steps, warmup, dev)
+    losses = tr.loss_log.flush()
+    r = {"metric": "training samples/sec, widened split CNN (BASELINE config 5)", "value": steps * B / dt,
+         "unit": "samples/s", "ms_per_step": dt / steps * 1e3, "dtype": "bf16",
+         "config": {"workload": "K5: widened split CNN (conv 3-64-128-256, 3x32x32, cut [256,8,8] after conv3; "
+                                "server dropout + fc 16384->10; Adam), fused on 1xMI355X, bf16 MFMA "
+                                "implicit-GEMM convs, HIP-graph step", "global_batch": B},
+         "loss_first_last": [round(losses[0][1], 5), round(losses[-1][1], 5)] if losses else None,
+         "step_roofline_frac": round(steps * B / dt * WIDE_FLOP_PER_SAMPLE / (BF16_PEAK_TFLOPS * 1e12), 4)}
+    if kernel_pass_on:
+        tr2 = WideTrainer(*init_wide_models(seed=0), device=dev, graph=False)
+        kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), 3, dev)
+        r["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
+        conv = {k: v for k, v in kern.items() if k in WIDE_CONV_FLOP}
+        name = max(conv, key=lambda k: conv[k]["avg_ms"])
+        ach = WIDE_CONV_FLOP[name] * B / (conv[name]["avg_ms"] * 1e-3) / 1e12
+        r["roofline"] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                         "flop_per_launch": WIDE_CONV_FLOP[name] * B, "avg_ms": round(conv[name]["avg_ms"], 4)}
+        r["conv_tflops"] = {k: round(WIDE_CONV_FLOP[k] * B / (v["avg_ms"] * 1e-3) / 1e12, 1) for k, v in conv.items()}
+    return r
+
+
 def run_distributed(args, out, rank, world, local):
     import torch
     import torch.distributed as dist
@@ -256,8 +298,19 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         run_distributed(args, out, rank, world, local)
+    elif args.config == "k5":
+        w = run_wide(args, args.k5_batch, args.steps, args.warmup, not args.no_kernel_pass)
+        out.update({k: v for k, v in w.items() if k != "metric"})
+        out["metric"] = w["metric"]
+        out["data"] = "synthetic CIFAR-shape batches (class prototypes + noise), random-init weights (seed 0)"
     else:
         run_single(args, out)
+        if not args.no_k5:
+            try:
+                out["widened"] = run_wide(args, args.k5_batch, max(5, min(args.steps, 20)), 3,
+                                          not args.no_kernel_pass)
+            except Exception as e:  # the headline stands on its own
+                out["widened"] = {"error": repr(e)[:300]}
     if cpu is not None:
         out["cpu_baseline"] = cpu
         if cpu.get("value"):

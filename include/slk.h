@@ -159,8 +159,9 @@ int slk_mnist_batch(const uint8_t* images, const uint8_t* labels, int n_images, 
 #define SLK_WIDE_CLIENT_NPARAM 370816
 #define SLK_WIDE_SERVER_NPARAM 163850
 
-/* a1 = bf16(relu(conv1(x))), x f32 NCHW [B,3,32,32]; f32 VALU (K = 27). */
-int slk_wide_conv1_fwd(const float* x, const float* W1, const float* b1, uint16_t* a1, int B, void* stream);
+/* a1 = bf16(relu(conv1(bf16(x)) + b1)), x f32 NCHW [B,3,32,32]; one bf16 MFMA K-step (K = 27 -> 32);
+ * w1b [64][32] bf16 from slk_wide_shadows. */
+int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, int B, void* stream);
 /* p2, code2 = pool(relu(conv2(a1) + b2)) — bf16 MFMA implicit GEMM, f32 accumulation. */
 int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2, uint16_t* p2, uint8_t* code2,
                        int B, void* stream);
@@ -181,7 +182,7 @@ int slk_wide_fc_wgrad_nslab(int B);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
  * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
  * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs
- * [nslab][1728 + 64]. Slabs are [dW (torch layout) | db] and reduce in fixed order. */
+ * [nslab][1728 + 64] (bf16(x) operand). Slabs are [dW (torch layout) | db], reduced in fixed order. */
 int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream);
 int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream);
 int slk_wide_conv3_wgrad_nslab(int B);
@@ -199,9 +200,10 @@ int slk_wide_conv1_wgrad_nslab(int B);
  * widened config (the north star's "fused SGD/Adam"). */
 int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab, int n,
                         float lr, float beta1, float beta2, float eps, const int* step, void* stream);
-/* Rebuild the bf16 conv weight shadows from the f32 masters W2 [128,64,3,3], W3 [256,128,3,3]. */
-int slk_wide_shadows(const float* W2, const float* W3, uint16_t* w2f, uint16_t* w2d, uint16_t* w3f, uint16_t* w3d,
-                     void* stream);
+/* Rebuild the bf16 weight shadows from the f32 masters: w1b [64][32] (W1 rows, k >= 27 zero) and the
+ * MFMA layouts of W2 [128,64,3,3] and W3 [256,128,3,3]. */
+int slk_wide_shadows(const float* W1, const float* W2, const float* W3, uint16_t* w1b, uint16_t* w2f, uint16_t* w2d,
+                     uint16_t* w3f, uint16_t* w3d, void* stream);
 /* wf8[j][(plane*64+pix)*8+k] = Wf[j][(plane*8+k)*64+pix]: the fc weight in the cut's C8 order. */
 int slk_wide_fc_shadow(const float* wf, float* wf8, void* stream);
 /* ++*counter on the device (the per-stage step counter a captured HIP graph advances). */

@@ -12,9 +12,11 @@ its step contract (client_part.py:110-138 <-> server_part.py:25-58) is kept, the
   optim   torch.optim.Adam(lr=1e-3, betas=(0.9, 0.999), eps=1e-8) on both sides
 
 Numerics of the bf16 path (what the GPU kernels compute, and therefore what this oracle restates):
-conv1 in f32 from the f32 input, activations stored as bf16 (round-to-nearest-even) after ReLU and
-after each pool; conv2/conv3 forward, their dgrad/wgrad and the cut gradient use bf16 operands (the
-weights as bf16 shadows of the f32 masters) with f32 accumulation; the max-pool argmax is taken on
+every convolution (forward, dgrad, wgrad) multiplies bf16 operands — the input image rounded to
+bf16, the weights as bf16 shadows of the f32 masters, activations and gradients as stored — with f32
+accumulation (as torch autocast runs a bf16 conv); activations are stored as bf16
+(round-to-nearest-even) after ReLU and after each pool, and so are the cut gradient and the
+unpooled / ReLU-masked gradients; the max-pool argmax is taken on
 the f32 pre-rounding values; the head, cross-entropy, Adam and all master weights are f32. With
 bf16=False every rounding is skipped: that float64 form is what tests/test_wide_oracle.py pins
 against torch autograd + torch.optim.Adam on the same modules (the reference has no fixtures for
@@ -174,7 +176,8 @@ def adam(p, g, m, v, t, lr=LR, b1=BETA1, b2=BETA2, eps=EPS, f32=True):
 # ----------------------------------------------------------------------------- the step
 def client_forward(P, x, bf=True):
     """Returns (cut, rec): cut = bf16(pool3) [B,256,8,8] and the saved tensors."""
-    a1 = _r(np.maximum(conv3x3p1(x, P["conv1.weight"], P["conv1.bias"]), 0.0), bf)
+    xb = _r(x, bf)
+    a1 = _r(np.maximum(conv3x3p1(xb, _r(P["conv1.weight"], bf), P["conv1.bias"]), 0.0), bf)
     W2 = _r(P["conv2.weight"], bf)
     c2 = conv3x3p1(a1, W2, P["conv2.bias"])
     p2f, code2 = relu_pool_code(c2)
@@ -183,7 +186,7 @@ def client_forward(P, x, bf=True):
     c3 = conv3x3p1(p2, W3, P["conv3.bias"])
     p3f, code3 = relu_pool_code(c3)
     cut = _r(p3f, bf)
-    return cut, dict(a1=a1, c2=c2, p2=p2, code2=code2, c3=c3, code3=code3, cut=cut, W2b=W2, W3b=W3)
+    return cut, dict(xb=xb, a1=a1, c2=c2, p2=p2, code2=code2, c3=c3, code3=code3, cut=cut, W2b=W2, W3b=W3)
 
 
 def server_step(P, cut, y, keep, grad_scale_batch=None, bf=True):
@@ -219,7 +222,7 @@ def client_backward(P, x, rec, dcut, bf=True):
     dW2, db2 = conv3x3p1_wgrad(rec["a1"], dc2)
     da1 = conv3x3p1_dgrad(dc2, rec["W2b"])
     da1m = _r(np.where(rec["a1"] > 0, da1, 0.0), bf)
-    dW1, db1 = conv3x3p1_wgrad(x, da1m)
+    dW1, db1 = conv3x3p1_wgrad(rec["xb"], da1m)
     grads = {"conv1.weight": dW1, "conv1.bias": db1, "conv2.weight": dW2, "conv2.bias": db2,
              "conv3.weight": dW3, "conv3.bias": db3}
     return grads, dict(dc3=dc3, dc2=dc2, da1m=da1m)

@@ -559,148 +559,212 @@ extern "C" int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, flo
     return launch_wgrad<CfgWg3>(dc3, p2, slabs, B, stream);
 }
 
-// ============================================================================ conv1 (3 -> 64), f32
-// conv1 has K = 27, no real contraction: f32 VALU. One 256-thread workgroup per image stages the
-// image with its zero halo in LDS ([3][34][34] f32); each thread owns 4 pixels (tid + 256k) and loops
-// over the 64 output channels with that channel's 27 weights + bias in SGPRs (wave-uniform loop,
-// scalar loads), 108 FMAs per channel; each 8-channel chunk leaves as one 16-byte bf16 store per pixel.
-constexpr int C1P = 34;  // padded image pitch
+// ============================================================================ conv1 (3 -> 64), bf16 MFMA
+// conv1 is a 64 x 27 contraction per pixel: one 16x16x32 MFMA K-step with K = (ci, ky, kx) padded to
+// 32 (k = 27 is a constant-1 column in the weight gradient: it yields db1 for free). The zero-padded
+// image [3][34][34] is staged in LDS as f32 (14 elements per thread: offsets computed once, all loads
+// issued back to back); each lane gathers its 8 im2col values of a fragment from it and converts them
+// to bf16. HBM-bound: the forward writes a1 (128 KB/sample), the weight gradient reads da1m.
+constexpr int C1P = 34;                               // padded image pitch
+constexpr int C1S = (3 * C1P * C1P + 255) / 256;      // 14 staged elements per thread
 
-__device__ __forceinline__ void stage_image(const float* __restrict__ x, float* xs) {
-    // xs[ci][34][34] with zero border
-    for (int e = threadIdx.x; e < 3 * C1P * C1P; e += 256) {
+__device__ __forceinline__ void stage_offsets(int (&off)[C1S]) {
+#pragma unroll
+    for (int k = 0; k < C1S; ++k) {
+        const int e = threadIdx.x + 256 * k;
         const int ci = e / (C1P * C1P), r = e - ci * (C1P * C1P);
         const int yy = r / C1P - 1, xx = r % C1P - 1;
-        xs[e] = (yy >= 0 && yy < 32 && xx >= 0 && xx < 32) ? x[(ci * 32 + yy) * 32 + xx] : 0.f;
+        off[k] = (e < 3 * C1P * C1P && yy >= 0 && yy < 32 && xx >= 0 && xx < 32) ? (ci * 32 + yy) * 32 + xx : -1;
     }
 }
-
-__global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W1,
-                                                             const float* __restrict__ b1, uint16_t* __restrict__ a1) {
-    __shared__ float xs[3 * C1P * C1P];
-    const int n = blockIdx.x;
-    stage_image(x + (size_t)n * 3 * 1024, xs);
-    __syncthreads();
-    float xv[4][27];
+__device__ __forceinline__ void stage_load(const float* __restrict__ img, const int (&off)[C1S], float (&v)[C1S]) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int p = threadIdx.x + 256 * k, y = p >> 5, xx = p & 31;
+    for (int k = 0; k < C1S; ++k) v[k] = off[k] >= 0 ? img[off[k]] : 0.f;
+}
+__device__ __forceinline__ void stage_store(float* xs, const float (&v)[C1S]) {
 #pragma unroll
-        for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-            for (int t = 0; t < 9; ++t) xv[k][ci * 9 + t] = xs[(ci * C1P + y + t / 3) * C1P + xx + t % 3];
+    for (int k = 0; k < C1S; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        if (e < 3 * C1P * C1P) xs[e] = v[k];
     }
+}
+// im2col offset of K index k (ci*1156 + ky*34 + kx) inside the padded image, -1 for k >= 27
+__device__ __forceinline__ int im2col_off(int k) {
+    const int ci = k / 9, t = k - (k / 9) * 9;
+    return k < 27 ? ci * C1P * C1P + (t / 3) * C1P + t % 3 : -1;
+}
+
+// Forward: a1[co][px] = relu(sum_k W1b[co][k] * bf16(x)[k][px] + b1[co]); A = W1b (4 fragments in
+// registers for the whole launch), B = the im2col fragment of 16 pixels. Wave w of a workgroup takes
+// pixel fragments w, w+4, ... of its image; grid-strided over images.
+__global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ w1b,
+                                                             const float* __restrict__ b1, uint16_t* __restrict__ a1, int B) {
+    __shared__ float xs[3 * C1P * C1P];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = lane >> 4, col = lane & 15;
+    bf16x8 av[4];
+    float bias[4][4];
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) {
+        av[cf] = *reinterpret_cast<const bf16x8*>(w1b + (cf * 16 + col) * 32 + 8 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[cf][r] = b1[cf * 16 + 4 * q + r];
+    }
+    int koff[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) koff[j] = im2col_off(8 * q + j);
+    int off[C1S];
+    stage_offsets(off);
 #pragma unroll 1
-    for (int c = 0; c < 8; ++c) {
-        uint32_t pk[4][4];
-#pragma unroll 1
-        for (int u = 0; u < 8; u += 2) {  // one channel pair per iteration; shift it into pk
-            float o[2][4];
+    for (int n = blockIdx.x; n < B; n += gridDim.x) {
+        float v[C1S];
+        stage_load(x + (size_t)n * 3 * 1024, off, v);
+        __syncthreads();
+        stage_store(xs, v);
+        __syncthreads();
+#pragma unroll 2
+        for (int f = wave; f < 64; f += 4) {
+            const int y = f >> 1, xx = (f & 1) * 16 + col;
+            const int base = y * C1P + xx;
+            float g[8];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int co = c * 8 + u + h;
-                const float* w = W1 + co * 27;
-                const float bb = b1[co];
+            for (int j = 0; j < 8; ++j) g[j] = koff[j] >= 0 ? xs[base + koff[j]] : 0.f;
+            bf16x8 bv;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    float acc = bb;
+            for (int j = 0; j < 8; ++j) bv[j] = (__bf16)g[j];
+            uint16_t* dst = a1 + ((size_t)(n * 8) * 1024 + y * 32 + xx) * 8 + 4 * (q & 1);
 #pragma unroll
-                    for (int i = 0; i < 27; ++i) acc = __builtin_fmaf(w[i], xv[k][i], acc);
-                    o[h][k] = acc > 0.f ? acc : 0.f;
+            for (int cf = 0; cf < 4; ++cf) {
+                f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[cf], bv, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                float o[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float t = acc[r] + bias[cf][r];
+                    o[r] = t > 0.f ? t : 0.f;
                 }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                pk[k][0] = pk[k][1];
-                pk[k][1] = pk[k][2];
-                pk[k][2] = pk[k][3];
-                pk[k][3] = pack_bf16x2(o[0][k], o[1][k]);
+                // channels cf*16 + 4q .. +3 = chunk 2cf + (q >> 1), offset 4 (q & 1)
+                *reinterpret_cast<uint2*>(dst + (size_t)(2 * cf + (q >> 1)) * 1024 * 8) =
+                    make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
             }
         }
-        uint16_t* dst = a1 + ((size_t)(n * 8 + c) * 1024) * 8;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *reinterpret_cast<uint4*>(dst + (threadIdx.x + 256 * k) * 8) = make_uint4(pk[k][0], pk[k][1], pk[k][2], pk[k][3]);
     }
 }
 
-// conv1 weight gradient from the ReLU-masked bf16 gradient da1m (conv2 dgrad's epilogue applied the
-// mask) and the f32 image: dW1[co][ci][tap] = sum_px da1m[co][px] * xpad[ci][px + off(tap)].
-// Grid = 16 channel quads x C1W_SPLIT batch slices; a thread owns 4 channels x 27 taps (+4 bias sums)
-// for 4 pixels of each image; the image is staged in LDS. Fixed-order wave/LDS reduction at the end;
-// one slab [1792] = [dW1 (torch layout) | db1] per batch slice.
-constexpr int C1W_SPLIT = 128;
+// Weight gradient: dW1[co][k] = sum_px da1m[co][px] * bf16(x)[k][px] (k = 27: db1). GEMM M = 64 co,
+// N = 32 k, K = pixels. da1m rows of a 4-row block land in LDS by LDS-DMA ([8 chunks][132 px], double
+// buffered) and are read transposed (ds_read_b64_tr_b16); wave w takes row w of each block. Each
+// workgroup walks images blockIdx.x, +grid, ...; its 4 waves' partial sums are added in fixed order
+// into one slab [1792] = [dW1 (torch layout) | db1].
+constexpr int C1W_GRID = 256;
+constexpr int C1W_NPXP = 132;                                  // 128 px + 4 pad: plane stride 64 mod 256 B
+constexpr int C1W_BUF = 8 * C1W_NPXP * 16;                     // 16,896 B
 
 __global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __restrict__ x, const uint16_t* __restrict__ da1m,
                                                                float* __restrict__ slabs, int B) {
-    __shared__ float xs[3 * C1P * C1P];
-    __shared__ float red[4][112];
-    const int cq = blockIdx.x & 15, split = blockIdx.x >> 4;
-    const int co0 = cq * 4;
-    float acc[4][27], accb[4];
+    __shared__ __attribute__((aligned(1024))) char smem[2 * C1W_BUF + 3 * C1P * C1P * 4];
+    float* xs = reinterpret_cast<float*>(smem + 2 * C1W_BUF);
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane >> 4, ig = lane & 15, a = ig >> 2, p = ig & 3, col = lane & 15;
+    int koff[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        accb[j] = 0.f;
+    for (int kf = 0; kf < 2; ++kf) koff[kf] = im2col_off(kf * 16 + col);
+    const int a_base = ((p >> 1) * C1W_NPXP + wave * 32 + 8 * q + a) * 16 + (p & 1) * 8;
+    int off[C1S];
+    stage_offsets(off);
+
+    f32x4 acc[4][2];
 #pragma unroll
-        for (int i = 0; i < 27; ++i) acc[j][i] = 0.f;
-    }
-#pragma unroll 1
-    for (int n = split; n < B; n += C1W_SPLIT) {
-        __syncthreads();
-        stage_image(x + (size_t)n * 3 * 1024, xs);
-        uint2 dv[4];
-        const uint16_t* src = da1m + ((size_t)(n * 8 + (co0 >> 3)) * 1024) * 8 + (co0 & 7);
+    for (int cf = 0; cf < 4; ++cf)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dv[k] = *reinterpret_cast<const uint2*>(src + (threadIdx.x + 256 * k) * 8);
-        __syncthreads();
+        for (int kf = 0; kf < 2; ++kf) acc[cf][kf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int n, int rb, char* buf) {
+        // 8 chunk planes x 2 KiB (4 rows x 32 px x 16 B); wave w moves chunks 2w, 2w+1
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int p = threadIdx.x + 256 * k, y = p >> 5, xx = p & 31;
-            const float d[4] = {bf16_lo(dv[k].x), bf16_hi(dv[k].x), bf16_lo(dv[k].y), bf16_hi(dv[k].y)};
-            float xv[27];
+            const int c = wave * 2 + (k >> 1), part = k & 1;
+            const char* src = reinterpret_cast<const char*>(da1m) + ((size_t)(n * 8 + c) * 1024 + rb * 128) * 16 +
+                              part * 1024 + lane * 16;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + c * C1W_NPXP * 16 + part * 1024), 16, 0, 0);
+        }
+    };
+    const int nimg = B > (int)blockIdx.x ? (B - 1 - (int)blockIdx.x) / C1W_GRID + 1 : 0;
+    const int nsteps = nimg * 8;
+    float xr[C1S];
+    if (nsteps > 0) {
+        stage_load(x + (size_t)blockIdx.x * 3 * 1024, off, xr);
+        issue(blockIdx.x, 0, smem);
+    }
+#pragma unroll 1
+    for (int s = 0; s < nsteps; ++s) {
+        const int n = blockIdx.x + (s >> 3) * C1W_GRID, rb = s & 7;
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (rb == 0) {           // all waves are done with the previous image's xs
+            stage_store(xs, xr);
+            __syncthreads();
+        }
+        if (s + 1 < nsteps) {
+            const int n1 = blockIdx.x + ((s + 1) >> 3) * C1W_GRID;
+            issue(n1, (s + 1) & 7, smem + ((s + 1) & 1) * C1W_BUF);
+            if (rb == 7) stage_load(x + (size_t)n1 * 3 * 1024, off, xr);
+        }
+        const char* buf = smem + (s & 1) * C1W_BUF;
+        typedef __attribute__((address_space(3))) bf16x4* lp4;
+        bf16x8 av[4];
 #pragma unroll
-            for (int ci = 0; ci < 3; ++ci)
+        for (int cf = 0; cf < 4; ++cf) {
+            const char* pa = buf + a_base + cf * 2 * C1W_NPXP * 16;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)pa);
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(pa + 64));
+            av[cf] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        const int y = rb * 4 + wave;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) xv[ci * 9 + t] = xs[(ci * C1P + y + t / 3) * C1P + xx + t % 3];
+        for (int kf = 0; kf < 2; ++kf) {
+            const int base = y * C1P + 8 * q + (koff[kf] >= 0 ? koff[kf] : 0);
+            bf16x8 bv;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                accb[j] += d[j];
-#pragma unroll
-                for (int i = 0; i < 27; ++i) acc[j][i] = __builtin_fmaf(d[j], xv[i], acc[j][i]);
+            for (int j = 0; j < 8; ++j) {
+                const float g = xs[base + j];
+                bv[j] = (__bf16)(koff[kf] >= 0 ? g : (kf * 16 + col == 27 ? 1.f : 0.f));
             }
-        }
-    }
-    // reduce 112 values over the workgroup: wave sums, then waves 0..3 in order
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int i = 0; i < 27; ++i) {
-            const float s = wave_sum(acc[j][i]);
-            if (lane == 0) red[wave][j * 27 + i] = s;
+            for (int cf = 0; cf < 4; ++cf) acc[cf][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[cf], bv, acc[cf][kf], 0, 0, 0);
         }
-        const float s = wave_sum(accb[j]);
-        if (lane == 0) red[wave][108 + j] = s;
+        (void)n;
     }
+    // fixed-order sum of the 4 waves' partials: red[wave][co][k]
     __syncthreads();
-    float* slab = slabs + (size_t)split * 1792;
-    for (int e = threadIdx.x; e < 112; e += 256) {
-        const float s = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-        if (e < 108) slab[co0 * 27 + e] = s;          // [co][ci][ky][kx] = co*27 + ci*9 + tap
-        else slab[1728 + co0 + (e - 108)] = s;
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(wave * 64 + cf * 16 + 4 * q + r) * 32 + kf * 16 + col] = acc[cf][kf][r];
+    __syncthreads();
+    float* slab = slabs + (size_t)blockIdx.x * 1792;
+    for (int e = threadIdx.x; e < 64 * 28; e += 256) {
+        const int co = e / 28, k = e - co * 28;
+        const float v = ((red[co * 32 + k] + red[(64 + co) * 32 + k]) + red[(128 + co) * 32 + k]) + red[(192 + co) * 32 + k];
+        if (k < 27) slab[co * 27 + k] = v;
+        else slab[1728 + co] = v;
     }
 }
 
-extern "C" int slk_wide_conv1_fwd(const float* x, const float* W1, const float* b1, uint16_t* a1, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && x && W1 && b1 && a1);
+extern "C" int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && x && w1b && b1 && a1);
     if (B == 0) return 0;
-    hipLaunchKernelGGL(wide_conv1_fwd_kernel, dim3(B), dim3(256), 0, slk_stream(stream), x, W1, b1, a1);
+    const int grid = B < 2048 ? B : 2048;
+    hipLaunchKernelGGL(wide_conv1_fwd_kernel, dim3(grid), dim3(256), 0, slk_stream(stream), x, w1b, b1, a1, B);
     return slk_launch_status();
 }
-extern "C" int slk_wide_conv1_wgrad_nslab(int B) { return B >= 0 ? C1W_SPLIT : 0; }
+extern "C" int slk_wide_conv1_wgrad_nslab(int B) { return B >= 0 ? C1W_GRID : 0; }
 extern "C" int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && x && da1m && slabs);
-    hipLaunchKernelGGL(wide_conv1_wgrad_kernel, dim3(16 * C1W_SPLIT), dim3(256), 0, slk_stream(stream), x, da1m, slabs, B);
+    hipLaunchKernelGGL(wide_conv1_wgrad_kernel, dim3(C1W_GRID), dim3(256), 0, slk_stream(stream), x, da1m, slabs, B);
     return slk_launch_status();
 }
 

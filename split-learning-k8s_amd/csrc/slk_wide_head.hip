@@ -16,7 +16,7 @@ namespace {
 constexpr int CUTF = 16384;       // features per sample
 constexpr int NCH = CUTF / 8;     // 2048 chunks of 8 channels (C8 order: chunk = plane*64 + pixel)
 constexpr int NC = 10;
-constexpr int HSB = 8;            // samples per head workgroup
+constexpr int HSB = 4;            // samples per head workgroup
 }  // namespace
 
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
@@ -73,7 +73,6 @@ __global__ __launch_bounds__(256) void wide_head_kernel(
     for (int s = 0; s < HSB; ++s)
 #pragma unroll
         for (int j = 0; j < NC; ++j) acc[s][j] = 0.f;
-    uint32_t keep[8][HSB / 4];  // 8 bits per (chunk, sample), 4 samples per word
 #pragma unroll 1
     for (int i = 0; i < 8; ++i) {
         const int fc = tid + 256 * i;
@@ -89,8 +88,6 @@ __global__ __launch_bounds__(256) void wide_head_kernel(
         for (int s = 0; s < HSB; ++s) {
             if (s >= nb) break;
             const uint32_t kb = keep_bits((uint32_t)(b0 + s), fc, step, seed, thresh);
-            if ((s & 3) == 0) keep[i][s >> 2] = 0;
-            keep[i][s >> 2] |= kb << (8 * (s & 3));
             float v[8];
             unpack8(*reinterpret_cast<const uint4*>(cut + ((size_t)(b0 + s) * NCH + fc) * 8), v);
 #pragma unroll
@@ -152,7 +149,7 @@ __global__ __launch_bounds__(256) void wide_head_kernel(
 #pragma unroll
         for (int s = 0; s < HSB; ++s) {
             if (s >= nb) break;
-            const uint32_t kb = (keep[i][s >> 2] >> (8 * (s & 3))) & 0xFF;
+            const uint32_t kb = keep_bits((uint32_t)(b0 + s), fc, step, seed, thresh);  // recomputed: no mask storage
             float o[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -259,11 +256,18 @@ __global__ __launch_bounds__(1024) void adam_from_slabs_kernel(float* __restrict
 // bf16 shadows of the client conv weights (torch layout [co][ci][3][3] f32 masters) in the layouts
 // slk_wide.hip's implicit GEMMs stream: forward [co/128][tap][ci/8][co%128][8]; dgrad (roles
 // swapped, taps flipped) [ci/MT][8-tap][co/8][ci%MT][8] with MT = 64 (conv2) / 128 (conv3).
-__global__ __launch_bounds__(256) void wide_shadows_kernel(const float* __restrict__ W2, const float* __restrict__ W3,
+// Also the bf16 conv1 weight w1b [64][32] = W1[co] (27, order ci, ky, kx) | 5 zeros: conv1's MFMA A operand.
+__global__ __launch_bounds__(256) void wide_shadows_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
+                                                           const float* __restrict__ W3, uint16_t* __restrict__ w1b,
                                                            uint16_t* __restrict__ w2f, uint16_t* __restrict__ w2d,
                                                            uint16_t* __restrict__ w3f, uint16_t* __restrict__ w3d) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     constexpr int N2 = 128 * 64 * 9, N3 = 256 * 128 * 9;
+    if (e < 64 * 32) {
+        const int co = e >> 5, i = e & 31;
+        const __bf16 h = (__bf16)(i < 27 ? W1[co * 27 + i] : 0.f);
+        w1b[e] = __builtin_bit_cast(uint16_t, h);
+    }
     if (e < N2) {
         const int co = e / (64 * 9), r = e - co * 64 * 9, ci = r / 9, tap = r - ci * 9;
         const __bf16 h = (__bf16)W2[e];
@@ -319,11 +323,12 @@ extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v
                        slabs, nslab, n, lr, beta1, beta2, eps, step);
     return slk_launch_status();
 }
-extern "C" int slk_wide_shadows(const float* W2, const float* W3, uint16_t* w2f, uint16_t* w2d, uint16_t* w3f,
-                                uint16_t* w3d, void* stream) {
-    SLK_CHECK_ARG(W2 && W3 && w2f && w2d && w3f && w3d);
+extern "C" int slk_wide_shadows(const float* W1, const float* W2, const float* W3, uint16_t* w1b, uint16_t* w2f,
+                                uint16_t* w2d, uint16_t* w3f, uint16_t* w3d, void* stream) {
+    SLK_CHECK_ARG(W1 && W2 && W3 && w1b && w2f && w2d && w3f && w3d);
     constexpr int N = 128 * 64 * 9 + 256 * 128 * 9;
-    hipLaunchKernelGGL(wide_shadows_kernel, dim3((N + 255) / 256), dim3(256), 0, slk_stream(stream), W2, W3, w2f, w2d, w3f, w3d);
+    hipLaunchKernelGGL(wide_shadows_kernel, dim3((N + 255) / 256), dim3(256), 0, slk_stream(stream), W1, W2, W3, w1b,
+                       w2f, w2d, w3f, w3d);
     return slk_launch_status();
 }
 extern "C" int slk_wide_fc_shadow(const float* wf, float* wf8, void* stream) {

@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .engine import LossLog, _Buffers
+from .engine import TIMER, LossLog, _Buffers
 from .ops import _dev, _stream
 
 P_DROP = 0.25
@@ -149,6 +149,12 @@ def _q(name, *args):
     return _lib.query(name, *args)
 
 
+def _k(name, *args):
+    """Launch slk_<name> under the (optional) HIP-event kernel timer."""
+    with TIMER(name):
+        _lib.call("slk_" + name, *args)
+
+
 # ------------------------------------------------------------------------------------ stages
 class WideClientStage:
     """Client half: forward(x) -> cut (bf16 C8); backward_step(dcut) = activations.backward(grads) +
@@ -168,6 +174,7 @@ class WideClientStage:
         self.v = torch.zeros_like(self.params)
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.lr, self.betas, self.eps = lr, betas, eps
+        self.w1b = torch.empty(64 * 32, dtype=_BF, device=self.device)
         self.w2f = torch.empty(73728, dtype=_BF, device=self.device)
         self.w2d = torch.empty(73728, dtype=_BF, device=self.device)
         self.w3f = torch.empty(294912, dtype=_BF, device=self.device)
@@ -185,7 +192,8 @@ class WideClientStage:
     def refresh_shadows(self):
         """Rebuild the bf16 conv weight shadows from the f32 masters (after load_state_dict or Adam)."""
         W2, W3 = self._p("W2", 73728), self._p("W3", 294912)
-        _lib.call("slk_wide_shadows", W2.data_ptr(), W3.data_ptr(), self.w2f.data_ptr(), self.w2d.data_ptr(),
+        _k("wide_shadows", self._p("W1", 1728).data_ptr(), W2.data_ptr(), W3.data_ptr(), self.w1b.data_ptr(),
+           self.w2f.data_ptr(), self.w2d.data_ptr(),
                   self.w3f.data_ptr(), self.w3d.data_ptr(), _stream(self.params))
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -198,11 +206,10 @@ class WideClientStage:
         cut = out if out is not None else self._b("cut", (B,) + CUT_SHAPE, _BF)
         _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
         code3 = self._b("code3", (B,) + CUT_SHAPE, _U8)
-        _lib.call("slk_wide_conv1_fwd", x.data_ptr(), self._p("W1", 1728).data_ptr(), self._p("b1", 64).data_ptr(),
-                  a1.data_ptr(), B, s)
-        _lib.call("slk_wide_conv2_fwd", a1.data_ptr(), self.w2f.data_ptr(), self._p("b2", 128).data_ptr(),
+        _k("wide_conv1_fwd", x.data_ptr(), self.w1b.data_ptr(), self._p("b1", 64).data_ptr(), a1.data_ptr(), B, s)
+        _k("wide_conv2_fwd", a1.data_ptr(), self.w2f.data_ptr(), self._p("b2", 128).data_ptr(),
                   p2.data_ptr(), code2.data_ptr(), B, s)
-        _lib.call("slk_wide_conv3_fwd", p2.data_ptr(), self.w3f.data_ptr(), self._p("b3", 256).data_ptr(),
+        _k("wide_conv3_fwd", p2.data_ptr(), self.w3f.data_ptr(), self._p("b3", 256).data_ptr(),
                   cut.data_ptr(), code3.data_ptr(), B, s)
         self._x, self._a1, self._p2, self._code2, self._code3 = x, a1, p2, code2, code3
         return cut
@@ -218,20 +225,20 @@ class WideClientStage:
         s3 = self._b("s3", (_q("slk_wide_conv3_wgrad_nslab", B), 294912 + 256), _F32)
         s2 = self._b("s2", (_q("slk_wide_conv2_wgrad_nslab", B), 73728 + 128), _F32)
         s1 = self._b("s1", (_q("slk_wide_conv1_wgrad_nslab", B), 1728 + 64), _F32)
-        _lib.call("slk_wide_unpool", dcut.data_ptr(), self._code3.data_ptr(), dc3.data_ptr(), B, s)
-        _lib.call("slk_wide_conv3_wgrad", dc3.data_ptr(), self._p2.data_ptr(), s3.data_ptr(), B, s)
-        _lib.call("slk_wide_conv3_dgrad", dc3.data_ptr(), self.w3d.data_ptr(), self._code2.data_ptr(),
+        _k("wide_unpool", dcut.data_ptr(), self._code3.data_ptr(), dc3.data_ptr(), B, s)
+        _k("wide_conv3_wgrad", dc3.data_ptr(), self._p2.data_ptr(), s3.data_ptr(), B, s)
+        _k("wide_conv3_dgrad", dc3.data_ptr(), self.w3d.data_ptr(), self._code2.data_ptr(),
                   dc2.data_ptr(), B, s)
-        _lib.call("slk_wide_conv2_wgrad", dc2.data_ptr(), self._a1.data_ptr(), s2.data_ptr(), B, s)
-        _lib.call("slk_wide_conv2_dgrad", dc2.data_ptr(), self.w2d.data_ptr(), self._a1.data_ptr(),
+        _k("wide_conv2_wgrad", dc2.data_ptr(), self._a1.data_ptr(), s2.data_ptr(), B, s)
+        _k("wide_conv2_dgrad", dc2.data_ptr(), self.w2d.data_ptr(), self._a1.data_ptr(),
                   da1m.data_ptr(), B, s)
-        _lib.call("slk_wide_conv1_wgrad", self._x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
+        _k("wide_conv1_wgrad", self._x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
         self._dc3, self._dc2, self._da1m = dc3, dc2, da1m
         return s1, s2, s3
 
     def _adam(self, lo, n, slabs):
         s = _stream(slabs)
-        _lib.call("slk_adam_from_slabs", self.params[lo:].data_ptr(), self.grads[lo:].data_ptr(),
+        _k("adam_from_slabs", self.params[lo:].data_ptr(), self.grads[lo:].data_ptr(),
                   self.m[lo:].data_ptr(), self.v[lo:].data_ptr(), slabs.data_ptr(), slabs.shape[0], n,
                   float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
                   self.step_ctr.data_ptr(), s)
@@ -242,7 +249,7 @@ class WideClientStage:
         self._adam(1792, 73856, s2)
         self._adam(75648, 295168, s3)
         self.refresh_shadows()
-        _lib.call("slk_tick", self.step_ctr.data_ptr(), _stream(self.params))
+        _k("tick", self.step_ctr.data_ptr(), _stream(self.params))
 
     def backward_step(self, dcut: torch.Tensor):
         self.step_from_slabs(*self.backward_slabs(dcut))
@@ -272,7 +279,7 @@ class WideServerStage:
         return self._buf.get(name, shape, dtype, self.device)
 
     def refresh_shadows(self):
-        _lib.call("slk_wide_fc_shadow", self.params.data_ptr(), self.wf8.data_ptr(), _stream(self.params))
+        _k("wide_fc_shadow", self.params.data_ptr(), self.wf8.data_ptr(), _stream(self.params))
 
     def forward_backward(self, cut, labels, grad_scale, dcut=None):
         B = cut.shape[0]
@@ -285,25 +292,25 @@ class WideServerStage:
         dcut = dcut if dcut is not None else self._b("dcut", (B,) + CUT_SHAPE, _BF)
         _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
         sf = self._b("sf", (_q("slk_wide_fc_wgrad_nslab", B), SERVER_NPARAM), _F32)
-        _lib.call("slk_wide_head", cut.data_ptr(), self.wf8.data_ptr(), self.params[163840:].data_ptr(),
+        _k("wide_head", cut.data_ptr(), self.wf8.data_ptr(), self.params[163840:].data_ptr(),
                   labels.data_ptr(), self.step_ctr.data_ptr(), self.seed, KEEP_THRESHOLD, KEEP_SCALE,
                   float(grad_scale), logits.data_ptr(), loss_i.data_ptr(), dlogits.data_ptr(), dcut.data_ptr(),
                   self.err_flag.data_ptr(), B, s)
-        _lib.call("slk_wide_fc_wgrad", cut.data_ptr(), dlogits.data_ptr(), self.step_ctr.data_ptr(), self.seed,
+        _k("wide_fc_wgrad", cut.data_ptr(), dlogits.data_ptr(), self.step_ctr.data_ptr(), self.seed,
                   KEEP_THRESHOLD, KEEP_SCALE, sf.data_ptr(), B, s)
         self._logits, self._dlogits = logits, dlogits
         return dcut, loss_i, sf
 
     def step_from_slabs(self, sf):
         s = _stream(sf)
-        _lib.call("slk_adam_from_slabs", self.params.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
+        _k("adam_from_slabs", self.params.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
                   self.v.data_ptr(), sf.data_ptr(), sf.shape[0], SERVER_NPARAM, float(self.lr),
                   float(self.betas[0]), float(self.betas[1]), float(self.eps), self.step_ctr.data_ptr(), s)
         self.refresh_shadows()
-        _lib.call("slk_tick", self.step_ctr.data_ptr(), s)
+        _k("tick", self.step_ctr.data_ptr(), s)
 
     def log_loss(self, loss_i, step=None):
-        _lib.call("slk_loss_log", loss_i.data_ptr(), loss_i.numel(), 1.0 / loss_i.numel(),
+        _k("loss_log", loss_i.data_ptr(), loss_i.numel(), 1.0 / loss_i.numel(),
                   self.loss_log.ring.data_ptr(), self.loss_log.ring.numel(), self.loss_log.counter.data_ptr(),
                   _stream(loss_i))
         if step is not None:

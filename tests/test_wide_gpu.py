@@ -96,7 +96,8 @@ def test_wide_step_layer_by_layer_vs_oracle(gpu):
 
     # conv1 (f32 VALU) -> a1 bf16
     a1 = _nchw(c._a1)
-    bf16_close(a1, bf(np.maximum(W.conv3x3p1(xs, P0["conv1.weight"], P0["conv1.bias"]), 0)))
+    xb = bf(xs)
+    bf16_close(a1, bf(np.maximum(W.conv3x3p1(xb, bf(P0["conv1.weight"]), P0["conv1.bias"]), 0)))
     # conv2 + pool on the GPU's a1
     W2b, W3b = bf(P0["conv2.weight"]), bf(P0["conv3.weight"])
     c2 = W.conv3x3p1(a1, W2b, P0["conv2.bias"])
@@ -140,7 +141,7 @@ def test_wide_step_layer_by_layer_vs_oracle(gpu):
     dW2, db2 = W.conv3x3p1_wgrad(a1, dc2_g)
     grad_close(g[1792:75520].reshape(128, 64, 3, 3), dW2)
     grad_close(g[75520:75648], db2)
-    dW1, db1 = W.conv3x3p1_wgrad(xs, _nchw(c._da1m))
+    dW1, db1 = W.conv3x3p1_wgrad(xb, _nchw(c._da1m))
     grad_close(g[:1728].reshape(64, 3, 3, 3), dW1)
     grad_close(g[1728:1792], db1)
     # Adam (t = 1) on the GPU's own gradients
