@@ -1,4 +1,5 @@
-"""Minimal driver for profiling: N eager split steps at batch B (default 4096) on cuda:0."""
+"""Minimal driver for profiling: N eager split steps (k2: reference CNN fp32; k5: widened bf16) at batch B
+(default 4096) on cuda:0."""
 import argparse
 import os
 import sys
@@ -14,10 +15,16 @@ from splitcnn.engine import SplitTrainer  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=3)
+ap.add_argument("--config", default="k2", choices=["k2", "k5"])
 args = ap.parse_args()
-x, y = SyntheticMNIST(42).batch(args.batch)
+if args.config == "k5":
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    x, y = SyntheticCIFAR(42).batch(args.batch)
+    tr = WideTrainer(*init_wide_models(seed=0), device="cuda:0", graph=False)
+else:
+    x, y = SyntheticMNIST(42).batch(args.batch)
+    tr = SplitTrainer(*init_models(seed=0), device="cuda:0", graph=False)
 x, y = x.cuda(), y.cuda()
-tr = SplitTrainer(*init_models(seed=0), device="cuda:0", graph=False)
 for _ in range(args.steps):
     tr.step(x, y)
 torch.cuda.synchronize()
