@@ -260,6 +260,32 @@ def run_distributed(args, out, rank, world, local):
     if topo in ("pipeline", "hub"):
         out["exchange"] = {"topology": topo, "bytes_per_step": t.exchange_bytes,
                            "GBps_effective": round(t.exchange_bytes / (dt / args.steps) / 1e9, 2)}
+    if not args.no_k5 and world >= 2:
+        # BASELINE config 5 SplitFed: N-1 client GPUs run the widened conv stack, GPU N-1 the head
+        try:
+            from splitcnn.wide import SyntheticCIFAR, WideClientStage, WideServerStage, init_wide_models
+            Bk = args.k5_batch
+            wgrp = sd.client_group_for(world)
+            wa, wb = init_wide_models(seed=0)
+            if rank < world - 1:
+                data = SyntheticCIFAR(42 + rank)
+                xs, ys = zip(*(data.batch(Bk) for _ in range(2)))
+                WX, WY = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
+                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=wgrp)
+                wfn = lambda i: wt.client_step(WX[i % 2], WY[i % 2])  # noqa: E731
+            else:
+                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=wgrp)
+                wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
+            Kw = max(3, min(args.steps, 10))
+            dtw = timed(wfn, Kw, 2, dev)
+            Gw = (world - 1) * Bk
+            out["widened_hub"] = {"workload": f"K5 SplitFed: {world - 1} client GPU(s) (widened conv stack, bf16) + "
+                                              "1 server GPU (dropout/fc/CE head), client all-reduce",
+                                  "samples_per_s": round(Kw * Gw / dtw, 1), "ms_per_step": round(dtw / Kw * 1e3, 3),
+                                  "global_batch": Gw, "exchange_bytes_per_step": wt.exchange_bytes,
+                                  "exchange_GBps_effective": round(wt.exchange_bytes / (dtw / Kw) / 1e9, 2)}
+        except Exception as e:
+            out["widened_hub"] = {"error": repr(e)[:300]}
     if topo == "replicated" and not args.no_exchange_phase:
         try:
             ex = "pipeline" if world == 2 else "hub"

@@ -319,6 +319,71 @@ class UShaped:
         self.global_step += 1
 
 
+class WideHub:
+    """SplitFed for the widened model (BASELINE config 5, splitcnn/wide.py): client ranks 0..N-2 run
+    the conv stack (99.9 % of the step's FLOPs), the server rank N-1 the dropout/fc head. Per step each
+    client sends its cut (bf16, 32 KB/sample) + labels, the server runs ONE head step on the
+    concatenated (N-1)*B batch (mean loss and dropout indices over the global batch), returns each
+    client its cut-gradient slice, and the clients all-reduce their weight gradient (370,816 f32)
+    before identical Adam steps: exactly the single-process widened step at batch (N-1)*B.
+    Stages: client.forward / backward_grads / step_from_grads / grads / cut_shape / cut_dtype;
+    server.step_request(cuts, labels) -> (dcut, loss_i)."""
+
+    def __init__(self, stage, rank: int, world: int, client_group=None):
+        self.stage, self.rank, self.world = stage, rank, world
+        self.server_rank = world - 1
+        self.nclients = world - 1
+        self.client_group = client_group
+        self.global_step = 0
+        self._bufs = {}
+        self.exchange_bytes = 0
+
+    def _buf(self, name, shape, dtype, device):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != device or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self._bufs[name] = t
+        return t
+
+    def client_step(self, x, y):
+        c = self.stage
+        B = x.shape[0]
+        cut = c.forward(x)
+        dcut = self._buf("dcut", c.cut_shape(B), c.cut_dtype, x.device)
+        w1 = dist.isend(cut, self.server_rank)
+        w2 = dist.isend(y, self.server_rank)
+        r = dist.irecv(dcut, self.server_rank)
+        r.wait()
+        c.backward_grads(dcut)
+        w1.wait()
+        w2.wait()
+        if self.nclients > 1:
+            dist.all_reduce(c.grads, group=self.client_group)
+        c.step_from_grads()
+        self.exchange_bytes = 2 * cut.numel() * cut.element_size() + y.numel() * 8
+        self.global_step += 1
+
+    def server_step(self, B: int, device, cut_shape, cut_dtype):
+        """B = per-client batch; cut_shape(n) / cut_dtype describe the client stage's cut tensor."""
+        s = self.stage
+        G = self.nclients * B
+        cuts = self._buf("cuts", cut_shape(G), cut_dtype, device)
+        labels = self._buf("labels", (G,), torch.int64, device)
+        reqs = []
+        for c in range(self.nclients):
+            sl = slice(c * B, (c + 1) * B)
+            reqs.append(dist.irecv(cuts[sl], c))
+            reqs.append(dist.irecv(labels[sl], c))
+        for r in reqs:
+            r.wait()
+        dcut, _ = s.step_request(cuts, labels, step=self.global_step)
+        sends = [dist.isend(dcut[c * B:(c + 1) * B], c) for c in range(self.nclients)]
+        for w in sends:
+            w.wait()
+        self.exchange_bytes = 2 * cuts.numel() * cuts.element_size() + labels.numel() * 8
+        self.global_step += 1
+
+
 def client_group_for(world: int):
     """The all-reduce group of the hub's client ranks (every rank must call this, in order)."""
     if world < 3:

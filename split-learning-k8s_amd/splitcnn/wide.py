@@ -254,6 +254,30 @@ class WideClientStage:
     def backward_step(self, dcut: torch.Tensor):
         self.step_from_slabs(*self.backward_slabs(dcut))
 
+    # --- multi-GPU (dist.WideHub): gradient into self.grads, all-reduced by the caller, then Adam
+    cut_dtype = _BF
+
+    @staticmethod
+    def cut_shape(B: int):
+        return (B,) + CUT_SHAPE
+
+    def backward_grads(self, dcut: torch.Tensor):
+        """activations.backward(grads) into the flat gradient block (fixed-order slab reduction)."""
+        s1, s2, s3 = self.backward_slabs(dcut)
+        st = _stream(dcut)
+        for lo, n, sl in ((0, 1792, s1), (1792, 73856, s2), (75648, 295168, s3)):
+            with TIMER("reduce_slabs"):
+                _lib.call("slk_reduce_slabs", sl.data_ptr(), sl.shape[0], n, self.grads[lo:].data_ptr(), 0, st)
+
+    def step_from_grads(self):
+        """Adam from self.grads (e.g. after an all-reduce over the client ranks)."""
+        g = self.grads
+        _k("adam_from_slabs", self.params.data_ptr(), None, self.m.data_ptr(), self.v.data_ptr(), g.data_ptr(), 1,
+           CLIENT_NPARAM, float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+           self.step_ctr.data_ptr(), _stream(g))
+        self.refresh_shadows()
+        _k("tick", self.step_ctr.data_ptr(), _stream(g))
+
 
 class WideServerStage:
     """Server half: step_request(cut, labels, step) -> (dcut, loss_i): dropout + fc + CE forward and

@@ -37,6 +37,25 @@ def _batches(n_samples):
     return [d.batch(n_samples) for _ in range(STEPS)]
 
 
+WB = 2  # per-client batch of the widened hub test
+
+
+def _wide_init():
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from splitcnn.wide import init_wide_models
+    A, Bm = init_wide_models(seed=0)
+    return {k: v.detach().double().numpy() for k, v in list(A.state_dict().items()) + list(Bm.state_dict().items())}
+
+
+def _wide_batches(n_samples):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from splitcnn.wide import SyntheticCIFAR
+    d = SyntheticCIFAR(5)
+    return [d.batch(n_samples) for _ in range(STEPS)]
+
+
 def _worker(rank, world, port, topo, outdir):
     import sys
     sys.path[:0] = [PKG, ROOT]
@@ -93,6 +112,22 @@ def _worker(rank, world, port, topo, outdir):
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"))
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
+        elif topo == "widehub":
+            from oracle.wide_stages import OracleWideClient, OracleWideServer
+            Pw = _wide_init()
+            batches = _wide_batches((world - 1) * WB)
+            grp = sd.client_group_for(world)
+            if rank < world - 1:
+                t = sd.WideHub(OracleWideClient(Pw), rank, world, client_group=grp)
+                for x, y in batches:
+                    sl = slice(rank * WB, (rank + 1) * WB)
+                    t.client_step(x[sl].contiguous(), y[sl].contiguous())
+                res = t.stage.named()
+            else:
+                t = sd.WideHub(OracleWideServer(Pw), rank, world, client_group=grp)
+                for _ in batches:
+                    t.server_step(WB, torch.device("cpu"), OracleWideClient.cut_shape, OracleWideClient.cut_dtype)
+                res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
         np.savez(os.path.join(outdir, f"r{rank}.npz"), **{k: np.asarray(v) for k, v in res.items()})
     finally:
         dist.destroy_process_group()
@@ -132,6 +167,27 @@ def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
                 np.testing.assert_allclose(outs[r]["losses"], losses, rtol=1e-6)
             else:
                 np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-6 * np.abs(P[k]).max())
+
+def test_widened_splitfed_hub_equals_single_process_step(tmp_path):
+    """dist.WideHub (BASELINE config 5 SplitFed: 2 client ranks -> 1 server rank, client all-reduce)
+    equals oracle/wide_step.py's single-process widened step at the concatenated batch, step by step."""
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    from oracle import wide_step as Wd
+    world = 3
+    mp.spawn(_worker, args=(world, _port(), "widehub", str(tmp_path)), nprocs=world, join=True)
+    P, opt, losses = _wide_init(), {}, []
+    for t, (x, y) in enumerate(_wide_batches((world - 1) * WB), start=1):
+        P, opt, rec = Wd.wide_step(P, opt, t, x.double().numpy(), y.numpy(), seed=0, bf=False)
+        losses.append(rec["loss"])
+    outs = [dict(np.load(tmp_path / f"r{r}.npz")) for r in range(world)]
+    for r in range(world - 1):
+        for k in Wd.CLIENT_KEYS:
+            np.testing.assert_allclose(outs[r][k], P[k], rtol=0, atol=1e-9 * np.abs(P[k]).max(), err_msg=k)
+    for k in Wd.SERVER_KEYS:
+        np.testing.assert_allclose(outs[world - 1][k], P[k], rtol=0, atol=1e-9 * np.abs(P[k]).max(), err_msg=k)
+    np.testing.assert_allclose(outs[world - 1]["losses"], losses, rtol=1e-10)
+
 
 FED_B = (4, 2)     # unequal local batches: FedAvg weights must follow the sample counts
 FED_ROUNDS = (2, 1)  # local steps per round
