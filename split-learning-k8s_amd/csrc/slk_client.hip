@@ -64,10 +64,17 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
 // channels, the cut gradient and the activation (relu-bwd mask act > 0) as coalesced rows, keeping
 // 8 x 10 accumulators. A fixed-order block reduction writes the group's slab row
 // [dW1 c*9+tap (288) | db1 c (32)] (the client flat layout) for those 8 channels.
+// REMASK = true: the ReLU mask is recomputed from x, W1, b1 with conv1_fwd_kernel's exact FMA order
+// (s = fma chain over taps from 0, then + bias; act > 0 <=> s > 0), so act is never read: the kernel
+// moves 89.6 KB per sample instead of 176 KB. Valid whenever W1/b1 are the weights of the forward
+// (true inside a split step: the client's SGD comes after its backward).
 constexpr int C1W_G = 16;
 constexpr int C1W_CG = 4;
+template <bool REMASK>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ act,
+                                                          const float* __restrict__ W1,
+                                                          const float* __restrict__ b1,
                                                           const float* __restrict__ gcut,
                                                           float* __restrict__ slabs, int B) {
     __shared__ float red[4][C1W_CG * 10];
@@ -108,23 +115,36 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
 #pragma unroll
             for (int u = 0; u < C1F_PPT; ++u) {
                 gv[c][u] = gb[c * A_PIX + pix[u]];
-                av[c][u] = ab[c * A_PIX + pix[u]];
+                av[c][u] = REMASK ? 0.f : ab[c * A_PIX + pix[u]];
             }
+        float xv[C1F_PPT][9];
+#pragma unroll
+        for (int u = 0; u < C1F_PPT; ++u)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) xv[u][k] = xi[xo[u] + (k / 3) * IN_HW + k % 3];
 #pragma unroll
         for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
             for (int u = 0; u < C1F_PPT; ++u) asm volatile("" : "+v"(gv[c][u]), "+v"(av[c][u]));
+        if (REMASK) {
+#pragma unroll
+            for (int c = 0; c < C1W_CG; ++c) {
+                const float* w = W1 + (c0 + c) * 9;
+#pragma unroll
+                for (int u = 0; u < C1F_PPT; ++u) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) t = fmaf(xv[u][k], w[k], t);
+                    av[c][u] = t + b1[c0 + c];
+                }
+            }
+        }
         float gm[C1W_CG][C1F_PPT];
 #pragma unroll
         for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
             for (int u = 0; u < C1F_PPT; ++u)
                 gm[c][u] = av[c][u] > 0.f ? gv[c][u] * valid[u] : 0.f;  // threshold_backward mask
-        float xv[C1F_PPT][9];
-#pragma unroll
-        for (int u = 0; u < C1F_PPT; ++u)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) xv[u][k] = xi[xo[u] + (k / 3) * IN_HW + k % 3];
 #pragma unroll
         for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
@@ -169,6 +189,16 @@ extern "C" int slk_conv1_wgrad(const float* x, const float* act, const float* cu
     if (B == 0) return 0;
     SLK_CHECK_ARG(x && act && cut_grad && slabs);
     dim3 grid(slk_conv1_wgrad_nslab(B), C1 / C1W_CG);
-    conv1_wgrad_kernel<<<grid, 256, 0, slk_stream(stream)>>>(x, act, cut_grad, slabs, B);
+    conv1_wgrad_kernel<false><<<grid, 256, 0, slk_stream(stream)>>>(x, act, nullptr, nullptr, cut_grad, slabs, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv1_wgrad_remask(const float* x, const float* W1, const float* b1, const float* cut_grad,
+                                      float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(x && W1 && b1 && cut_grad && slabs);
+    dim3 grid(slk_conv1_wgrad_nslab(B), C1 / C1W_CG);
+    conv1_wgrad_kernel<true><<<grid, 256, 0, slk_stream(stream)>>>(x, nullptr, W1, b1, cut_grad, slabs, B);
     return slk_launch_status();
 }

@@ -31,6 +31,24 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// Build-time knobs (tools/ablate_wide.py builds variants): weight lookahead of the conv stream, and
+// XCD grouping of tiles (all row blocks / channel blocks of one image on one XCD at the same time,
+// so halo rows and shared input tiles are L2 hits).
+#ifndef SLK_WIDE_XCD
+#define SLK_WIDE_XCD 1
+#endif
+#ifndef SLK_WIDE_PF
+#define SLK_WIDE_PF 1
+#endif
+// Profiling-only ablation bits of the non-prefetch conv loop (tools/ablate_wide.py): 1 = no DMA in
+// the loop, 2 = no MFMA, 4 = no LDS fragment reads, 8 = no waits / barriers. Production = 0.
+#ifndef SLK_WABL
+#define SLK_WABL 0
+#endif
+#ifndef SLK_WIDE_L
+#define SLK_WIDE_L (SLK_WIDE_PF ? 3 : 2)
+#endif
+
 namespace wide {
 constexpr int IMG = 32;                 // input 3 x 32 x 32
 constexpr int C1 = 64, C2 = 128, C3 = 256;
@@ -57,11 +75,14 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // ----------------------------------------------------------------------------- conv geometry
-template <int CI_, int CO_, int HW_, int MT_, int MODE_>
+template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_>
 struct ConvCfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = MT_, MODE = MODE_;
-    static constexpr int NPX = MT == 128 ? 128 : 256;       // pixels per tile (4 waves of 64 x 64)
-    static constexpr int WN = NPX / 64;                     // waves along pixels
+    static constexpr int FW = FW_;                          // 16-pixel fragments per wave (wave tile 64 x 16*FW)
+    static constexpr int NWV = NWV_;                        // waves per workgroup (4: 2 WGs/CU; 8: 1 WG/CU)
+    static constexpr int THREADS = NWV * 64;
+    static constexpr int WM = MT / 64, WN = NWV / WM;       // WM waves along channels x WN along pixels
+    static constexpr int NPX = WN * 16 * FW;                // pixels per tile
     static constexpr int TR = NPX / HW;                     // image rows per tile
     static constexpr int PW = HW + 2;                       // LDS row pitch (pixels, with halo)
     static constexpr int NP = (TR + 2) * PW;
@@ -71,16 +92,19 @@ struct ConvCfg {
     static constexpr int S = G * 9;                         // steps per tile
     static constexpr int IN_SLOT = NPP * 64;                // bytes: 4 chunks x NPP x 16
     static constexpr int W_SLOT = MT * 64;                  // bytes: 4 chunks x MT x 16
-    static constexpr int NW = W_SLOT / 1024 / 4;            // weight DMA instructions per wave per step
-    static constexpr int L = 2;                             // weight lookahead (steps)
+    static constexpr int NW = W_SLOT / 1024 / NWV;          // weight DMA instructions per wave per step
+    static constexpr int DSPLIT = NWV / 4;                  // waves sharing one input chunk plane
+    static constexpr int NDW = ND / DSPLIT;                 // input DMA instructions per wave per group
+    static constexpr int L = SLK_WIDE_L;                    // weight lookahead (steps)
     static constexpr int RW = L + 1;                        // weight ring slots
     static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
     static constexpr int RB = HW / TR;                      // row blocks per image
     static constexpr int NCB = CO / MT;                     // output-channel blocks
     static constexpr int FPR = HW / 16;                     // 16-pixel fragments per image row
     static_assert(MT == 128 || MT == 64, "MT");
-    static_assert(HW % TR == 0 && TR % 2 == 0 && (64 % HW == 0 || HW == 64), "tile rows");
-    static_assert(NW >= 1 && (W_SLOT % 4096) == 0, "weight slot must split over 4 waves");
+    static_assert(HW % TR == 0 && TR % 2 == 0 && (16 * FW) % (2 * HW) == 0, "tile rows / pool pairs per wave");
+    static_assert(NW >= 1 && W_SLOT % (1024 * NWV) == 0, "weight slot must split over the waves");
+    static_assert(ND % DSPLIT == 0, "input planes must split over the waves");
     static_assert(NCB == 1 || NCB == 2, "NCB");
 };
 
@@ -90,10 +114,18 @@ struct TileState {
 
 template <class C>
 __device__ __forceinline__ TileState tile_state(int t, int B) {
-    // XCD-aware: with NCB = 2 the two channel blocks of a pixel tile are tiles t and t + 8, i.e.
-    // blocks b and b + 8 of a grid that is a multiple of 16 — the same XCD under round-robin
-    // placement, so the second reads the input tile from L2. (Speed only; any placement is correct.)
+    // Blocks b and b + 8 of a grid that is a multiple of 8 share an XCD under round-robin placement
+    // and process tiles t and t + 8 in the same round. XCD grouping sends all RB x NCB tiles of image
+    // n to XCD (n % 8) in one round: neighbouring row blocks share halo rows and the channel blocks
+    // share the input tile through that XCD's L2. (Speed only; any placement is correct.)
     TileState s;
+#if SLK_WIDE_XCD
+    const int xcd = t & 7, j = t >> 3;
+    s.rb = j % C::RB;
+    s.cob = (j / C::RB) % C::NCB;
+    s.n = (j / (C::RB * C::NCB)) * 8 + xcd;
+    s.valid = s.n < B;
+#else
     int pt;
     if (C::NCB == 2) {
         s.cob = (t >> 3) & 1;
@@ -105,32 +137,37 @@ __device__ __forceinline__ TileState tile_state(int t, int B) {
     s.valid = pt < B * C::RB;
     s.n = pt / C::RB;
     s.rb = pt - s.n * C::RB;
+#endif
     return s;
 }
 
 template <class C>
-__device__ __forceinline__ void tile_poff(const TileState& s, int lane, int (&poff)[C::ND]) {
+__device__ __forceinline__ void tile_poff(const TileState& s, int wave, int lane, int (&poff)[C::NDW]) {
+    // this wave's DMA pieces of its chunk plane: d = (wave / 4) + k * DSPLIT
 #pragma unroll
-    for (int d = 0; d < C::ND; ++d) {
+    for (int k = 0; k < C::NDW; ++k) {
+        const int d = (wave >> 2) + k * C::DSPLIT;
         const int P = d * 64 + lane;
         const int ry = P / C::PW, rx = P - (P / C::PW) * C::PW;
         const int y = s.rb * C::TR - 1 + ry, x = rx - 1;
         const bool ok = P < C::NP && y >= 0 && y < C::HW && x >= 0 && x < C::HW;
-        poff[d] = ok ? y * C::HW + x : -1;
+        poff[k] = ok ? y * C::HW + x : -1;
     }
 }
 
 // input tile of group g (chunks 4g .. 4g+3) -> LDS slot; wave w moves chunk plane w
 template <class C>
 __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, const TileState& s,
-                                            const int (&poff)[C::ND], int g, char* slot, int wave, int lane) {
+                                            const int (&poff)[C::NDW], int g, char* slot, int wave, int lane) {
+    const int c = wave & 3;
     const char* plane = reinterpret_cast<const char*>(in) +
-                        ((size_t)(s.n * (C::CI / 8) + g * 4 + wave) * (C::HW * C::HW)) * 16;
+                        ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * (C::HW * C::HW)) * 16;
     const char* zero = reinterpret_cast<const char*>(slk_wide_zero);
-    char* dst = slot + wave * C::NPP * 16;
+    char* dst = slot + c * C::NPP * 16;
 #pragma unroll
-    for (int d = 0; d < C::ND; ++d) {
-        const char* src = poff[d] >= 0 ? plane + (size_t)poff[d] * 16 : zero;
+    for (int k = 0; k < C::NDW; ++k) {
+        const int d = (wave >> 2) + k * C::DSPLIT;
+        const char* src = poff[k] >= 0 ? plane + (size_t)poff[k] * 16 : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + d * 1024), 16, 0, 0);
     }
 }
@@ -154,7 +191,7 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
 // out: forward = pooled bf16 C8 [B][CO/8][HW/2][HW/2][8] (+ code u8 same layout in out2);
 //      dgrad-unpool = bf16 C8 [B][CO/8][2HW][2HW][8]; dgrad-mask = bf16 C8 [B][CO/8][HW][HW][8].
 template <class C>
-__global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __restrict__ in,
+__global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t* __restrict__ in,
                                                            const uint16_t* __restrict__ wsh,
                                                            const void* __restrict__ aux,
                                                            uint16_t* __restrict__ out,
@@ -173,16 +210,16 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
     if (!cur.valid) return;
     int tn = t + grid;
     TileState nxt = tile_state<C>(tn, B);
-    int pcur[C::ND], pnxt[C::ND];
-    tile_poff<C>(cur, lane, pcur);
-    tile_poff<C>(nxt, lane, pnxt);
+    int pcur[C::NDW], pnxt[C::NDW];
+    tile_poff<C>(cur, wave, lane, pcur);
+    tile_poff<C>(nxt, wave, lane, pnxt);
 
     // per-lane fragment read offsets (bytes, relative to the slot)
     const int a_off = ((lane >> 4) * C::MT + wm * 64 + (lane & 15)) * 16;
-    int b_off[4];
+    int b_off[C::FW];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        const int q = wn * 64 + f * 16 + (lane & 15);
+    for (int f = 0; f < C::FW; ++f) {
+        const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
         const int r = q / C::HW, x = q - (q / C::HW) * C::HW;
         b_off[f] = ((lane >> 4) * C::NPP + (r + 1) * C::PW + x + 1) * 16;
     }
@@ -196,36 +233,50 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
             for (int r = 0; r < 4; ++r) bias[i][r] = b[cur.cob * C::MT + wm * 64 + i * 16 + 4 * (lane >> 4) + r];
     }
 
-    // prologue: input group 0 of the first tile, then weight steps 0 .. L-1
+#if SLK_WIDE_PF
+    // Fragment prefetch: during step s the MFMAs consume fragments read in step s-1 while the reads
+    // for step s+1 are in flight, so no step opens with an LDS-latency bubble. The wait of step s
+    // therefore covers weight step s+1 (issued 2 steps earlier; lookahead L = 3, 4 ring slots) and,
+    // at tap 8, the next group's input tile.
+    static_assert(C::L == 3, "prefetch schedule assumes a weight lookahead of 3");
     issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
 #pragma unroll
     for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
-
+    if (!nxt.valid && C::S == 1) wait_vmcnt<0>();
+    else wait_vmcnt<2 * C::NW>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16x8 av_n[4], bv_n[C::FW];
+    {
+        const int toff = -(C::PW + 1) * 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av_n[i] = *reinterpret_cast<const bf16x8*>(wslot0 + a_off + i * 256);
+#pragma unroll
+        for (int f = 0; f < C::FW; ++f) bv_n[f] = *reinterpret_cast<const bf16x8*>(islot0 + b_off[f] + toff);
+    }
     int wslot = 0;   // ring slot of the current step
     int islot = 0;   // input slot of the current group
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
-        f32x4 acc[4][4];
+        f32x4 acc[4][C::FW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int f = 0; f < 4; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int f = 0; f < C::FW; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
         for (int g = 0; g < C::G; ++g) {
-            const char* ib = islot0 + islot * C::IN_SLOT;
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                // this step's weight slice (and, at tap 0, this group's input tile) has landed
+                const bool last = tail && g == C::G - 1 && tap == 8;
+                // step s+1's weight slice (and at tap 8 the next group's input tile) has landed
                 if (tail) wait_vmcnt<0>();
-                else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::ND>();
-                else wait_vmcnt<(C::L - 1) * C::NW>();
+                else if (tap == 1 || tap == 2) wait_vmcnt<C::NW + C::NDW>();
+                else wait_vmcnt<C::NW>();
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
-                // lookahead: weight step +L (ring slot of step -1, free since the barrier), then at
-                // tap 0 the next group's input tile (slot of group -1)
-                {
+                {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
                     const int sl = g * 9 + tap + C::L;
                     int ws = wslot + C::L;
                     ws = ws >= C::RW ? ws - C::RW : ws;
@@ -237,23 +288,107 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
                     if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
                     else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
                 }
-                const char* wb = wslot0 + wslot * C::W_SLOT;
-                const int toff = ((tap / 3 - 1) * C::PW + (tap % 3 - 1)) * 16;
-                bf16x8 av[4], bv[4];
+                bf16x8 av[4], bv[C::FW];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const bf16x8*>(wb + a_off + i * 256);
+                for (int i = 0; i < 4; ++i) av[i] = av_n[i];
 #pragma unroll
-                for (int f = 0; f < 4; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
+                for (int f = 0; f < C::FW; ++f) bv[f] = bv_n[f];
+                const int wn1 = wslot + 1 == C::RW ? 0 : wslot + 1;
+                if (!last) {
+                    const char* wb = wslot0 + wn1 * C::W_SLOT;
+                    const char* ib = islot0 + (tap == 8 ? (islot ^ 1) : islot) * C::IN_SLOT;
+                    const int tn = tap == 8 ? 0 : tap + 1;
+                    const int toff = ((tn / 3 - 1) * C::PW + (tn % 3 - 1)) * 16;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) av_n[i] = *reinterpret_cast<const bf16x8*>(wb + a_off + i * 256);
+#pragma unroll
+                    for (int f = 0; f < C::FW; ++f) bv_n[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
+                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int f = 0; f < 4; ++f)
+                    for (int f = 0; f < C::FW; ++f)
                         acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
+                wslot = wn1;
+            }
+            islot ^= 1;
+        }
+#else
+    // prologue: input group 0 of the first tile, then weight steps 0 .. L-1
+    issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
+#pragma unroll
+    for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
+
+    int wslot = 0;   // ring slot of the current step
+    int islot = 0;   // input slot of the current group
+#pragma unroll 1
+    while (true) {
+        const bool tail = !nxt.valid;
+        f32x4 acc[4][C::FW];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int f = 0; f < C::FW; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+        for (int g = 0; g < C::G; ++g) {
+            const char* ib = islot0 + islot * C::IN_SLOT;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                // this step's weight slice (and, at tap 0, this group's input tile) has landed
+                if (!(SLK_WABL & 8)) {
+                    if (tail || (SLK_WABL & 1)) wait_vmcnt<0>();
+                    else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
+                    else wait_vmcnt<(C::L - 1) * C::NW>();
+                    __builtin_amdgcn_s_barrier();
+                }
+                asm volatile("" ::: "memory");
+                // lookahead: weight step +L (ring slot of step -1, free since the barrier), then at
+                // tap 0 the next group's input tile (slot of group -1)
+                if (!(SLK_WABL & 1)) {
+                    const int sl = g * 9 + tap + C::L;
+                    int ws = wslot + C::L;
+                    ws = ws >= C::RW ? ws - C::RW : ws;
+                    if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                    else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
+                }
+                if (tap == 0 && !(SLK_WABL & 1)) {
+                    char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
+                    if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
+                    else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
+                }
+                const char* wb = wslot0 + wslot * C::W_SLOT;
+                const int toff = ((tap / 3 - 1) * C::PW + (tap % 3 - 1)) * 16;
+                bf16x8 av[4], bv[C::FW];
+#if SLK_WABL & 4
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { av[i] = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) int){a_off + i, tap, 0, 0}); slk_keep(av[i]); }
+#pragma unroll
+                for (int f = 0; f < C::FW; ++f) { bv[f] = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) int){b_off[f], tap, 0, 0}); slk_keep(bv[f]); }
+#else
+#pragma unroll
+                for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const bf16x8*>(wb + a_off + i * 256);
+#pragma unroll
+                for (int f = 0; f < C::FW; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
+#endif
+#if SLK_WABL & 2
+#pragma unroll
+                for (int i = 0; i < 4; ++i) slk_keep(av[i]);
+#pragma unroll
+                for (int f = 0; f < C::FW; ++f) slk_keep(bv[f]);
+#else
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int f = 0; f < C::FW; ++f)
+                        acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
+#endif
                 wslot = wslot + 1 == C::RW ? 0 : wslot + 1;
             }
             islot ^= 1;
         }
 
+#endif
         // ------------------------------------------------------------------ epilogue
         const int ch_base = cur.cob * C::MT + wm * 64 + 4 * (lane >> 4);
         if constexpr (C::MODE == wide::MODE_FWD_POOL) {
@@ -262,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
             for (int i = 0; i < 4; ++i) {
                 const int ch0 = ch_base + i * 16;
 #pragma unroll
-                for (int f = 0; f < 4; ++f) {
+                for (int f = 0; f < C::FW; ++f) {
                     if ((f / C::FPR) & 1) continue;       // bottom row of a window pair
                     const int fb = f + C::FPR;
                     float pv[4];
@@ -283,7 +418,7 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
                         cw |= (uint32_t)(best > 0.f ? idx : slk::CODE_NONE) << (8 * r);
                     }
                     if ((lane & 1) == 0) {
-                        const int q = wn * 64 + f * 16 + (lane & 15);
+                        const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                         const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                         const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * PH + (y >> 1)) * PH + (x >> 1)) * 8 + (ch0 & 7);
                         *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
@@ -298,8 +433,8 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
             for (int i = 0; i < 4; ++i) {
                 const int ch0 = ch_base + i * 16;
 #pragma unroll
-                for (int f = 0; f < 4; ++f) {
-                    const int q = wn * 64 + f * 16 + (lane & 15);
+                for (int f = 0; f < C::FW; ++f) {
+                    const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
                     const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + ((plane * C::HW + y) * C::HW + x) * 8 + (ch0 & 7));
@@ -319,8 +454,8 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
             for (int i = 0; i < 4; ++i) {
                 const int ch0 = ch_base + i * 16;
 #pragma unroll
-                for (int f = 0; f < 4; ++f) {
-                    const int q = wn * 64 + f * 16 + (lane & 15);
+                for (int f = 0; f < C::FW; ++f) {
+                    const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
                     const uint2 m = *reinterpret_cast<const uint2*>(a1 + o);
@@ -337,17 +472,23 @@ __global__ __launch_bounds__(256, 2) void wide_conv_kernel(const uint16_t* __res
         if (tail) break;
         cur = nxt;
 #pragma unroll
-        for (int d = 0; d < C::ND; ++d) pcur[d] = pnxt[d];
+        for (int d = 0; d < C::NDW; ++d) pcur[d] = pnxt[d];
         tn += grid;
         nxt = tile_state<C>(tn, B);
-        tile_poff<C>(nxt, lane, pnxt);
+        tile_poff<C>(nxt, wave, lane, pnxt);
     }
 }
 
-using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL>;
-using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL>;
-using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK>;
+#ifndef SLK_WIDE_FW
+#define SLK_WIDE_FW 4
+#endif
+#ifndef SLK_WIDE_NWV
+#define SLK_WIDE_NWV 4
+#endif
+using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4>;
 
 template <class C>
 static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux, uint16_t* out, uint8_t* out2,
@@ -356,9 +497,14 @@ static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux,
     if (C::MODE == wide::MODE_FWD_POOL) SLK_CHECK_ARG(out2 != nullptr);
     if (B == 0) return 0;
     const long ntiles = (long)B * C::RB * C::NCB;
-    long grid = 512;                                   // 2 workgroups per CU (256 CUs)
+    long grid = C::NWV == 4 ? 512 : 256;               // 2 (4-wave) or 1 (8-wave) workgroups per CU
+#if SLK_WIDE_XCD
+    const long span = 8L * ((B + 7) / 8) * C::RB * C::NCB;  // tile indices covering every image
+    if (span < grid) grid = span;                           // a multiple of 8
+#else
     if (ntiles < grid) grid = C::NCB == 2 ? ((ntiles + 15) / 16) * 16 : ntiles;
-    hipLaunchKernelGGL(wide_conv_kernel<C>, dim3((unsigned)grid), dim3(256), 0, slk_stream(stream), in, wsh, aux,
+#endif
+    hipLaunchKernelGGL(wide_conv_kernel<C>, dim3((unsigned)grid), dim3(C::THREADS), 0, slk_stream(stream), in, wsh, aux,
                        out, out2, B);
     return slk_launch_status();
 }
@@ -432,7 +578,6 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     if (C::NBLK == 1) { blk = 0; ks = w; }
     else { blk = (w >> 3) % C::NBLK; ks = ((w >> 3) / C::NBLK) * 8 + (w & 7); }
     const int cob = blk / C::NCIB, cib = blk - (blk / C::NCIB) * C::NCIB;
-    const int NT = B * C::RB;
 
     // per-lane transposed-read bases (bytes within a buffer)
     const int q = lane >> 4, ig = lane & 15, a = ig >> 2, p = ig & 3;
@@ -451,8 +596,26 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         for (int u = 0; u < 9; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // tile t -> (image, row block). XCD grouping: ks and ks + 8 share an XCD, so tiles t = ks + k*KSPLIT
+    // with equal t % 8 run there together; all RB row blocks of image n go to XCD n % 8.
+    auto tile_of = [&](int t, int& n, int& rb) {
+#if SLK_WIDE_XCD
+        const int j = t >> 3;
+        rb = j % C::RB;
+        n = (j / C::RB) * 8 + (t & 7);
+#else
+        n = t / C::RB;
+        rb = t - n * C::RB;
+#endif
+    };
+    auto valid = [&](int t) {
+        int n, rb;
+        tile_of(t, n, rb);
+        return n < B;
+    };
     auto issue_tile = [&](int t, char* buf) {
-        const int n = t / C::RB, rb = t - (t / C::RB) * C::RB;
+        int n, rb;
+        tile_of(t, n, rb);
         // dC rows: 16 chunk planes x (NPX*16/1024) KiB, 4 pieces per wave
         constexpr int PPC = C::NPX * 16 / 1024;
 #pragma unroll
@@ -480,13 +643,13 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     };
 
     int t = ks, b = 0;
-    if (t < NT) issue_tile(t, smem);
+    if (valid(t)) issue_tile(t, smem);
 #pragma unroll 1
-    for (; t < NT; t += C::KSPLIT) {
+    for (; valid(t); t += C::KSPLIT) {
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + C::KSPLIT < NT) issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
+        if (valid(t + C::KSPLIT)) issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
         const char* buf = smem + b * C::BUF;
 #pragma unroll
         for (int j = 0; j < C::KS; ++j) {

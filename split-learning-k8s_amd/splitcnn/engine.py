@@ -186,7 +186,9 @@ class ClientStage:
         B = x.shape[0]
         slabs = self._buf.get(tag, (ops.conv1_wgrad_nslab(B), ops.CLIENT_NPARAM), torch.float32, self.device)
         with TIMER("conv1_wgrad"):
-            ops.conv1_wgrad_slabs(x, act, cut_grad, slabs=slabs)
+            # the mask act > 0 is recomputed from x and W1 (unchanged since the forward: the client
+            # steps after its backward), so only x and cut_grad are read
+            ops.conv1_wgrad_remask_slabs(x, self.W1.detach(), self.b1.detach(), cut_grad, slabs=slabs)
         return slabs
 
     def backward_step(self, cut_grad: torch.Tensor, x: Optional[torch.Tensor] = None,

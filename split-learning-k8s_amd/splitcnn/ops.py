@@ -75,6 +75,18 @@ def conv1_wgrad_slabs(x, act, cut_grad, slabs=None):
     return slabs
 
 
+def conv1_wgrad_remask_slabs(x, W1, b1, cut_grad, slabs=None):
+    """conv1_wgrad_slabs with the ReLU mask recomputed from x, W1, b1 (bit-identical to act > 0 for
+    the forward's weights): half the HBM traffic, act is not read."""
+    B = batch_of(x, (1, 28, 28), "x")
+    nslab = conv1_wgrad_nslab(B)
+    slabs = _out(slabs, (nslab, CLIENT_NPARAM), x, name="slabs")
+    _lib.call("slk_conv1_wgrad_remask", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)),
+              _dev(b1, "conv1.bias", (32,)), _dev(cut_grad, "cut_grad", (B, 32, 26, 26)), _dev(slabs, "slabs"),
+              B, _stream(x))
+    return slabs
+
+
 # ------------------------------------------------------------------------------------ server stage
 def conv2_fwd_pool(act, W2, b2, pooled=None, code=None):
     B = batch_of(act, (32, 26, 26), "act")

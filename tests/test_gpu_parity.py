@@ -269,3 +269,21 @@ def test_cpu_tensors_raise(gpu):
     m = ModelPartA()
     with pytest.raises(RuntimeError, match="HIP kernels"):
         m(torch.zeros(2, 1, 28, 28))
+
+
+@pytest.mark.gpu
+def test_conv1_wgrad_remask_bit_identical_to_act_mask(gpu):
+    """slk_conv1_wgrad_remask recomputes the ReLU mask from x, W1, b1 in conv1_fwd's FMA order: its
+    slabs must equal slk_conv1_wgrad's (mask read from act) bit for bit, incl. a ragged batch."""
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    a, _ = init_models(seed=0)
+    W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
+    for B in (5, 4096):
+        x, _y = SyntheticMNIST(3).batch(B)
+        x = x.to(gpu)
+        act = ops.conv1_fwd(x, W1, b1)
+        g = torch.randn(B, 32, 26, 26, generator=torch.Generator().manual_seed(1)).to(gpu)
+        s_act = ops.conv1_wgrad_slabs(x, act, g)
+        s_rm = ops.conv1_wgrad_remask_slabs(x, W1, b1, g)
+        assert torch.equal(s_act, s_rm), B

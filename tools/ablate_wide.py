@@ -1,0 +1,93 @@
+"""Profiling-only: time the widened-model (K5) kernels of several libslk builds side by side in ONE
+process, interleaved rounds, HIP events on one stream (random operands: DVFS-realistic).
+usage: python tools/ablate_wide.py lib0.so lib1.so ... [--batch 4096 --rounds 5 --reps 5]"""
+import argparse
+import ctypes
+import json
+
+import torch
+
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="+")
+ap.add_argument("--batch", type=int, default=4096)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--reps", type=int, default=5)
+args = ap.parse_args()
+B = args.batch
+dev = torch.device("cuda:0")
+P = ctypes.c_void_p
+g = torch.Generator(device=dev).manual_seed(0)
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev, generator=g) * scale).to(torch.bfloat16)
+
+
+def codes(*shape):
+    return torch.randint(0, 5, shape, device=dev, generator=g).to(torch.uint8)
+
+
+x = torch.randn(B, 3, 32, 32, device=dev, generator=g)
+a1 = bf(B, 8, 32, 32, 8).abs()
+p2 = bf(B, 16, 16, 16, 8).abs()
+code2 = codes(B, 16, 16, 16, 8)
+cut = bf(B, 32, 8, 8, 8)
+code3 = codes(B, 32, 8, 8, 8)
+dcut = bf(B, 32, 8, 8, 8, scale=1e-3)
+dc3 = bf(B, 32, 16, 16, 8, scale=1e-3)
+dc2 = bf(B, 16, 32, 32, 8, scale=1e-3)
+da1m = bf(B, 8, 32, 32, 8, scale=1e-3)
+w1b, w2f, w2d, w3f, w3d = bf(64 * 32, scale=0.1), bf(73728, scale=0.05), bf(73728, scale=0.05), bf(294912, scale=0.03), bf(294912, scale=0.03)
+b1, b2, b3 = (torch.randn(n, device=dev, generator=g) * 0.01 for n in (64, 128, 256))
+out_a1 = torch.empty_like(a1)
+out_p2, out_c2 = torch.empty_like(p2), torch.empty_like(code2)
+out_cut, out_c3 = torch.empty_like(cut), torch.empty_like(code3)
+out_dc2, out_dc3, out_da1m = torch.empty_like(dc2), torch.empty_like(dc3), torch.empty_like(da1m)
+slabs = torch.empty(256 * (73728 + 128) + 64 * (294912 + 256), device=dev)
+s = torch.cuda.current_stream().cuda_stream
+p = lambda t: P(t.data_ptr())  # noqa: E731
+FLOP = 150_994_944 * B
+
+libs = []
+for path in args.libs:
+    L = ctypes.CDLL(path)
+    libs.append(L)
+
+
+def calls(L):
+    return {
+        "conv1_fwd": lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), B, P(s)),
+        "conv2_fwd": lambda: L.slk_wide_conv2_fwd(p(a1), p(w2f), p(b2), p(out_p2), p(out_c2), B, P(s)),
+        "conv3_fwd": lambda: L.slk_wide_conv3_fwd(p(p2), p(w3f), p(b3), p(out_cut), p(out_c3), B, P(s)),
+        "unpool": lambda: L.slk_wide_unpool(p(dcut), p(code3), p(out_dc3), B, P(s)),
+        "conv3_wgrad": lambda: L.slk_wide_conv3_wgrad(p(dc3), p(p2), p(slabs), B, P(s)),
+        "conv3_dgrad": lambda: L.slk_wide_conv3_dgrad(p(dc3), p(w3d), p(code2), p(out_dc2), B, P(s)),
+        "conv2_wgrad": lambda: L.slk_wide_conv2_wgrad(p(dc2), p(a1), p(slabs), B, P(s)),
+        "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dc2), p(w2d), p(a1), p(out_da1m), B, P(s)),
+        "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
+    }
+
+
+res = {i: {} for i in range(len(libs))}
+for r in range(args.rounds):
+    for i, L in enumerate(libs):
+        for name, fn in calls(L).items():
+            assert fn() == 0, name
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            res[i].setdefault(name, []).append(e0.elapsed_time(e1) / args.reps)
+out = {}
+for i, path in enumerate(args.libs):
+    d = {}
+    for name, v in res[i].items():
+        ms = sorted(v)[len(v) // 2]
+        d[name] = {"ms": round(ms, 4)}
+        if name.startswith(("conv2_", "conv3_")):
+            d[name]["TFs"] = round(FLOP / (ms * 1e-3) / 1e12, 1)
+    out[path] = d
+print(json.dumps(out, indent=1))
