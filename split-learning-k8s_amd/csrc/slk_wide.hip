@@ -78,6 +78,7 @@ __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)
 template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_>
 struct ConvCfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = MT_, MODE = MODE_;
+    static constexpr bool K32 = false;                      // 16x16x32 kernel (wide_conv_kernel)
     static constexpr int FW = FW_;                          // 16-pixel fragments per wave (wave tile 64 x 16*FW)
     static constexpr int NWV = NWV_;                        // waves per workgroup (4: 2 WGs/CU; 8: 1 WG/CU)
     static constexpr int THREADS = NWV * 64;
@@ -479,15 +480,260 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     }
 }
 
+
+
+// ----------------------------------------------------------------------------- 32x32x16 variant
+// Same stream and LDS images as wide_conv_kernel, but each wave owns a 64-channel x 128-pixel tile as
+// 2 x 4 v_mfma_f32_32x32x16_bf16 accumulators (128 VGPRs): per 32-channel step a wave issues 12
+// fragment reads for 16 MFMAs of 32 cycles (vs 8 reads for 16 MFMAs of 16 cycles), and every weight
+// slice streamed into LDS now serves 256 pixels — half the LDS-DMA instructions per FLOP of the
+// 64 x 64 / 16x16x32 form, at the same 2 workgroups per CU.
+// Fragment maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h+j]
+// and B[k = 8h+j][col r]; C/D: col = r, row = (reg & 3) + 8 (reg >> 2) + 4h.
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+template <int CI_, int CO_, int HW_, int MODE_>
+struct Conv32Cfg {
+    static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = 128, MODE = MODE_;
+    static constexpr bool K32 = true;
+    static constexpr int NWV = 4, THREADS = 256;
+    static constexpr int WM = 2, WN = 2;                    // waves: 2 along channels x 2 along pixels
+    static constexpr int NPX = WN * 128;                    // 256 pixels per tile
+    static constexpr int TR = NPX / HW;
+    static constexpr int PW = HW + 2;
+    static constexpr int NP = (TR + 2) * PW;
+    static constexpr int NPP = (NP + 63) / 64 * 64;
+    static constexpr int ND = NPP / 64;
+    static constexpr int DSPLIT = 1, NDW = ND;
+    static constexpr int G = CI / 32;
+    static constexpr int S = G * 9;
+    static constexpr int IN_SLOT = NPP * 64;
+    static constexpr int W_SLOT = MT * 64;
+    static constexpr int NW = W_SLOT / 1024 / NWV;          // 2
+    static constexpr int L = 2, RW = 3;
+    static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
+    static constexpr int RB = HW / TR;
+    static constexpr int NCB = CO / MT;
+    static_assert(HW % TR == 0 && TR % 2 == 0 && (HW == 32 || HW == 16), "tile rows");
+    static_assert(NCB == 1 || NCB == 2, "NCB");
+};
+
+template <class C>
+__global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __restrict__ in,
+                                                             const uint16_t* __restrict__ wsh,
+                                                             const void* __restrict__ aux,
+                                                             uint16_t* __restrict__ out,
+                                                             uint8_t* __restrict__ out2, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[C::LDS + C::MT * 4];   // + bias (fwd)
+    char* islot0 = smem;
+    char* wslot0 = smem + 2 * C::IN_SLOT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int r = lane & 31, h = lane >> 5;
+    const int grid = gridDim.x;
+
+    int t = blockIdx.x;
+    TileState cur = tile_state<C>(t, B);
+    if (!cur.valid) return;
+    int tn = t + grid;
+    TileState nxt = tile_state<C>(tn, B);
+    int pcur[C::NDW], pnxt[C::NDW];
+    tile_poff<C>(cur, wave, lane, pcur);
+    tile_poff<C>(nxt, wave, lane, pnxt);
+
+    // A: chunk (2ks + h), channel wm*64 + ct*32 + r;  B: chunk (2ks + h), pixel wn*128 + pt*32 + r
+    const int a_off = (h * C::MT + wm * 64 + r) * 16;
+    int b_off[4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+        const int q = wn * 128 + pt * 32 + r;
+        const int y = q / C::HW, x = q - (q / C::HW) * C::HW;
+        b_off[pt] = (h * C::NPP + (y + 1) * C::PW + x + 1) * 16;
+    }
+    float* bias_s = reinterpret_cast<float*>(smem + C::LDS);   // this workgroup's channel block (fixed cob)
+    if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+        if (tid < C::MT) bias_s[tid] = reinterpret_cast<const float*>(aux)[cur.cob * C::MT + tid];
+        __syncthreads();
+    }
+
+    issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
+#pragma unroll
+    for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
+
+    int wslot = 0, islot = 0;
+#pragma unroll 1
+    while (true) {
+        const bool tail = !nxt.valid;
+        f32x16v acc[2][4];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) acc[ct][pt][g] = 0.f;
+#pragma unroll 1
+        for (int g = 0; g < C::G; ++g) {
+            const char* ib = islot0 + islot * C::IN_SLOT;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                if (tail) wait_vmcnt<0>();
+                else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
+                else wait_vmcnt<(C::L - 1) * C::NW>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                {
+                    const int sl = g * 9 + tap + C::L;
+                    int ws = wslot + C::L;
+                    ws = ws >= C::RW ? ws - C::RW : ws;
+                    if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                    else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
+                }
+                if (tap == 0) {
+                    char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
+                    if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
+                    else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
+                }
+                const char* wb = wslot0 + wslot * C::W_SLOT;
+                const int toff = ((tap / 3 - 1) * C::PW + (tap % 3 - 1)) * 16;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    bf16x8 av[2], bv[4];
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct)
+                        av[ct] = *reinterpret_cast<const bf16x8*>(wb + a_off + (2 * ks * C::MT + ct * 32) * 16);
+#pragma unroll
+                    for (int pt = 0; pt < 4; ++pt)
+                        bv[pt] = *reinterpret_cast<const bf16x8*>(ib + b_off[pt] + 2 * ks * C::NPP * 16 + toff);
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                        for (int pt = 0; pt < 4; ++pt)
+                            acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ct], bv[pt], acc[ct][pt], 0, 0, 0);
+                }
+                wslot = wslot + 1 == C::RW ? 0 : wslot + 1;
+            }
+            islot ^= 1;
+        }
+
+        // ------------------------------------------------------------------ epilogue
+        if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+            constexpr int PH = C::HW / 2;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+                for (int pp = 0; pp < (C::HW == 32 ? 2 : 4); ++pp) {
+                    // HW 32: windows of tiles (2pp, 2pp+1) [rows], lanes (r, r^1) [cols];
+                    // HW 16: tile pp holds rows 2y, 2y+1 in lane halves 0-15 / 16-31
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        float pv[4];
+                        uint32_t cw = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int g = 4 * g4 + e;
+                            const float bb = bias_s[wm * 64 + ct * 32 + 8 * g4 + 4 * h + e];
+                            float v0, v2;
+                            if (C::HW == 32) {
+                                v0 = acc[ct][2 * pp][g] + bb;
+                                v2 = acc[ct][2 * pp + 1][g] + bb;
+                            } else {
+                                v0 = acc[ct][pp][g] + bb;
+                                v2 = __shfl_xor(v0, 16, 64);
+                            }
+                            const float v1 = dpp_xor1(v0), v3 = dpp_xor1(v2);
+                            float best = v0 > 0.f ? v0 : 0.f;
+                            int idx = 0;
+                            const float r1 = v1 > 0.f ? v1 : 0.f, r2 = v2 > 0.f ? v2 : 0.f, r3 = v3 > 0.f ? v3 : 0.f;
+                            if (r1 > best) { best = r1; idx = 1; }
+                            if (r2 > best) { best = r2; idx = 2; }
+                            if (r3 > best) { best = r3; idx = 3; }
+                            pv[e] = best;
+                            cw |= (uint32_t)(best > 0.f ? idx : slk::CODE_NONE) << (8 * e);
+                        }
+                        const bool owner = C::HW == 32 ? (r & 1) == 0 : (r & 17) == 0;
+                        if (owner) {
+                            int y, x;
+                            if (C::HW == 32) {
+                                const int q = wn * 128 + 2 * pp * 32 + r;
+                                y = cur.rb * C::TR + q / 32;
+                                x = q % 32;
+                            } else {
+                                const int q = wn * 128 + pp * 32 + r;
+                                y = cur.rb * C::TR + q / 16;
+                                x = q % 16;
+                            }
+                            const int ch0 = cur.cob * C::MT + wm * 64 + ct * 32 + 8 * g4 + 4 * h;
+                            const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * PH + (y >> 1)) * PH + (x >> 1)) * 8 + (ch0 & 7);
+                            *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+                            *reinterpret_cast<uint32_t*>(out2 + o) = cw;
+                        }
+                    }
+                }
+            }
+        } else {
+            static_assert(C::MODE == wide::MODE_DGRAD_UNPOOL, "conv32: fwd-pool or dgrad-unpool");
+            const uint8_t* code = reinterpret_cast<const uint8_t*>(aux);
+            constexpr int FH = 2 * C::HW;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+                for (int pt = 0; pt < 4; ++pt) {
+                    const int q = wn * 128 + pt * 32 + r;
+                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const int ch0 = wm * 64 + ct * 32 + 8 * g4 + 4 * h;
+                        const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
+                        const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + ((plane * C::HW + y) * C::HW + x) * 8 + (ch0 & 7));
+#pragma unroll
+                        for (int pos = 0; pos < 4; ++pos) {
+                            float v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = ((cw >> (8 * e)) & 0xFF) == (uint32_t)pos ? acc[ct][pt][4 * g4 + e] : 0.f;
+                            const size_t o = ((plane * FH + 2 * y + (pos >> 1)) * FH + 2 * x + (pos & 1)) * 8 + (ch0 & 7);
+                            *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                        }
+                    }
+                }
+            }
+        }
+
+        if (tail) break;
+        cur = nxt;
+#pragma unroll
+        for (int d = 0; d < C::NDW; ++d) pcur[d] = pnxt[d];
+        tn += grid;
+        nxt = tile_state<C>(tn, B);
+        tile_poff<C>(nxt, wave, lane, pnxt);
+    }
+}
+
 #ifndef SLK_WIDE_FW
 #define SLK_WIDE_FW 4
 #endif
 #ifndef SLK_WIDE_NWV
 #define SLK_WIDE_NWV 4
 #endif
+#ifndef SLK_WIDE_K32
+#define SLK_WIDE_K32 1
+#endif
+// Per-layer kernel choice from tools/ablate_wide.py on MI355X (B = 4096): conv2 forward runs faster on
+// the 32x32x16 form (0.655 vs 0.693 ms), conv3 forward on the 16x16x32 form (0.585 vs 0.672), conv3
+// dgrad ties (0.667 / 0.672). SLK_WIDE_K32 = 0 / 2 forces all-16x16 / all-32x32 for A/B runs.
+#if SLK_WIDE_K32 == 2
+using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
+using CfgConv3Fwd = Conv32Cfg<128, 256, 16, wide::MODE_FWD_POOL>;
+using CfgConv3Dgrad = Conv32Cfg<256, 128, 16, wide::MODE_DGRAD_UNPOOL>;
+#elif SLK_WIDE_K32 == 1
+using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
+using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+#else
 using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
 using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
 using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+#endif
 using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4>;
 
 template <class C>
@@ -504,8 +750,12 @@ static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux,
 #else
     if (ntiles < grid) grid = C::NCB == 2 ? ((ntiles + 15) / 16) * 16 : ntiles;
 #endif
-    hipLaunchKernelGGL(wide_conv_kernel<C>, dim3((unsigned)grid), dim3(C::THREADS), 0, slk_stream(stream), in, wsh, aux,
-                       out, out2, B);
+    if constexpr (C::K32)
+        hipLaunchKernelGGL(wide_conv32_kernel<C>, dim3((unsigned)grid), dim3(256), 0, slk_stream(stream), in, wsh, aux,
+                           out, out2, B);
+    else
+        hipLaunchKernelGGL(wide_conv_kernel<C>, dim3((unsigned)grid), dim3(C::THREADS), 0, slk_stream(stream), in, wsh,
+                           aux, out, out2, B);
     return slk_launch_status();
 }
 
