@@ -175,16 +175,17 @@ int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2,
 int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const float* b3, uint16_t* cut, uint8_t* code3,
                        int B, void* stream);
 /* Server: dropout (hash of seed, *step, sample, feature; keep iff hash >= keep_threshold, kept values
- * scaled by keep_scale), fc forward, cross-entropy forward+backward (dlogits scaled by grad_scale) and
- * the cut gradient dcut = keep * keep_scale * dlogits @ Wf (bf16, C8). wf8 = slk_wide_fc_shadow(Wf).
- * Replaces server_part.py:48-51 + the cut-gradient return (:57) for the widened model. */
+ * scaled by keep_scale), fc forward, cross-entropy forward+backward (dlogits scaled by grad_scale), the
+ * cut gradient dcut = keep * keep_scale * dlogits @ Wf (bf16, C8) and the fc weight-gradient slabs
+ * [slk_wide_head_nslab(B)][163850] = [dWf (torch layout) | dbf]. wf8 = slk_wide_fc_shadow(Wf);
+ * work = slk_wide_head_work(B) floats of scratch. Replaces server_part.py:48-51 + the cut-gradient
+ * return (:57) for the widened model. */
 int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
                   unsigned seed, unsigned keep_threshold, float keep_scale, float grad_scale, float* logits,
-                  float* loss_i, float* dlogits, uint16_t* dcut, int* err_flag, int B, void* stream);
-/* fc weight-gradient slabs [slk_wide_fc_wgrad_nslab(B)][163850] = [dWf (torch layout) | dbf]. */
-int slk_wide_fc_wgrad(const uint16_t* cut, const float* dlogits, const int* step, unsigned seed,
-                      unsigned keep_threshold, float keep_scale, float* slabs, int B, void* stream);
-int slk_wide_fc_wgrad_nslab(int B);
+                  float* loss_i, float* dlogits, uint16_t* dcut, float* slabs, float* work, int* err_flag, int B,
+                  void* stream);
+int slk_wide_head_nslab(int B);
+int slk_wide_head_work(int B);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
  * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
  * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs

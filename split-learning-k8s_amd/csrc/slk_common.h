@@ -80,8 +80,16 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 #define SLK_LDS(ptr_expr) (ptr_expr)
 #endif
 
+// Butterfly sum over the 64 lanes: every lane ends with the total, bit-identically (each step adds
+// the same two partial sums, commutatively, in both partner lanes). Inside a 16-lane row by DPP
+// (quad_perm 1032 / 2301, row_half_mirror, row_mirror: no LDS traffic), then across rows by
+// ds_swizzle/bpermute.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }

@@ -16,7 +16,6 @@ namespace {
 constexpr int CUTF = 16384;       // features per sample
 constexpr int NCH = CUTF / 8;     // 2048 chunks of 8 channels (C8 order: chunk = plane*64 + pixel)
 constexpr int NC = 10;
-constexpr int HSB = 4;            // samples per head workgroup
 }  // namespace
 
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
@@ -55,155 +54,155 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
-// One 256-thread workgroup per HSB samples; thread t owns chunks t + 256 i (i < 8).
-__global__ __launch_bounds__(256) void wide_head_kernel(
-    const uint16_t* __restrict__ cut, const float* __restrict__ wf8, const float* __restrict__ bf,
-    const int64_t* __restrict__ labels, const int* __restrict__ step_ptr, uint32_t seed, uint32_t thresh,
-    float keep_scale, float grad_scale, float* __restrict__ logits, float* __restrict__ loss_i,
-    float* __restrict__ dlogits, uint16_t* __restrict__ dcut, int* __restrict__ err_flag, int B) {
-    __shared__ float red[4][HSB * NC];
-    __shared__ float dl_s[HSB * NC];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * HSB;
-    const int nb = min(HSB, B - b0);
-    const uint32_t step = (uint32_t)*step_ptr;
+// The head as three launches over a (feature slice x sample group) grid, so every fc weight is read
+// into registers once per workgroup and reused over 64 samples (the weight matrix is 655 KB: re-read
+// per handful of samples it, not the cut, was the traffic):
+//   head_logits : thread = one 8-feature chunk of a 2048-feature slice, weights in registers; per
+//                 sample: dropout, 80 FMAs, wave reduction -> partial logits [B][32][10] (workspace)
+//   head_ce     : thread = sample; fixed-order sum of the 32 partials + bias, cross-entropy fwd/bwd
+//   head_back   : same grid; per sample the cut gradient chunk (bf16) and the fc weight-gradient
+//                 accumulation (80 registers) -> one slab per sample group [dWf | dbf]
+constexpr int HSLICE = 8;            // 2048-feature slices (256 chunks each)
+constexpr int HSG = 64;              // samples per group
+constexpr int HPART = HSLICE * 4;    // partial logits per sample (slices x waves)
 
-    float acc[HSB][NC];
+__device__ __forceinline__ void load_w(const float* __restrict__ wf8, int fc, float (&w)[NC][8]) {
 #pragma unroll
-    for (int s = 0; s < HSB; ++s)
-#pragma unroll
-        for (int j = 0; j < NC; ++j) acc[s][j] = 0.f;
-#pragma unroll 1
-    for (int i = 0; i < 8; ++i) {
-        const int fc = tid + 256 * i;
-        float w[NC][8];
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const float4 lo = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8);
-            const float4 hi = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8 + 4);
-            w[j][0] = lo.x; w[j][1] = lo.y; w[j][2] = lo.z; w[j][3] = lo.w;
-            w[j][4] = hi.x; w[j][5] = hi.y; w[j][6] = hi.z; w[j][7] = hi.w;
-        }
-#pragma unroll
-        for (int s = 0; s < HSB; ++s) {
-            if (s >= nb) break;
-            const uint32_t kb = keep_bits((uint32_t)(b0 + s), fc, step, seed, thresh);
-            float v[8];
-            unpack8(*reinterpret_cast<const uint4*>(cut + ((size_t)(b0 + s) * NCH + fc) * 8), v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = (kb >> k) & 1 ? v[k] * keep_scale : 0.f;
-#pragma unroll
-            for (int j = 0; j < NC; ++j) {
-                float a = acc[s][j];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) a = __builtin_fmaf(v[k], w[j][k], a);
-                acc[s][j] = a;
-            }
-        }
+    for (int j = 0; j < NC; ++j) {
+        const float4 lo = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8);
+        const float4 hi = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8 + 4);
+        w[j][0] = lo.x; w[j][1] = lo.y; w[j][2] = lo.z; w[j][3] = lo.w;
+        w[j][4] = hi.x; w[j][5] = hi.y; w[j][6] = hi.z; w[j][7] = hi.w;
     }
+}
+
+// dropout applied to a loaded cut chunk v of sample b; returns the keep bits
+__device__ __forceinline__ uint32_t dropped(uint4 v, int b, int fc, uint32_t step, uint32_t seed, uint32_t thresh,
+                                            float keep_scale, float (&d)[8]) {
+    const uint32_t kb = keep_bits((uint32_t)b, fc, step, seed, thresh);
+    unpack8(v, d);
 #pragma unroll
-    for (int s = 0; s < HSB; ++s)
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const float t = wave_sum(acc[s][j]);
-            if (lane == 0) red[wave][s * NC + j] = t;
-        }
-    __syncthreads();
-    if (tid < nb) {
-        const int s = tid, b = b0 + s;
-        float z[NC], m = -__builtin_inff();
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            z[j] = (((red[0][s * NC + j] + red[1][s * NC + j]) + red[2][s * NC + j]) + red[3][s * NC + j]) + bf[j];
-            m = fmaxf(m, z[j]);
-        }
-        float se = 0.f;
-#pragma unroll
-        for (int j = 0; j < NC; ++j) se += expf(z[j] - m);
-        const float lse = m + logf(se);
-        const int64_t y = labels[b];
-        const bool ok = y >= 0 && y < NC;
-        if (!ok && err_flag) atomicOr(err_flag, 1);
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            logits[(size_t)b * NC + j] = z[j];
-            const float d = ok ? (expf(z[j] - lse) - (j == y ? 1.f : 0.f)) * grad_scale : __builtin_nanf("");
-            dlogits[(size_t)b * NC + j] = d;
-            dl_s[s * NC + j] = d;
-        }
-        loss_i[b] = ok ? lse - z[(int)y] : __builtin_nanf("");
-    }
-    __syncthreads();
-    // dcut = keep * scale * (dlogits @ Wf)   (bf16, C8)
+    for (int k = 0; k < 8; ++k) d[k] = (kb >> k) & 1 ? d[k] * keep_scale : 0.f;
+    return kb;
+}
+__device__ __forceinline__ uint4 cut_chunk(const uint16_t* __restrict__ cut, int b, int fc, int B) {
+    return b < B ? *reinterpret_cast<const uint4*>(cut + ((size_t)b * NCH + fc) * 8) : make_uint4(0, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
+                                                               const int* __restrict__ step_ptr, uint32_t seed,
+                                                               uint32_t thresh, float keep_scale,
+                                                               float* __restrict__ part, int B) {
+    const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int fc = slice * 256 + threadIdx.x;
+    const uint32_t step = (uint32_t)*step_ptr;
+    float w[NC][8];
+    load_w(wf8, fc, w);
+    const int b1 = min(B, (grp + 1) * HSG);
+    uint4 vn = cut_chunk(cut, grp * HSG, fc, b1);
 #pragma unroll 1
-    for (int i = 0; i < 8; ++i) {
-        const int fc = tid + 256 * i;
-        float w[NC][8];
+    for (int b = grp * HSG; b < b1; ++b) {
+        const uint4 v = vn;
+        vn = cut_chunk(cut, b + 1, fc, b1);      // next sample's chunk in flight during this one
+        float d[8];
+        dropped(v, b, fc, step, seed, thresh, keep_scale, d);
+        float pj[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            const float4 lo = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8);
-            const float4 hi = *reinterpret_cast<const float4*>(wf8 + (size_t)j * CUTF + fc * 8 + 4);
-            w[j][0] = lo.x; w[j][1] = lo.y; w[j][2] = lo.z; w[j][3] = lo.w;
-            w[j][4] = hi.x; w[j][5] = hi.y; w[j][6] = hi.z; w[j][7] = hi.w;
+            float a = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a = __builtin_fmaf(d[k], w[j][k], a);
+            pj[j] = wave_sum(a);
         }
+        if (lane < NC) {
+            float v = pj[0];
 #pragma unroll
-        for (int s = 0; s < HSB; ++s) {
-            if (s >= nb) break;
-            const uint32_t kb = keep_bits((uint32_t)(b0 + s), fc, step, seed, thresh);  // recomputed: no mask storage
-            float o[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                float a = 0.f;
-#pragma unroll
-                for (int j = 0; j < NC; ++j) a = __builtin_fmaf(dl_s[s * NC + j], w[j][k], a);
-                o[k] = (kb >> k) & 1 ? a * keep_scale : 0.f;
-            }
-            *reinterpret_cast<uint4*>(dcut + ((size_t)(b0 + s) * NCH + fc) * 8) =
-                make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+            for (int j = 1; j < NC; ++j) v = lane == j ? pj[j] : v;
+            part[((size_t)b * HPART + slice * 4 + wave) * NC + lane] = v;
         }
     }
 }
 
-// fc weight gradient: slab[slice] = [dWf (torch layout [10][16384]) | dbf]. Thread = chunk (8
-// features x 10 classes = 80 accumulators), workgroup = 256 chunks x one batch slice.
-constexpr int FCW_SLICES = 64;
-__global__ __launch_bounds__(256) void wide_fc_wgrad_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ dlogits,
-                                                            const int* __restrict__ step_ptr, uint32_t seed, uint32_t thresh,
-                                                            float keep_scale, float* __restrict__ slabs, int B) {
-    const int cb = blockIdx.x & 7, slice = blockIdx.x >> 3;
-    const int fc = cb * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void wide_head_ce_kernel(const float* __restrict__ part, const float* __restrict__ bf,
+                                                           const int64_t* __restrict__ labels, float grad_scale,
+                                                           float* __restrict__ logits, float* __restrict__ loss_i,
+                                                           float* __restrict__ dlogits, int* __restrict__ err_flag, int B) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    float z[NC], m = -__builtin_inff();
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        float v = 0.f;
+        for (int q = 0; q < HPART; ++q) v += part[((size_t)b * HPART + q) * NC + j];
+        z[j] = v + bf[j];
+        m = fmaxf(m, z[j]);
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) se += expf(z[j] - m);
+    const float lse = m + logf(se);
+    const int64_t y = labels[b];
+    const bool ok = y >= 0 && y < NC;
+    if (!ok && err_flag) atomicOr(err_flag, 1);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        logits[(size_t)b * NC + j] = z[j];
+        dlogits[(size_t)b * NC + j] = ok ? (expf(z[j] - lse) - (j == y ? 1.f : 0.f)) * grad_scale : __builtin_nanf("");
+    }
+    loss_i[b] = ok ? lse - z[(int)y] : __builtin_nanf("");
+}
+
+__global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
+                                                             const float* __restrict__ dlogits,
+                                                             const int* __restrict__ step_ptr, uint32_t seed,
+                                                             uint32_t thresh, float keep_scale,
+                                                             uint16_t* __restrict__ dcut, float* __restrict__ slabs, int B) {
+    const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
+    const int fc = slice * 256 + threadIdx.x;
     const uint32_t step = (uint32_t)*step_ptr;
-    const int per = (B + FCW_SLICES - 1) / FCW_SLICES;
-    const int s0 = slice * per, s1 = min(B, s0 + per);
-    float acc[NC][8];
+    float w[NC][8], acc[NC][8];
+    load_w(wf8, fc, w);
 #pragma unroll
     for (int j = 0; j < NC; ++j)
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
     float accb = 0.f;
+    const int b1 = min(B, (grp + 1) * HSG);
+    uint4 vn = cut_chunk(cut, grp * HSG, fc, b1);
 #pragma unroll 1
-    for (int b = s0; b < s1; ++b) {
-        const uint32_t kb = keep_bits((uint32_t)b, fc, step, seed, thresh);
-        float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(cut + ((size_t)b * NCH + fc) * 8), v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = (kb >> k) & 1 ? v[k] * keep_scale : 0.f;
+    for (int b = grp * HSG; b < b1; ++b) {
+        const uint4 v = vn;
+        vn = cut_chunk(cut, b + 1, fc, b1);
+        float d[8];
+        const uint32_t kb = dropped(v, b, fc, step, seed, thresh, keep_scale, d);
         const float* dl = dlogits + (size_t)b * NC;
+        float dlr[NC];
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const float d = dl[j];
+        for (int j = 0; j < NC; ++j) dlr[j] = dl[j];
+        float o[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) acc[j][k] = __builtin_fmaf(d, v[k], acc[j][k]);
+        for (int k = 0; k < 8; ++k) {
+            float a = 0.f;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) a = __builtin_fmaf(dlr[j], w[j][k], a);
+            o[k] = (kb >> k) & 1 ? a * keep_scale : 0.f;
         }
-        if (cb == 0 && threadIdx.x < NC) accb += dl[threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[j][k] = __builtin_fmaf(dlr[j], d[k], acc[j][k]);
+        if (slice == 0 && threadIdx.x < NC) accb += dl[threadIdx.x];
+        *reinterpret_cast<uint4*>(dcut + ((size_t)b * NCH + fc) * 8) =
+            make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
     }
-    float* slab = slabs + (size_t)slice * (NC * CUTF + NC);
+    float* slab = slabs + (size_t)grp * (NC * CUTF + NC);
     const int plane = fc >> 6, pix = fc & 63;
 #pragma unroll
     for (int j = 0; j < NC; ++j)
 #pragma unroll
         for (int k = 0; k < 8; ++k) slab[(size_t)j * CUTF + (plane * 8 + k) * 64 + pix] = acc[j][k];
-    if (cb == 0 && threadIdx.x < NC) slab[NC * CUTF + threadIdx.x] = accb;
+    if (slice == 0 && threadIdx.x < NC) slab[NC * CUTF + threadIdx.x] = accb;
 }
 
 // Fixed-order slab reduction + Adam (torch.optim.Adam, amsgrad=False, maximize=False, no weight
@@ -295,23 +294,22 @@ __global__ __launch_bounds__(256) void wide_fc_shadow_kernel(const float* __rest
 
 __global__ void tick_kernel(int* __restrict__ ctr) { *ctr += 1; }
 
+extern "C" int slk_wide_head_nslab(int B) { return B > 0 ? (B + HSG - 1) / HSG : 0; }
+extern "C" int slk_wide_head_work(int B) { return B > 0 ? B * HPART * NC : 0; }
 extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels,
                              const int* step, unsigned seed, unsigned keep_threshold, float keep_scale,
                              float grad_scale, float* logits, float* loss_i, float* dlogits, uint16_t* dcut,
-                             int* err_flag, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && dcut);
+                             float* slabs, float* work, int* err_flag, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && dcut && slabs && work);
     if (B == 0) return 0;
-    hipLaunchKernelGGL(wide_head_kernel, dim3((B + HSB - 1) / HSB), dim3(256), 0, slk_stream(stream), cut, wf8, bf,
-                       labels, step, seed, keep_threshold, keep_scale, grad_scale, logits, loss_i, dlogits, dcut,
-                       err_flag, B);
-    return slk_launch_status();
-}
-extern "C" int slk_wide_fc_wgrad_nslab(int B) { return B >= 0 ? FCW_SLICES : 0; }
-extern "C" int slk_wide_fc_wgrad(const uint16_t* cut, const float* dlogits, const int* step, unsigned seed,
-                                 unsigned keep_threshold, float keep_scale, float* slabs, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && cut && dlogits && step && slabs);
-    hipLaunchKernelGGL(wide_fc_wgrad_kernel, dim3(8 * FCW_SLICES), dim3(256), 0, slk_stream(stream), cut, dlogits,
-                       step, seed, keep_threshold, keep_scale, slabs, B);
+    const int ng = slk_wide_head_nslab(B);
+    hipStream_t st = slk_stream(stream);
+    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, step, seed,
+                       keep_threshold, keep_scale, work, B);
+    hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + 255) / 256), dim3(256), 0, st, work, bf, labels, grad_scale,
+                       logits, loss_i, dlogits, err_flag, B);
+    hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, dlogits, step, seed,
+                       keep_threshold, keep_scale, dcut, slabs, B);
     return slk_launch_status();
 }
 extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab,

@@ -315,13 +315,12 @@ class WideServerStage:
         dlogits = self._b("dlogits", (B, 10), _F32)
         dcut = dcut if dcut is not None else self._b("dcut", (B,) + CUT_SHAPE, _BF)
         _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
-        sf = self._b("sf", (_q("slk_wide_fc_wgrad_nslab", B), SERVER_NPARAM), _F32)
+        sf = self._b("sf", (_q("slk_wide_head_nslab", B), SERVER_NPARAM), _F32)
+        work = self._b("work", (_q("slk_wide_head_work", B),), _F32)
         _k("wide_head", cut.data_ptr(), self.wf8.data_ptr(), self.params[163840:].data_ptr(),
-                  labels.data_ptr(), self.step_ctr.data_ptr(), self.seed, KEEP_THRESHOLD, KEEP_SCALE,
-                  float(grad_scale), logits.data_ptr(), loss_i.data_ptr(), dlogits.data_ptr(), dcut.data_ptr(),
-                  self.err_flag.data_ptr(), B, s)
-        _k("wide_fc_wgrad", cut.data_ptr(), dlogits.data_ptr(), self.step_ctr.data_ptr(), self.seed,
-                  KEEP_THRESHOLD, KEEP_SCALE, sf.data_ptr(), B, s)
+           labels.data_ptr(), self.step_ctr.data_ptr(), self.seed, KEEP_THRESHOLD, KEEP_SCALE,
+           float(grad_scale), logits.data_ptr(), loss_i.data_ptr(), dlogits.data_ptr(), dcut.data_ptr(),
+           sf.data_ptr(), work.data_ptr(), self.err_flag.data_ptr(), B, s)
         self._logits, self._dlogits = logits, dlogits
         return dcut, loss_i, sf
 
