@@ -308,6 +308,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the multi-GPU path on a 1-GPU box: SLK_BENCH_BACKEND=gloo SLK_BENCH_ONE_GPU=1 puts
+    # every rank on cuda:0 over gloo (which moves CUDA tensors through the host). Never for numbers.
+    backend = os.environ.get("SLK_BENCH_BACKEND", "nccl")
+    if os.environ.get("SLK_BENCH_ONE_GPU"):
+        local = 0
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     out = {"metric": "training samples/sec (node) for split CNN", "value": None, "unit": "samples/s",
@@ -322,7 +327,10 @@ def main():
     import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
         run_distributed(args, out, rank, world, local)
     elif args.config == "k5":
         w = run_wide(args, args.k5_batch, args.steps, args.warmup, not args.no_kernel_pass)
