@@ -271,16 +271,17 @@ def run_distributed(args, out, rank, world, local):
                 data = SyntheticCIFAR(42 + rank)
                 xs, ys = zip(*(data.batch(Bk) for _ in range(2)))
                 WX, WY = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
-                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=wgrp)
+                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=wgrp, micro=args.micro)
                 wfn = lambda i: wt.client_step(WX[i % 2], WY[i % 2])  # noqa: E731
             else:
-                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=wgrp)
+                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=wgrp, micro=args.micro)
                 wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
             Kw = max(3, min(args.steps, 10))
             dtw = timed(wfn, Kw, 2, dev)
             Gw = (world - 1) * Bk
             out["widened_hub"] = {"workload": f"K5 SplitFed: {world - 1} client GPU(s) (widened conv stack, bf16) + "
-                                              "1 server GPU (dropout/fc/CE head), client all-reduce",
+                                              f"1 server GPU (dropout/fc/CE head), {args.micro} micro-batches, "
+                                              "client all-reduce",
                                   "samples_per_s": round(Kw * Gw / dtw, 1), "ms_per_step": round(dtw / Kw * 1e3, 3),
                                   "global_batch": Gw, "exchange_bytes_per_step": wt.exchange_bytes,
                                   "exchange_GBps_effective": round(wt.exchange_bytes / (dtw / Kw) / 1e9, 2)}

@@ -174,16 +174,17 @@ int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2,
 /* cut, code3 = pool(relu(conv3(p2) + b3)). The cut is what the client sends (client_part.py:117-125). */
 int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const float* b3, uint16_t* cut, uint8_t* code3,
                        int B, void* stream);
-/* Server: dropout (hash of seed, *step, sample, feature; keep iff hash >= keep_threshold, kept values
+/* Server: dropout (hash of seed, *step, b0 + sample, feature; keep iff hash >= keep_threshold, kept values
  * scaled by keep_scale), fc forward, cross-entropy forward+backward (dlogits scaled by grad_scale), the
  * cut gradient dcut = keep * keep_scale * dlogits @ Wf (bf16, C8) and the fc weight-gradient slabs
  * [slk_wide_head_nslab(B)][163850] = [dWf (torch layout) | dbf]. wf8 = slk_wide_fc_shadow(Wf);
- * work = slk_wide_head_work(B) floats of scratch. Replaces server_part.py:48-51 + the cut-gradient
- * return (:57) for the widened model. */
+ * work = slk_wide_head_work(B) floats of scratch; b0 = global index of sample 0 (micro-batches and
+ * SplitFed slices of one step draw the dropout mask of the concatenated batch). Replaces
+ * server_part.py:48-51 + the cut-gradient return (:57) for the widened model. */
 int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
                   unsigned seed, unsigned keep_threshold, float keep_scale, float grad_scale, float* logits,
-                  float* loss_i, float* dlogits, uint16_t* dcut, float* slabs, float* work, int* err_flag, int B,
-                  void* stream);
+                  float* loss_i, float* dlogits, uint16_t* dcut, float* slabs, float* work, int* err_flag, int b0,
+                  int B, void* stream);
 int slk_wide_head_nslab(int B);
 int slk_wide_head_work(int B);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the

@@ -48,16 +48,23 @@ class OracleWideClient:
     def cut_shape(B):
         return (B, 256, 8, 8)
 
-    def forward(self, x):
+    def forward(self, x, tag=""):
         P = _unflat(self.params, W.CLIENT_KEYS)
-        self._x = x.double().numpy()
-        cut, self._rec = W.client_forward(P, self._x, bf=False)
+        xs = x.double().numpy()
+        cut, rec = W.client_forward(P, xs, bf=False)
+        self._saved = getattr(self, "_saved", {})
+        self._saved[tag] = (xs, rec)
         return torch.from_numpy(cut).contiguous()
 
-    def backward_grads(self, dcut):
+    def backward_grads(self, dcut, tag="", accumulate=False):
         P = _unflat(self.params, W.CLIENT_KEYS)
-        g, _ = W.client_backward(P, self._x, self._rec, dcut.double().numpy(), bf=False)
-        self.grads.copy_(torch.from_numpy(np.concatenate([np.asarray(g[k]).reshape(-1) for k in W.CLIENT_KEYS])))
+        xs, rec = self._saved[tag]
+        g, _ = W.client_backward(P, xs, rec, dcut.double().numpy(), bf=False)
+        gt = torch.from_numpy(np.concatenate([np.asarray(g[k]).reshape(-1) for k in W.CLIENT_KEYS]))
+        if accumulate:
+            self.grads += gt
+        else:
+            self.grads.copy_(gt)
 
     def step_from_grads(self):
         self.params = torch.from_numpy(self.opt.step(self.params.numpy(), self.grads.numpy()))
@@ -72,6 +79,24 @@ class OracleWideServer:
         self.opt = _Adam(self.params.numel())
         self.seed = seed
         self.losses = []
+
+    def accumulate(self, cut, labels, grad_scale, b0, k, nparts, dcut=None):
+        P = _unflat(self.params, W.SERVER_KEYS)
+        n = cut.shape[0]
+        keep = W.dropout_keep(self.seed, self.opt.t, n, b0=b0)
+        s = W.server_step(P, cut.double().numpy(), labels.numpy(), keep, grad_scale_batch=1.0 / grad_scale, bf=False)
+        g = np.concatenate([s["grads"][key].reshape(-1) for key in W.SERVER_KEYS])
+        self._g = g if k == 0 else self._g + g
+        self._parts = ([] if k == 0 else self._parts) + [s["loss_i"].sum() * grad_scale]
+        out = torch.from_numpy(s["dcut"]).contiguous()
+        if dcut is not None:
+            dcut.copy_(out)
+            return dcut
+        return out
+
+    def finish_step(self, nparts, step=None):
+        self.params = torch.from_numpy(self.opt.step(self.params.numpy(), self._g))
+        self.losses.append((step, float(np.sum(self._parts))))
 
     def step_request(self, cuts, labels, step=None):
         P = _unflat(self.params, W.SERVER_KEYS)

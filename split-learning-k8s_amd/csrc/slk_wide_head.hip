@@ -92,7 +92,7 @@ __device__ __forceinline__ uint4 cut_chunk(const uint16_t* __restrict__ cut, int
 __global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
                                                                const int* __restrict__ step_ptr, uint32_t seed,
                                                                uint32_t thresh, float keep_scale,
-                                                               float* __restrict__ part, int B) {
+                                                               float* __restrict__ part, int b0, int B) {
     const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int fc = slice * 256 + threadIdx.x;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* _
         const uint4 v = vn;
         vn = cut_chunk(cut, b + 1, fc, b1);      // next sample's chunk in flight during this one
         float d[8];
-        dropped(v, b, fc, step, seed, thresh, keep_scale, d);
+        dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
         float pj[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
@@ -157,7 +157,8 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
                                                              const float* __restrict__ dlogits,
                                                              const int* __restrict__ step_ptr, uint32_t seed,
                                                              uint32_t thresh, float keep_scale,
-                                                             uint16_t* __restrict__ dcut, float* __restrict__ slabs, int B) {
+                                                             uint16_t* __restrict__ dcut, float* __restrict__ slabs, int b0,
+                                                             int B) {
     const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
     const int fc = slice * 256 + threadIdx.x;
     const uint32_t step = (uint32_t)*step_ptr;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
         const uint4 v = vn;
         vn = cut_chunk(cut, b + 1, fc, b1);
         float d[8];
-        const uint32_t kb = dropped(v, b, fc, step, seed, thresh, keep_scale, d);
+        const uint32_t kb = dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
         const float* dl = dlogits + (size_t)b * NC;
         float dlr[NC];
 #pragma unroll
@@ -299,17 +300,18 @@ extern "C" int slk_wide_head_work(int B) { return B > 0 ? B * HPART * NC : 0; }
 extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels,
                              const int* step, unsigned seed, unsigned keep_threshold, float keep_scale,
                              float grad_scale, float* logits, float* loss_i, float* dlogits, uint16_t* dcut,
-                             float* slabs, float* work, int* err_flag, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && dcut && slabs && work);
+                             float* slabs, float* work, int* err_flag, int b0, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && dcut &&
+                  slabs && work);
     if (B == 0) return 0;
     const int ng = slk_wide_head_nslab(B);
     hipStream_t st = slk_stream(stream);
     hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, step, seed,
-                       keep_threshold, keep_scale, work, B);
+                       keep_threshold, keep_scale, work, b0, B);
     hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + 255) / 256), dim3(256), 0, st, work, bf, labels, grad_scale,
                        logits, loss_i, dlogits, err_flag, B);
     hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, dlogits, step, seed,
-                       keep_threshold, keep_scale, dcut, slabs, B);
+                       keep_threshold, keep_scale, dcut, slabs, b0, B);
     return slk_launch_status();
 }
 extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab,

@@ -321,19 +321,22 @@ class UShaped:
 
 class WideHub:
     """SplitFed for the widened model (BASELINE config 5, splitcnn/wide.py): client ranks 0..N-2 run
-    the conv stack (99.9 % of the step's FLOPs), the server rank N-1 the dropout/fc head. Per step each
-    client sends its cut (bf16, 32 KB/sample) + labels, the server runs ONE head step on the
-    concatenated (N-1)*B batch (mean loss and dropout indices over the global batch), returns each
-    client its cut-gradient slice, and the clients all-reduce their weight gradient (370,816 f32)
-    before identical Adam steps: exactly the single-process widened step at batch (N-1)*B.
-    Stages: client.forward / backward_grads / step_from_grads / grads / cut_shape / cut_dtype;
-    server.step_request(cuts, labels) -> (dcut, loss_i)."""
+    the conv stack (99.9 % of the step's FLOPs), the server rank N-1 the dropout/fc head. Each client
+    cuts its batch into `micro` micro-batches: it sends micro-batch k's cut (bf16, 32 KB/sample) +
+    labels while computing k+1, the server runs the head on every (micro-batch, client) part as it
+    arrives — mean-loss scale and dropout indices of the concatenated (N-1)*B batch, fc gradient
+    accumulated — and returns that part's cut gradient, which the client back-propagates while later
+    parts are still in flight. Clients then all-reduce their weight gradient (370,816 f32) and take
+    identical Adam steps: exactly the single-process widened step at batch (N-1)*B.
+    Stages: client.forward(x, tag) / backward_grads(dcut, tag, accumulate) / step_from_grads / grads /
+    cut_shape / cut_dtype; server.accumulate(cut, labels, scale, b0, k, nparts, dcut) / finish_step."""
 
-    def __init__(self, stage, rank: int, world: int, client_group=None):
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1):
         self.stage, self.rank, self.world = stage, rank, world
         self.server_rank = world - 1
         self.nclients = world - 1
         self.client_group = client_group
+        self.micro = micro
         self.global_step = 0
         self._bufs = {}
         self.exchange_bytes = 0
@@ -347,37 +350,52 @@ class WideHub:
 
     def client_step(self, x, y):
         c = self.stage
-        B = x.shape[0]
-        cut = c.forward(x)
+        B, m = x.shape[0], self.micro
+        assert B % m == 0, "batch must be divisible by the micro-batch count"
+        b = B // m
         dcut = self._buf("dcut", c.cut_shape(B), c.cut_dtype, x.device)
-        w1 = dist.isend(cut, self.server_rank)
-        w2 = dist.isend(y, self.server_rank)
-        r = dist.irecv(dcut, self.server_rank)
-        r.wait()
-        c.backward_grads(dcut)
-        w1.wait()
-        w2.wait()
+        sends, recvs = [], []
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            cut = c.forward(x[sl], tag=k)
+            sends.append(dist.isend(cut, self.server_rank))
+            sends.append(dist.isend(y[sl], self.server_rank))
+        for k in range(m):
+            recvs.append(dist.irecv(dcut[k * b:(k + 1) * b], self.server_rank))
+        for k in range(m):
+            recvs[k].wait()
+            c.backward_grads(dcut[k * b:(k + 1) * b], tag=k, accumulate=k > 0)
+        for w in sends:
+            w.wait()
         if self.nclients > 1:
             dist.all_reduce(c.grads, group=self.client_group)
         c.step_from_grads()
-        self.exchange_bytes = 2 * cut.numel() * cut.element_size() + y.numel() * 8
+        self.exchange_bytes = 2 * dcut.numel() * dcut.element_size() + y.numel() * 8
         self.global_step += 1
 
     def server_step(self, B: int, device, cut_shape, cut_dtype):
         """B = per-client batch; cut_shape(n) / cut_dtype describe the client stage's cut tensor."""
         s = self.stage
-        G = self.nclients * B
+        m, nc = self.micro, self.nclients
+        b, G = B // m, nc * B
         cuts = self._buf("cuts", cut_shape(G), cut_dtype, device)
+        dcuts = self._buf("dcuts", cut_shape(G), cut_dtype, device)
         labels = self._buf("labels", (G,), torch.int64, device)
-        reqs = []
-        for c in range(self.nclients):
-            sl = slice(c * B, (c + 1) * B)
-            reqs.append(dist.irecv(cuts[sl], c))
-            reqs.append(dist.irecv(labels[sl], c))
-        for r in reqs:
-            r.wait()
-        dcut, _ = s.step_request(cuts, labels, step=self.global_step)
-        sends = [dist.isend(dcut[c * B:(c + 1) * B], c) for c in range(self.nclients)]
+        reqs = {}
+        for c in range(nc):
+            for k in range(m):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                reqs[c, k] = (dist.irecv(cuts[sl], c), dist.irecv(labels[sl], c))
+        sends, part = [], 0
+        for k in range(m):
+            for c in range(nc):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                for r in reqs[c, k]:
+                    r.wait()
+                s.accumulate(cuts[sl], labels[sl], 1.0 / G, c * B + k * b, part, m * nc, dcut=dcuts[sl])
+                sends.append(dist.isend(dcuts[sl], c))
+                part += 1
+        s.finish_step(m * nc, step=self.global_step)
         for w in sends:
             w.wait()
         self.exchange_bytes = 2 * cuts.numel() * cuts.element_size() + labels.numel() * 8

@@ -180,6 +180,7 @@ class WideClientStage:
         self.w3f = torch.empty(294912, dtype=_BF, device=self.device)
         self.w3d = torch.empty(294912, dtype=_BF, device=self.device)
         self._buf = _Buffers()
+        self._saved = {}
         self.refresh_shadows()
 
     def _b(self, name, shape, dtype):
@@ -196,28 +197,31 @@ class WideClientStage:
            self.w2f.data_ptr(), self.w2d.data_ptr(),
                   self.w3f.data_ptr(), self.w3d.data_ptr(), _stream(self.params))
 
-    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, tag="") -> torch.Tensor:
+        """cut = client forward of x; `tag` keeps separate saved tensors per micro-batch."""
         B = x.shape[0]
         _dev(x, "x", (B, 3, 32, 32))
         s = _stream(x)
-        a1 = self._b("a1", (B, 8, 32, 32, 8), _BF)
-        p2 = self._b("p2", (B, 16, 16, 16, 8), _BF)
-        code2 = self._b("code2", (B, 16, 16, 16, 8), _U8)
-        cut = out if out is not None else self._b("cut", (B,) + CUT_SHAPE, _BF)
+        a1 = self._b(f"a1{tag}", (B, 8, 32, 32, 8), _BF)
+        p2 = self._b(f"p2{tag}", (B, 16, 16, 16, 8), _BF)
+        code2 = self._b(f"code2{tag}", (B, 16, 16, 16, 8), _U8)
+        cut = out if out is not None else self._b(f"cut{tag}", (B,) + CUT_SHAPE, _BF)
         _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
-        code3 = self._b("code3", (B,) + CUT_SHAPE, _U8)
+        code3 = self._b(f"code3{tag}", (B,) + CUT_SHAPE, _U8)
         _k("wide_conv1_fwd", x.data_ptr(), self.w1b.data_ptr(), self._p("b1", 64).data_ptr(), a1.data_ptr(), B, s)
         _k("wide_conv2_fwd", a1.data_ptr(), self.w2f.data_ptr(), self._p("b2", 128).data_ptr(),
                   p2.data_ptr(), code2.data_ptr(), B, s)
         _k("wide_conv3_fwd", p2.data_ptr(), self.w3f.data_ptr(), self._p("b3", 256).data_ptr(),
                   cut.data_ptr(), code3.data_ptr(), B, s)
         self._x, self._a1, self._p2, self._code2, self._code3 = x, a1, p2, code2, code3
+        self._saved[tag] = (x, a1, p2, code2, code3)
         return cut
 
-    def backward_slabs(self, dcut: torch.Tensor):
+    def backward_slabs(self, dcut: torch.Tensor, tag=""):
         """Client backward into three slab sets (conv3, conv2, conv1); returns them."""
         B = dcut.shape[0]
         _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
+        self._x, self._a1, self._p2, self._code2, self._code3 = self._saved[tag]
         s = _stream(dcut)
         dc3 = self._b("dc3", (B, 32, 16, 16, 8), _BF)
         dc2 = self._b("dc2", (B, 16, 32, 32, 8), _BF)
@@ -261,13 +265,15 @@ class WideClientStage:
     def cut_shape(B: int):
         return (B,) + CUT_SHAPE
 
-    def backward_grads(self, dcut: torch.Tensor):
-        """activations.backward(grads) into the flat gradient block (fixed-order slab reduction)."""
-        s1, s2, s3 = self.backward_slabs(dcut)
+    def backward_grads(self, dcut: torch.Tensor, tag="", accumulate: bool = False):
+        """activations.backward(grads) into the flat gradient block (fixed-order slab reduction);
+        accumulate=True adds (micro-batches of one step)."""
+        s1, s2, s3 = self.backward_slabs(dcut, tag)
         st = _stream(dcut)
         for lo, n, sl in ((0, 1792, s1), (1792, 73856, s2), (75648, 295168, s3)):
             with TIMER("reduce_slabs"):
-                _lib.call("slk_reduce_slabs", sl.data_ptr(), sl.shape[0], n, self.grads[lo:].data_ptr(), 0, st)
+                _lib.call("slk_reduce_slabs", sl.data_ptr(), sl.shape[0], n, self.grads[lo:].data_ptr(),
+                          int(bool(accumulate)), st)
 
     def step_from_grads(self):
         """Adam from self.grads (e.g. after an all-reduce over the client ranks)."""
@@ -305,7 +311,7 @@ class WideServerStage:
     def refresh_shadows(self):
         _k("wide_fc_shadow", self.params.data_ptr(), self.wf8.data_ptr(), _stream(self.params))
 
-    def forward_backward(self, cut, labels, grad_scale, dcut=None):
+    def forward_backward(self, cut, labels, grad_scale, dcut=None, b0: int = 0):
         B = cut.shape[0]
         _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
         _dev(labels, "labels", (B,), torch.int64)
@@ -320,7 +326,7 @@ class WideServerStage:
         _k("wide_head", cut.data_ptr(), self.wf8.data_ptr(), self.params[163840:].data_ptr(),
            labels.data_ptr(), self.step_ctr.data_ptr(), self.seed, KEEP_THRESHOLD, KEEP_SCALE,
            float(grad_scale), logits.data_ptr(), loss_i.data_ptr(), dlogits.data_ptr(), dcut.data_ptr(),
-           sf.data_ptr(), work.data_ptr(), self.err_flag.data_ptr(), B, s)
+           sf.data_ptr(), work.data_ptr(), self.err_flag.data_ptr(), int(b0), B, s)
         self._logits, self._dlogits = logits, dlogits
         return dcut, loss_i, sf
 
@@ -352,6 +358,35 @@ class WideServerStage:
     def check_labels(self):
         if int(self.err_flag.item()) != 0:
             raise IndexError("splitcnn: a label was out of range [0, 10)")
+
+    # --- micro-batched / multi-client steps (dist.WideHub): accumulate, then one Adam step
+    def accumulate(self, cut, labels, grad_scale: float, b0: int, k: int, nparts: int, dcut=None):
+        """Head forward/backward for samples b0 .. b0+len(cut)-1 of the step's global batch (mean-loss
+        scale grad_scale = 1/global batch); the fc gradient adds into self.grads (k = 0 starts it) and
+        this part's loss sum lands in loss part k of nparts. Returns dcut."""
+        dcut, loss_i, sf = self.forward_backward(cut, labels, grad_scale, dcut=dcut, b0=b0)
+        s = _stream(sf)
+        with TIMER("reduce_slabs"):
+            _lib.call("slk_reduce_slabs", sf.data_ptr(), sf.shape[0], SERVER_NPARAM, self.grads.data_ptr(),
+                      int(k > 0), s)
+        parts = self._b("loss_parts", (nparts,), _F32)
+        _lib.call("slk_loss_sum", loss_i.data_ptr(), loss_i.numel(), float(grad_scale), parts[k:].data_ptr(), s)
+        return dcut
+
+    def finish_step(self, nparts: int, step=None):
+        """Adam from the accumulated gradient, loss logged (sum of the parts), step counter ticked."""
+        g = self.grads
+        s = _stream(g)
+        _k("adam_from_slabs", self.params.data_ptr(), None, self.m.data_ptr(), self.v.data_ptr(), g.data_ptr(), 1,
+           SERVER_NPARAM, float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+           self.step_ctr.data_ptr(), s)
+        self.refresh_shadows()
+        parts = self._b("loss_parts", (nparts,), _F32)
+        _k("loss_log", parts.data_ptr(), nparts, 1.0, self.loss_log.ring.data_ptr(), self.loss_log.ring.numel(),
+           self.loss_log.counter.data_ptr(), s)
+        if step is not None:
+            self.loss_log.note_step(step)
+        _k("tick", self.step_ctr.data_ptr(), s)
 
 
 class WideTrainer:

@@ -118,13 +118,13 @@ def _worker(rank, world, port, topo, outdir):
             batches = _wide_batches((world - 1) * WB)
             grp = sd.client_group_for(world)
             if rank < world - 1:
-                t = sd.WideHub(OracleWideClient(Pw), rank, world, client_group=grp)
+                t = sd.WideHub(OracleWideClient(Pw), rank, world, client_group=grp, micro=2)
                 for x, y in batches:
                     sl = slice(rank * WB, (rank + 1) * WB)
                     t.client_step(x[sl].contiguous(), y[sl].contiguous())
                 res = t.stage.named()
             else:
-                t = sd.WideHub(OracleWideServer(Pw), rank, world, client_group=grp)
+                t = sd.WideHub(OracleWideServer(Pw), rank, world, client_group=grp, micro=2)
                 for _ in batches:
                     t.server_step(WB, torch.device("cpu"), OracleWideClient.cut_shape, OracleWideClient.cut_dtype)
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}

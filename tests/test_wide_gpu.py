@@ -219,38 +219,52 @@ def test_wide_loss_curve_vs_oracle(gpu):
 
 
 def test_wide_hub_stage_interface_loopback(gpu):
-    """The stage methods dist.WideHub drives (forward / backward_grads / step_from_grads on clients,
-    step_request on the server at the concatenated batch), run in one process for 2 simulated clients
-    with the all-reduce done by hand, equal the fused single-GPU step at the concatenated batch:
-    loss and server weights bit-identical (same head launch), client gradient to 1e-6 (summation
-    order of two client slab sets vs one)."""
+    """The stage methods dist.WideHub drives — clients: forward(x, tag) / backward_grads(dcut, tag,
+    accumulate) / step_from_grads; server: accumulate(part) / finish_step — run in one process for 2
+    simulated clients x 2 micro-batches (server order: micro-batch outer, client inner; all-reduce by
+    hand) equal the fused single-GPU step at the concatenated batch: loss, server and client gradients
+    to 1e-6 (summation order), Adam on those gradients to the torch formula."""
     from splitcnn.wide import SyntheticCIFAR, WideClientStage, WideServerStage, WideTrainer, init_wide_models
-    B = 24
+    B, m = 24, 2
+    b = B // m
     x, y = SyntheticCIFAR(3).batch(2 * B)
     x, y = x.to(gpu), y.to(gpu)
     ref = WideTrainer(*init_wide_models(seed=0), device=gpu, graph=False)
     ref.step(x, y)
     clients = [WideClientStage(init_wide_models(seed=0)[0], device=gpu) for _ in range(2)]
     server = WideServerStage(init_wide_models(seed=0)[1], device=gpu)
-    cuts = torch.cat([clients[k].forward(x[k * B:(k + 1) * B].contiguous()).clone() for k in range(2)])
-    dcut, _ = server.step_request(cuts, y, step=0)
-    for k in range(2):
-        clients[k].backward_grads(dcut[k * B:(k + 1) * B].contiguous())
+    cuts = {}
+    for c in range(2):
+        for k in range(m):
+            cuts[c, k] = clients[c].forward(x[c * B + k * b:c * B + (k + 1) * b].contiguous(), tag=k).clone()
+    dcuts, part = {}, 0
+    for k in range(m):
+        for c in range(2):
+            sl = slice(c * B + k * b, c * B + (k + 1) * b)
+            dcuts[c, k] = server.accumulate(cuts[c, k], y[sl].contiguous(), 1.0 / (2 * B), c * B + k * b, part,
+                                            2 * m).clone()
+            part += 1
+    server_grads = server.grads.clone()
+    server.finish_step(2 * m, step=0)
+    for c in range(2):
+        for k in range(m):
+            clients[c].backward_grads(dcuts[c, k], tag=k, accumulate=k > 0)
     total = clients[0].grads + clients[1].grads
     for c in clients:
         c.grads.copy_(total)
         c.step_from_grads()
     torch.cuda.synchronize()
-    assert torch.equal(server.params, ref.server.params)
-    assert server.loss_log.flush()[0][1] == ref.loss_log.flush()[0][1]
+    assert abs(server.loss_log.flush()[0][1] - ref.loss_log.flush()[0][1]) <= 1e-6
+    grad_close(_np(server_grads), _np(ref.server.grads), rtol=1e-6)
     grad_close(_np(clients[0].grads), _np(ref.client.grads), rtol=1e-6)
     assert torch.equal(clients[0].params, clients[1].params)
     # Adam from the all-reduced gradient (nslab = 1 path) = the torch formula on that gradient. (Not
     # compared with ref's params: Adam's first step is ~lr*sign(g), so a 1e-7 summation-order
     # difference on a gradient that cancels to ~0 legitimately flips that weight's update.)
-    flat0 = np.concatenate([v.detach().double().numpy().ravel() for v in init_wide_models(seed=0)[0].state_dict().values()])
-    g = _np(clients[0].grads)
-    want, _, _ = W.adam(flat0, g, np.zeros_like(g), np.zeros_like(g), 1)
-    got = _np(clients[0].params)
-    tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
-    assert (np.abs(got - want) <= tol).all()
+    for stage, model, g in ((clients[0], init_wide_models(seed=0)[0], _np(clients[0].grads)),
+                            (server, init_wide_models(seed=0)[1], _np(server_grads))):
+        flat0 = np.concatenate([v.detach().double().numpy().ravel() for v in model.state_dict().values()])
+        want, _, _ = W.adam(flat0, g, np.zeros_like(g), np.zeros_like(g), 1)
+        got = _np(stage.params)
+        tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
+        assert (np.abs(got - want) <= tol).all()
