@@ -41,10 +41,23 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #define SLK_WIDE_PF 1
 #endif
 // Profiling-only ablation bits of the non-prefetch conv loop (tools/ablate_wide.py): 1 = no DMA in
-// the loop, 2 = no MFMA, 4 = no LDS fragment reads, 8 = no waits / barriers. Production = 0.
+// the loop, 2 = no MFMA, 4 = no LDS fragment reads, 8 = no waits / barriers, 16 = no weight DMA,
+// 32 = no input DMA, 64 = no epilogue. Production = 0.
 #ifndef SLK_WABL
 #define SLK_WABL 0
 #endif
+// Stagger: the second half of the grid (the second workgroup of each CU under round-robin dispatch)
+// sleeps SLK_WIDE_STAGGER x 127 x 64 cycles before its first tile, so the two co-resident workgroups
+// run half a tile apart and one's epilogue (VALU + stores) overlaps the other's MFMA main loop.
+#ifndef SLK_WIDE_STAGGER
+#define SLK_WIDE_STAGGER 0
+#endif
+__device__ __forceinline__ void wide_stagger() {
+#if SLK_WIDE_STAGGER
+    if (blockIdx.x >= gridDim.x / 2)
+        for (int i = 0; i < SLK_WIDE_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+}
 #ifndef SLK_WIDE_L
 #define SLK_WIDE_L (SLK_WIDE_PF ? 3 : 2)
 #endif
@@ -209,6 +222,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     int t = blockIdx.x;
     TileState cur = tile_state<C>(t, B);
     if (!cur.valid) return;
+    wide_stagger();
     int tn = t + grid;
     TileState nxt = tile_state<C>(tn, B);
     int pcur[C::NDW], pnxt[C::NDW];
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
             for (int tap = 0; tap < 9; ++tap) {
                 // this step's weight slice (and, at tap 0, this group's input tile) has landed
                 if (!(SLK_WABL & 8)) {
-                    if (tail || (SLK_WABL & 1)) wait_vmcnt<0>();
+                    if (tail || (SLK_WABL & 49)) wait_vmcnt<0>();
                     else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
                     else wait_vmcnt<(C::L - 1) * C::NW>();
                     __builtin_amdgcn_s_barrier();
@@ -346,14 +360,14 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 asm volatile("" ::: "memory");
                 // lookahead: weight step +L (ring slot of step -1, free since the barrier), then at
                 // tap 0 the next group's input tile (slot of group -1)
-                if (!(SLK_WABL & 1)) {
+                if (!(SLK_WABL & 17)) {
                     const int sl = g * 9 + tap + C::L;
                     int ws = wslot + C::L;
                     ws = ws >= C::RW ? ws - C::RW : ws;
                     if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
                     else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
                 }
-                if (tap == 0 && !(SLK_WABL & 1)) {
+                if (tap == 0 && !(SLK_WABL & 33)) {
                     char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
                     if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
                     else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
@@ -392,7 +406,12 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
 #endif
         // ------------------------------------------------------------------ epilogue
         const int ch_base = cur.cob * C::MT + wm * 64 + 4 * (lane >> 4);
-        if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+        if (SLK_WABL & 64) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int f = 0; f < C::FW; ++f) slk_keep(acc[i][f]);
+        } else if constexpr (C::MODE == wide::MODE_FWD_POOL) {
             constexpr int PH = C::HW / 2;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -536,6 +555,7 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
     int t = blockIdx.x;
     TileState cur = tile_state<C>(t, B);
     if (!cur.valid) return;
+    wide_stagger();
     int tn = t + grid;
     TileState nxt = tile_state<C>(tn, B);
     int pcur[C::NDW], pnxt[C::NDW];
