@@ -86,6 +86,17 @@ __device__ __forceinline__ float dpp_xor1(float v) {
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// vmcnt is 6 bits: an allowance above 63 saturates (waiting for more than needed is always safe)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_sat() { wait_vmcnt<(N > 63 ? 63 : N)>(); }
+
+// Epilogue-aware waits: the first steps of a tile wait for weight slices that were issued BEFORE the
+// previous tile's epilogue, so that epilogue's stores (and this tile's prefetched epilogue loads) are
+// younger and may stay in flight. Without the allowance those steps drain every store before the
+// next MFMA. 0 = plain counts (profiling only).
+#ifndef SLK_WIDE_EPI
+#define SLK_WIDE_EPI 1
+#endif
 
 // ----------------------------------------------------------------------------- conv geometry
 template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_>
@@ -115,6 +126,10 @@ struct ConvCfg {
     static constexpr int RB = HW / TR;                      // row blocks per image
     static constexpr int NCB = CO / MT;                     // output-channel blocks
     static constexpr int FPR = HW / 16;                     // 16-pixel fragments per image row
+    // VMEM instructions per lane in the epilogue: stores (pooled value + code, 4 unpooled positions,
+    // masked value) and the code2 / a1 words loaded at tile start. Must never over-count.
+    static constexpr int EPI_ST = MODE == 1 ? 16 * FW : 4 * FW;
+    static constexpr int EPI_LD = MODE == 0 ? 0 : 4 * FW;
     static_assert(MT == 128 || MT == 64, "MT");
     static_assert(HW % TR == 0 && TR % 2 == 0 && (16 * FW) % (2 * HW) == 0, "tile rows / pool pairs per wave");
     static_assert(NW >= 1 && W_SLOT % (1024 * NWV) == 0, "weight slot must split over the waves");
@@ -200,6 +215,30 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
     }
 }
 
+// Epilogue operands of a tile (dgrad-unpool: code2 words, dgrad-mask: a1 words), loaded when the tile
+// starts so their latency hides under its main loop instead of draining the DMA queue at the epilogue.
+template <class C>
+__device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const TileState& s, int wm, int wn,
+                                             int lane, uint32_t (&ecw)[4][C::FW], uint2 (&em)[4][C::FW]) {
+    if constexpr (C::MODE != wide::MODE_FWD_POOL) {
+        const int ch_base = s.cob * C::MT + wm * 64 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ch0 = ch_base + i * 16;
+#pragma unroll
+            for (int f = 0; f < C::FW; ++f) {
+                const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
+                const int y = s.rb * C::TR + q / C::HW, x = q % C::HW;
+                const size_t o = (((size_t)(s.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
+                if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL)
+                    ecw[i][f] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(aux) + o);
+                else
+                    em[i][f] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + o);
+            }
+        }
+    }
+}
+
 // aux: forward = bias (f32 [CO]); dgrad-unpool = code2 (u8, C8 [B][CO/8][HW][HW][8]);
 //      dgrad-mask = a1 (bf16, C8 [B][CO/8][HW][HW][8]).
 // out: forward = pooled bf16 C8 [B][CO/8][HW/2][HW/2][8] (+ code u8 same layout in out2);
@@ -271,9 +310,13 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     }
     int wslot = 0;   // ring slot of the current step
     int islot = 0;   // input slot of the current group
+    bool post = false;   // a previous tile's epilogue stores may be in flight
+    uint32_t ecw[4][C::FW];
+    uint2 em[4][C::FW];
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
+        epi_prefetch<C>(aux, cur, wm, wn, lane, ecw, em);
         f32x4 acc[4][C::FW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -287,6 +330,16 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 const bool last = tail && g == C::G - 1 && tap == 8;
                 // step s+1's weight slice (and at tap 8 the next group's input tile) has landed
                 if (tail) wait_vmcnt<0>();
+                else if (SLK_WIDE_EPI && tap < 2 && g == 0) {
+                    // weight step +1 predates the previous epilogue and this tile's epilogue loads
+                    if (tap == 0) {
+                        if (post) wait_vmcnt_sat<C::NW + C::EPI_ST + C::EPI_LD>();
+                        else wait_vmcnt_sat<C::NW + C::EPI_LD>();
+                    } else {
+                        if (post) wait_vmcnt_sat<C::NW + C::NDW + C::EPI_ST + C::EPI_LD>();
+                        else wait_vmcnt_sat<C::NW + C::NDW + C::EPI_LD>();
+                    }
+                }
                 else if (tap == 1 || tap == 2) wait_vmcnt<C::NW + C::NDW>();
                 else wait_vmcnt<C::NW>();
                 __builtin_amdgcn_s_barrier();
@@ -336,9 +389,13 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
 
     int wslot = 0;   // ring slot of the current step
     int islot = 0;   // input slot of the current group
+    bool post = false;   // a previous tile's epilogue stores may be in flight
+    uint32_t ecw[4][C::FW];
+    uint2 em[4][C::FW];
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
+        epi_prefetch<C>(aux, cur, wm, wn, lane, ecw, em);
         f32x4 acc[4][C::FW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -353,6 +410,16 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 // this step's weight slice (and, at tap 0, this group's input tile) has landed
                 if (!(SLK_WABL & 8)) {
                     if (tail || (SLK_WABL & 49)) wait_vmcnt<0>();
+                    else if (SLK_WIDE_EPI && tap < C::L && g == 0) {
+                        // this step's weights predate the previous epilogue and this tile's loads
+                        if (tap == 0) {
+                            if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_ST + C::EPI_LD>();
+                            else wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_LD>();
+                        } else {
+                            if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_ST + C::EPI_LD>();
+                            else wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_LD>();
+                        }
+                    }
                     else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
                     else wait_vmcnt<(C::L - 1) * C::NW>();
                     __builtin_amdgcn_s_barrier();
@@ -457,7 +524,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
-                    const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + ((plane * C::HW + y) * C::HW + x) * 8 + (ch0 & 7));
+                    const uint32_t cw = ecw[i][f];
 #pragma unroll
                     for (int pos = 0; pos < 4; ++pos) {
                         float v[4];
@@ -478,7 +545,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
-                    const uint2 m = *reinterpret_cast<const uint2*>(a1 + o);
+                    const uint2 m = em[i][f];
                     // a1 > 0 (bf16): sign bit clear and not +0
                     const float v0 = (int)(m.x << 16) > 0 ? acc[i][f][0] : 0.f;
                     const float v1 = (int)(m.x & 0xFFFF0000u) > 0 ? acc[i][f][1] : 0.f;
@@ -533,6 +600,8 @@ struct Conv32Cfg {
     static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
     static constexpr int RB = HW / TR;
     static constexpr int NCB = CO / MT;
+    static constexpr int EPI_ST = MODE == 0 ? (HW == 32 ? 32 : 64) : 128;
+    static constexpr int EPI_LD = MODE == 0 ? 0 : 32;
     static_assert(HW % TR == 0 && TR % 2 == 0 && (HW == 32 || HW == 16), "tile rows");
     static_assert(NCB == 1 || NCB == 2, "NCB");
 };
@@ -582,6 +651,7 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
     for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
 
     int wslot = 0, islot = 0;
+    bool post = false;
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
@@ -598,6 +668,15 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 if (tail) wait_vmcnt<0>();
+                else if (SLK_WIDE_EPI && tap < C::L && g == 0) {
+                    if (tap == 0) {
+                        if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_ST + C::EPI_LD>();
+                        else wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_LD>();
+                    } else {
+                        if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_ST + C::EPI_LD>();
+                        else wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_LD>();
+                    }
+                }
                 else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
                 else wait_vmcnt<(C::L - 1) * C::NW>();
                 __builtin_amdgcn_s_barrier();
