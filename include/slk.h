@@ -71,10 +71,15 @@ int slk_conv1_wgrad_remask(const float* x, const float* W1, const float* b1, con
 
 /* ---------------------------------------------------------------- server stage (ModelPartB) */
 
-/* pooled = maxpool2(relu(conv2d(act, W2, b2))) and its argmax code, fused (MFMA f32 implicit GEMM).
- * Replaces ModelPartB.forward lines src/model_def.py:25-27 as called at src/server_part.py:48. */
+/* pooled = maxpool2(relu(conv2d(act, W2, b2))) and its argmax code, fused (Winograd F(2x2,3x3) on
+ * the f32 MFMA: one transformed 2x2 output tile = one pool window). Replaces ModelPartB.forward lines
+ * src/model_def.py:25-27 as called at src/server_part.py:48. */
 int slk_conv2_fwd_pool(const float* act, const float* W2, const float* b2, float* pooled,
                        uint8_t* code, int B, void* stream);
+/* The same op as a direct implicit GEMM (f32 MFMA, k-ordered fma chains); kept as the A/B and
+ * cross-check path. */
+int slk_conv2_fwd_pool_direct(const float* act, const float* W2, const float* b2, float* pooled,
+                              uint8_t* code, int B, void* stream);
 
 /* logits = pooled @ W3^T + b3.  Replaces model_def.py:28 (fc1). */
 int slk_fc_fwd(const float* pooled, const float* W3, const float* b3, float* logits, int B,

@@ -704,7 +704,7 @@ extern "C" int slk_fc_wgrad_nslab(int B) {
 }
 
 // ============================================================================ C ABI
-extern "C" int slk_conv2_fwd_pool(const float* act, const float* W2, const float* b2, float* pooled,
+extern "C" int slk_conv2_fwd_pool_direct(const float* act, const float* W2, const float* b2, float* pooled,
                                   uint8_t* code, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;

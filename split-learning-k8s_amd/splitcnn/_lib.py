@@ -29,6 +29,7 @@ _SIGS = {
     "slk_conv1_wgrad_nslab": [_I],
     "slk_conv1_wgrad_remask": [_P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_fwd_pool": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_fwd_pool_direct": [_P, _P, _P, _P, _P, _I, _P],
     "slk_fc_fwd": [_P, _P, _P, _P, _I, _P],
     "slk_xent_fwd_bwd": [_P, _P, _P, _P, _F, _P, _I, _P],
     "slk_fc_dgrad": [_P, _P, _P, _I, _P],

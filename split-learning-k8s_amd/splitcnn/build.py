@@ -16,7 +16,7 @@ CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include")
 LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
 SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip", "slk_wide.hip",
-           "slk_wide_head.hip"]
+           "slk_wide_head.hip", "slk_wino.hip"]
 ARCH = "gfx950"
 
 

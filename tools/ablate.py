@@ -59,6 +59,15 @@ def calls(L):
             "conv2_dgrad_fc": lambda: L.slk_conv2_dgrad_fc(p(dl), p(W3), p(code), p(W2), p(gcut), B, P(s)),
             "conv2_wgrad_fc": lambda: L.slk_conv2_wgrad_fc(p(act), p(dl), p(W3), p(code), p(slabs), B, P(s)),
         }
+    for n in ("slk_conv2_fwd_pool_direct", "slk_conv2_dgrad_direct", "slk_conv2_wgrad_direct"):
+        if hasattr(L, n):
+            getattr(L, n).restype = ctypes.c_int
+    if hasattr(L, "slk_conv2_fwd_pool_direct"):
+        extra["conv2_fwd_pool_direct"] = lambda: L.slk_conv2_fwd_pool_direct(p(act), p(W2), p(b2), p(pooled), p(code), B, P(s))
+    if hasattr(L, "slk_conv2_dgrad_direct"):
+        extra["conv2_dgrad_direct"] = lambda: L.slk_conv2_dgrad_direct(p(dp), p(code), p(W2), p(gcut), B, P(s))
+    if hasattr(L, "slk_conv2_wgrad_direct"):
+        extra["conv2_wgrad_direct"] = lambda: L.slk_conv2_wgrad_direct(p(act), p(dp), p(code), p(slabs), B, P(s))
     return {**extra,
         "conv2_fwd_pool": lambda: L.slk_conv2_fwd_pool(p(act), p(W2), p(b2), p(pooled), p(code), B, P(s)),
         "fc_xent": lambda: L.slk_fc_xent(p(pooled), p(W3), p(b3), p(y), p(logits), p(loss_i), p(dl), p(dp2),
