@@ -110,9 +110,13 @@ int slk_fc_wgrad_nslab(int B);
 
 /* Cut-layer gradient: cut_grad = conv2 input gradient of maxpool/relu-masked dpooled
  * (uses `code` from slk_conv2_fwd_pool). This is `client_activations.grad` of
- * src/server_part.py:45,51,57. MFMA f32 implicit GEMM. */
+ * src/server_part.py:45,51,57. Winograd F(2x2,3x3) on the f32 MFMA; the routed conv2 output
+ * gradient is expanded per transform tile in registers (never materialised). */
 int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const float* W2, float* cut_grad,
                     int B, void* stream);
+/* The same op as a direct implicit GEMM (A/B and cross-check path). */
+int slk_conv2_dgrad_direct(const float* dpooled, const uint8_t* code, const float* W2, float* cut_grad,
+                           int B, void* stream);
 
 /* conv2 weight/bias gradient partials: slabs [slk_conv2_wgrad_nslab(B)][18496] laid out as
  * [dW2 (64*288) | db2 (64)], i.e. the head of the server flat block. MFMA f32. */

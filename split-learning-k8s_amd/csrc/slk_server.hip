@@ -714,7 +714,7 @@ extern "C" int slk_conv2_fwd_pool_direct(const float* act, const float* W2, cons
     return slk_launch_status();
 }
 
-extern "C" int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const float* W2,
+extern "C" int slk_conv2_dgrad_direct(const float* dpooled, const uint8_t* code, const float* W2,
                                float* cut_grad, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;

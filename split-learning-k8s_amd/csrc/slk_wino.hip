@@ -158,21 +158,23 @@ __device__ __forceinline__ void lds_barrier() {
 
 // ============================================================================ forward + pool
 // M[ij][co][tile] = sum_ci U[ij][co][ci] * V[ij][ci][tile] : 16 GEMMs of 64 x 144 x 32 per sample.
-// Persistent, one 8-wave workgroup per CU (two waves per SIMD). Wave w owns output channels
-// 16*(w&3) .. +15 and input-channel half kh = w>>2 (ci 16kh .. 16kh+15), and keeps their transformed
-// filters in registers for the whole launch: A operand of v_mfma_f32_16x16x4_f32, lane l holds
-// U[ij][16(w&3) + (l&15)][16kh + 4s + (l>>4)] for k step s = 0..3 (64 VGPRs).
+// On gfx950 the f32 MFMA and the VALU do not execute concurrently (tools/ubench/coexec.hip: every
+// packed add issued between MFMAs adds ~4-5 cycles, from one wave per SIMD or two), so the design
+// minimises VALU instructions per MFMA rather than relying on overlap:
+// Persistent, one 4-wave workgroup per CU (one wave per SIMD, 512 registers each). Wave w owns output
+// channels 16w .. 16w+15 over the FULL reduction (32 input channels): their transformed filters stay
+// in registers for the whole launch (A operand of v_mfma_f32_16x16x4_f32: lane l holds
+// U[ij][16w + (l&15)][4s + (l>>4)] for k step s = 0..7, 128 VGPRs), so no partial sums cross waves and
+// there is no barrier inside a band.
 // Work unit = (sample, band of 4 tile rows = 48 tiles = 3 groups of 16): input rows 8*band ..
-// 8*band+9 of all 32 channels (33,280 B) double-buffered in LDS by 16-byte LDS-DMA.
-// Per group and k step a lane (ci, tile = l&15) reads its 4x4 input patch from LDS (8 ds_read_b64),
-// transforms it in registers (B operand of 16 MFMAs, one per (i,j)); the 16 accumulators of a
-// (co, tile) pair sit in one lane and register slot, so the output transform is in-register.
-// K halves: both waves of a pair apply the (linear) output transform to their partial sums; one parks
-// its 2x2 partials in LDS, the other adds them (always y_kh0 + y_kh1), then bias, ReLU, the 2x2 max-pool
-// (first max wins) and the routing code, and stores. The finishing role alternates per group; the
-// two waves of a pair share a SIMD (waves w, w+4), so the parking wave's MFMAs for the next group run
-// under its partner's epilogue.
-constexpr int WF_WAVES = 8;
+// 8*band+9 of all 32 channels (33,280 B) double-buffered in LDS by 16-byte LDS-DMA (inline asm, so the
+// next band stays in flight under the current band's MFMAs; one counted vmcnt + barrier per band).
+// Per group and k step a lane (ci = 4s + (l>>4), tile = l&15) reads its 4x4 input patch (8
+// ds_read_b64), transforms it with 8 packed adds (B operand of 16 MFMAs, one per (i,j)); the 16
+// accumulators of a (co, tile) pair sit in one lane and register slot, so the output transform (two
+// channels per packed op), bias, ReLU, the 2x2 max-pool (first max wins) and the routing code are
+// in-register and pooled/code leave by buffer stores.
+constexpr int WF_WAVES = 4;
 constexpr int WF_THREADS = WF_WAVES * 64;
 constexpr int WF_ROWS = 10;                    // input rows per band
 constexpr int WF_CSTR = WF_ROWS * A_HW;        // 260 floats per channel in LDS (contiguous)
@@ -180,7 +182,6 @@ constexpr int WF_BUF = C1 * WF_CSTR;           // 8320 floats = 33,280 B
 constexpr int WF_PIECES = WF_BUF / 4;          // 2080 sixteen-byte pieces
 constexpr int WF_CHUNKS = (WF_PIECES + 63) / 64;
 constexpr int WF_BSTR = WF_CHUNKS * 256;       // buffer stride: the last chunk writes a full KiB
-constexpr int WF_XCH = 4 * 16 * 64;            // parked partials per parity: [co block][r*4+q][lane]
 constexpr int WF_GRID = 256;                   // one workgroup per CU
 
 __device__ __forceinline__ void wf_dma_band(const float* __restrict__ act, int u, const float* dst, int wave, int lane) {
@@ -199,25 +200,23 @@ __device__ __forceinline__ void wf_dma_band(const float* __restrict__ act, int u
 __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
     const float* __restrict__ act, const float* __restrict__ W2, const float* __restrict__ b2,
     float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * WF_BSTR + 2 * WF_XCH + C2];
-    float* xch = smem + 2 * WF_BSTR;
-    float* bias_s = xch + 2 * WF_XCH;
+    __shared__ __attribute__((aligned(16))) float smem[2 * WF_BSTR + C2];
+    float* bias_s = smem + 2 * WF_BSTR;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int cb = wave & 3, kh = wave >> 2;
     const int nunit = 3 * B;
 
     int u = blockIdx.x;
     if (u < nunit) wf_dma_band(act, u, smem, wave, lane);
 
     // transformed filters of this lane's (co, ci) pairs
-    float uw[4][16];
+    float uw[8][16];
     {
-        const int co = 16 * cb + li;
+        const int co = 16 * wave + li;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const float* gp = W2 + (size_t)co * K2 + (16 * kh + 4 * s + lk) * 9;
+        for (int s = 0; s < 8; ++s) {
+            const float* gp = W2 + (size_t)co * K2 + (4 * s + lk) * 9;
             float g[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) g[k] = gp[k];
@@ -230,13 +229,14 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
     int buf = 0;
 #pragma unroll 1
     for (; u < nunit; u += gridDim.x) {
-        // this unit's band has landed: its DMA was issued before the previous unit's epilogue
-        // stores (>= 8 per wave) — and every wave is done reading the other buffer
-        wg_wait_vmcnt<8>();
+        // this unit's band has landed: its DMA was issued before the previous unit's 24 epilogue
+        // stores of this wave — and every wave is done reading the other buffer
+        wg_wait_vmcnt<16>();
         lds_barrier();
         const int nu = u + gridDim.x;
         if (nu < nunit) wf_dma_band(act, nu, smem + (buf ^ 1) * WF_BSTR, wave, lane);
         const float* img = smem + buf * WF_BSTR;
+        const float4 bv = reinterpret_cast<const float4*>(bias_s)[4 * wave + lk];
         const int b = u / 3, band = u - 3 * (u / 3);
         const auto prs = __builtin_amdgcn_make_buffer_rsrc(pooled + (size_t)b * P_SAMPLE, 0, P_SAMPLE * 4, 0x00020000);
         const auto crs = __builtin_amdgcn_make_buffer_rsrc(code + (size_t)b * P_SAMPLE, 0, P_SAMPLE, 0x00020000);
@@ -244,25 +244,36 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
         for (int g = 0; g < 3; ++g) {
             const int t = 48 * band + 16 * g + li;       // tile = pooling window index
             const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
-            const float* pp = img + (16 * kh + lk) * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
+            const float* pp = img + lk * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
             f32x4 acc[16];
 #pragma unroll
             for (int ij = 0; ij < 16; ++ij) acc[ij] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f2 Rlo[4], Rhi[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const float* ps = pp + 4 * s * WF_CSTR;
-                f2 Rlo[4], Rhi[4], v01[4], v23[4];
+            for (int r = 0; r < 4; ++r) {
+                Rlo[r] = *reinterpret_cast<const f2*>(pp + r * A_HW);
+                Rhi[r] = *reinterpret_cast<const f2*>(pp + r * A_HW + 2);
+            }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    Rlo[r] = *reinterpret_cast<const f2*>(ps + r * A_HW);
-                    Rhi[r] = *reinterpret_cast<const f2*>(ps + r * A_HW + 2);
-                }
+            for (int s = 0; s < 8; ++s) {
+                f2 v01[4], v23[4];
                 if (SLK_WINO_ABL & 1) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) { v01[r] = Rlo[r]; v23[r] = Rhi[r]; }
                 } else {
                     pk_wino_in(Rlo, Rhi, v01, v23);
                 }
+                if (s < 7) {  // next step's patch: in flight under this step's 16 MFMAs
+                    const float* ps = pp + 4 * (s + 1) * WF_CSTR;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        Rlo[r] = *reinterpret_cast<const f2*>(ps + r * A_HW);
+                        Rhi[r] = *reinterpret_cast<const f2*>(ps + r * A_HW + 2);
+                    }
+                }
+                // pin the order (hipcc otherwise sinks the prefetch next to its use and exposes the
+                // LDS latency twice per step at one wave per SIMD)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     acc[4 * i + 0] = mfma16x16x4(uw[s][4 * i + 0], v01[i].x, acc[4 * i + 0]);
@@ -270,51 +281,38 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
                     acc[4 * i + 2] = mfma16x16x4(uw[s][4 * i + 2], v23[i].x, acc[4 * i + 2]);
                     acc[4 * i + 3] = mfma16x16x4(uw[s][4 * i + 3], v23[i].y, acc[4 * i + 3]);
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
-            // partial output transform, two rows (co = 16cb + 4lk + r, r = 2h, 2h+1) per packed op;
-            // column = tile t
-            f2 y[2][4];
+            // output transform, two rows (co = 16w + 4lk + r, r = 2h, 2h+1) per packed op; + bias
+            f2 z[2][4];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 f2 m[16];
 #pragma unroll
                 for (int ij = 0; ij < 16; ++ij) m[ij] = h ? acc[ij].zw : acc[ij].xy;
-                pk_wino_out(m, y[h]);
-            }
-            // parked partials: [q][lane][r] (16 B per lane and q: ds_write_b128 / ds_read_b128)
-            float4* xp = reinterpret_cast<float4*>(xch + (g & 1) * WF_XCH + cb * 16 * 64) + lane;
-            const bool fin = kh == (g & 1);
-            if (!fin) {
+                if (SLK_WINO_ABL & 4) {  // cheapest use of every accumulator
 #pragma unroll
-                for (int q = 0; q < 4; ++q) xp[q * 64] = make_float4(y[0][q].x, y[0][q].y, y[1][q].x, y[1][q].y);
-            }
-            lds_barrier();
-            if (fin) {
-                const float4 bv = reinterpret_cast<const float4*>(bias_s)[4 * cb + lk];
-                f2 z[2][4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 o4 = xp[q * 64];
-                    const f2 olo = {o4.x, o4.y}, ohi = {o4.z, o4.w};
-                    // fixed order: K half 0 + K half 1, then bias
-                    z[0][q] = (kh == 0 ? y[0][q] + olo : olo + y[0][q]) + f2{bv.x, bv.y};
-                    z[1][q] = (kh == 0 ? y[1][q] + ohi : ohi + y[1][q]) + f2{bv.z, bv.w};
+                    for (int q = 0; q < 4; ++q) z[h][q] = (m[q] + m[q + 4]) + (m[q + 8] + m[q + 12]);
+                } else {
+                    pk_wino_out(m, z[h]);
                 }
+                const f2 bb = h ? f2{bv.z, bv.w} : f2{bv.x, bv.y};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int h = r >> 1;
-                    float yq[4];
+                for (int q = 0; q < 4; ++q) z[h][q] += bb;
+            }
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) yq[q] = (r & 1) ? z[h][q].y : z[h][q].x;
-                    // max over the raw window, first max wins; = torch's relu-then-pool scan
-                    const float mx = fmaxf(fmaxf(yq[0], yq[1]), fmaxf(yq[2], yq[3]));
-                    const int idx = yq[0] == mx ? 0 : yq[1] == mx ? 1 : yq[2] == mx ? 2 : 3;
-                    const bool pos = mx > 0.f;
-                    const int co = 16 * cb + 4 * lk + r;
-                    const int o = co * P_WIN + t;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pos ? mx : 0.f), prs, 4 * o, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pos ? idx : CODE_NONE), crs, o, 0, 0);
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int h = r >> 1;
+                float yq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) yq[q] = (r & 1) ? z[h][q].y : z[h][q].x;
+                // max over the raw window, first max wins; = torch's relu-then-pool scan
+                const float mx = fmaxf(fmaxf(yq[0], yq[1]), fmaxf(yq[2], yq[3]));
+                const int idx = yq[0] == mx ? 0 : yq[1] == mx ? 1 : yq[2] == mx ? 2 : 3;
+                const bool pos = mx > 0.f;
+                const int o = (16 * wave + 4 * lk + r) * P_WIN + t;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pos ? mx : 0.f), prs, 4 * o, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pos ? idx : CODE_NONE), crs, o, 0, 0);
             }
         }
         buf ^= 1;
@@ -329,5 +327,238 @@ extern "C" int slk_conv2_fwd_pool(const float* act, const float* W2, const float
     const int nunit = 3 * B;
     conv2_fwd_pool_wino_kernel<<<nunit < WF_GRID ? nunit : WF_GRID, WF_THREADS, 0, slk_stream(stream)>>>(
         act, W2, b2, pooled, code, B);
+    return slk_launch_status();
+}
+
+// ============================================================================ shared helpers
+// 4x4 patch of a row-major LDS image (row stride A_HW floats) as 8 ds_read_b64, as row pairs
+__device__ __forceinline__ void lds_patch_pk(const float* ps, f2 (&lo)[4], f2 (&hi)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        lo[r] = *reinterpret_cast<const f2*>(ps + r * A_HW);
+        hi[r] = *reinterpret_cast<const f2*>(ps + r * A_HW + 2);
+    }
+}
+
+// Routing lookup tables, built once per workgroup in LDS (float4 entries, code c = 0..4):
+//   dgrad  EXP[c] = (c==0, c==1, c==2, c==3): the 2x2 block of a window whose gradient sits at c;
+//   wgrad  ZT[c][16] = A[i][c>>1] * A[j][c&1] (A = [1 0; 1 1; 1 -1; 0 -1]): Z = A dY A^T of that block.
+// Code 4 (ReLU-blocked window) maps to zeros. A lookup + packed multiplies replaces per-element
+// compares and selects: on gfx950 every VALU instruction costs its issue cycles on top of the f32
+// MFMA stream (tools/ubench/fillers.hip), packed or not, so the count of instructions is what matters.
+__device__ __forceinline__ void build_luts(float* lut_exp, float* lut_z, int tid) {
+    if (tid < 5 * 4) {
+        const int c = tid >> 2, k = tid & 3;
+        lut_exp[tid] = (c == k) ? 1.f : 0.f;
+    }
+    if (tid < 5 * 16) {
+        const int c = tid >> 4, i = (tid >> 2) & 3, j = tid & 3;
+        const float a0[4] = {1.f, 1.f, 1.f, 0.f}, a1[4] = {0.f, 1.f, -1.f, -1.f};
+        const float ai = (c & 2) ? a1[i] : a0[i];
+        const float aj = (c & 1) ? a1[j] : a0[j];
+        lut_z[tid] = c < 4 ? ai * aj : 0.f;
+    }
+}
+
+// ============================================================================ dgrad (cut gradient)
+// g[ci][y][x] = sum_co sum_{a,b} dcpad[co][y+a][x+b] * W2[co][ci][2-a][2-b]: a "full" correlation of
+// the pool/ReLU-routed conv2 output gradient dc (24x24, zero border of 2 -> 28x28) with the flipped
+// filter. Winograd F(2x2,3x3): 13 x 13 = 169 output tiles per sample (11 groups of 16, the last one
+// 9 wide), M[ij][ci][tile] = sum_co U'[ij][ci][co] * V[ij][co][tile]: 16 GEMMs of 32 x 169 x 64.
+// The 4x4 input patch of tile (ty, tx) is dcpad rows 2ty .. 2ty+3 = pooling windows (ty-1 .. ty,
+// tx-1 .. tx): each quadrant holds at most ONE nonzero, dpooled at the window's routing code, so the
+// patch is expanded in registers straight from (dpooled, code) staged in LDS (lookup + 2 packed
+// multiplies per window) — dc never exists.
+// Persistent, one 4-wave workgroup per CU (one wave per SIMD, 512 registers): wave w owns the K half
+// kh = w&1 (co 32kh .. 32kh+31, 8 k steps) for BOTH 16-row M blocks (all 32 ci), so one expanded
+// patch feeds 32 MFMAs, and group slot gs = w>>1 (groups 2p + gs, p = 0..5; slot 12 is empty). The
+// transformed flipped filters stay in registers for the launch (A operand: lane l holds
+// U'[ij][16m + (l&15)][32kh + 4s + (l>>4)], 256 VGPRs). Unit = one sample: dpooled (36,864 B) + code
+// (9,216 B) by LDS-DMA, double-buffered. Per group the two K halves meet once: each wave parks the
+// 2x2 partial outputs of the M block its partner finishes (ds_write_b128), one barrier, then finishes
+// its own M block (mine + partner's: commutative, so bitwise reproducible) and stores the cut gradient.
+constexpr int WD_WAVES = 4;
+constexpr int WD_THREADS = WD_WAVES * 64;
+constexpr int WD_PAIRS = 6;                    // group pairs per sample: groups 0..10 (+ an empty 11th)
+constexpr int WD_NT = 13 * 13;
+constexpr int WD_DP_CH = P_SAMPLE / 256;       // 36 KiB chunks of dpooled
+constexpr int WD_CD_OFF = P_SAMPLE + 64;       // float offset of the code bytes in a buffer
+constexpr int WD_CD_CH = P_SAMPLE / 1024;      // 9 KiB chunks of code
+constexpr int WD_BSTR = WD_CD_OFF + P_SAMPLE / 4 + 64;   // 11648 floats = 46,592 B per buffer
+constexpr int WD_XCH = 2 * 2 * 4 * 64 * 4;     // per parity: [group slot][writer kh][r][lane] float4
+constexpr int WD_GRID = 256;
+
+__device__ __forceinline__ void wd_dma_sample(const float* __restrict__ dpool, const uint8_t* __restrict__ code, int b,
+                                              const float* dst, int wave, int lane) {
+    const uint32_t base = (uint32_t)(uintptr_t)dst;
+    const float* dsrc = dpool + (size_t)b * P_SAMPLE;
+    const uint8_t* csrc = code + (size_t)b * P_SAMPLE;
+#pragma unroll 1
+    for (int c = wave; c < WD_DP_CH + WD_CD_CH; c += WD_WAVES) {
+        if (c < WD_DP_CH)
+            glds16(dsrc + c * 256 + lane * 4, __builtin_amdgcn_readfirstlane(base + c * 1024));
+        else
+            glds16(csrc + (c - WD_DP_CH) * 1024 + lane * 16,
+                   __builtin_amdgcn_readfirstlane(base + WD_CD_OFF * 4 + (c - WD_DP_CH) * 1024));
+    }
+}
+
+__global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
+    const float* __restrict__ dpool, const uint8_t* __restrict__ code, const float* __restrict__ W2,
+    float* __restrict__ gcut, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * WD_BSTR + 2 * WD_XCH + 32];
+    float* xch = smem + 2 * WD_BSTR;
+    float* lut = xch + 2 * WD_XCH;  // EXP table, 5 float4
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int kh = wave & 1, gs = wave >> 1;
+
+    int b = blockIdx.x;
+    if (b < B) wd_dma_sample(dpool, code, b, smem, wave, lane);
+    if (tid < 20) lut[tid] = (tid >> 2) == (tid & 3) ? 1.f : 0.f;
+
+    // transformed flipped filters: lane (ci = 16m + li, co = 32kh + 4s + lk)
+    float uw[2][8][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const float* gp = W2 + (size_t)(32 * kh + 4 * s + lk) * K2 + (16 * m + li) * 9;
+            float g[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) g[k] = gp[8 - k];
+            wino_filter(g, uw[m][s]);
+        }
+    wg_wait_vmcnt<0>();
+
+    int buf = 0;
+#pragma unroll 1
+    for (; b < B; b += gridDim.x) {
+        // this sample's staging has landed (its DMA preceded this wave's 48 stores of the previous
+        // sample) and every wave is done with the other buffer
+        wg_wait_vmcnt<8>();
+        lds_barrier();
+        const int nb = b + gridDim.x;
+        if (nb < B) wd_dma_sample(dpool, code, nb, smem + (buf ^ 1) * WD_BSTR, wave, lane);
+        const float* dps = smem + buf * WD_BSTR + (32 * kh + lk) * P_WIN;
+        const uint8_t* cds = reinterpret_cast<const uint8_t*>(smem + buf * WD_BSTR + WD_CD_OFF) + (32 * kh + lk) * P_WIN;
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(gcut + (size_t)b * A_SAMPLE, 0, A_SAMPLE * 4, 0x00020000);
+#pragma unroll 1
+        for (int p = 0; p < WD_PAIRS; ++p) {
+            const int t = 16 * (2 * p + gs) + li;
+            const int tc = t < WD_NT ? t : WD_NT - 1;
+            const int ty = tc / 13, tx = tc - 13 * (tc / 13);
+            // windows (ty-1+wy, tx-1+wx), clamped in range; out-of-range ones use code 4 (zeros)
+            int woff[4];
+            bool wok[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int py = ty - 1 + (w >> 1), px = tx - 1 + (w & 1);
+                wok[w] = py >= 0 && py < P_HW && px >= 0 && px < P_HW;
+                woff[w] = min(max(py, 0), P_HW - 1) * P_HW + min(max(px, 0), P_HW - 1);
+            }
+            f32x4 acc[2][16];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int ij = 0; ij < 16; ++ij) acc[m][ij] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+            // k step s = channel co = 32kh + 4s + lk: raw (value, code) of the 4 windows
+            float dv[2][4];
+            int cd[2][4];
+            auto load = [&](int s, float (&v)[4], int (&c)[4]) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    v[w] = dps[s * 4 * P_WIN + woff[w]];
+                    c[w] = wok[w] ? (int)cds[s * 4 * P_WIN + woff[w]] : 4;
+                }
+            };
+            auto expand = [&](const float (&v)[4], const int (&c)[4], f2 (&v01)[4], f2 (&v23)[4]) {
+                f2 Rlo[4], Rhi[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const float4 e = reinterpret_cast<const float4*>(lut)[c[w]];
+                    const f2 vv = {v[w], v[w]};
+                    const f2 r0 = vv * f2{e.x, e.y}, r1 = vv * f2{e.z, e.w};
+                    const int wy = w >> 1;
+                    if (w & 1) { Rhi[2 * wy] = r0; Rhi[2 * wy + 1] = r1; }
+                    else { Rlo[2 * wy] = r0; Rlo[2 * wy + 1] = r1; }
+                }
+                pk_wino_in(Rlo, Rhi, v01, v23);
+            };
+            load(0, dv[0], cd[0]);
+            load(1, dv[1], cd[1]);
+            f2 v01[4], v23[4];
+            expand(dv[0], cd[0], v01, v23);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                if (s < 6) load(s + 2, dv[s & 1], cd[s & 1]);  // in flight under this step's MFMAs
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[m][4 * i + 0] = mfma16x16x4(uw[m][s][4 * i + 0], v01[i].x, acc[m][4 * i + 0]);
+                        acc[m][4 * i + 1] = mfma16x16x4(uw[m][s][4 * i + 1], v01[i].y, acc[m][4 * i + 1]);
+                        acc[m][4 * i + 2] = mfma16x16x4(uw[m][s][4 * i + 2], v23[i].x, acc[m][4 * i + 2]);
+                        acc[m][4 * i + 3] = mfma16x16x4(uw[m][s][4 * i + 3], v23[i].y, acc[m][4 * i + 3]);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+                if (s < 7) expand(dv[(s + 1) & 1], cd[(s + 1) & 1], v01, v23);
+            }
+            // partial output transform (rows ci = 16m + 4lk + r, pairs r = 2h, 2h+1)
+            f2 y[2][2][4];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    f2 mm[16];
+#pragma unroll
+                    for (int ij = 0; ij < 16; ++ij) mm[ij] = h ? acc[m][ij].zw : acc[m][ij].xy;
+                    pk_wino_out(mm, y[m][h]);
+                }
+            auto row = [&](const f2 (&ym)[2][4], int r) -> float4 {
+                const int h = r >> 1;
+                return (r & 1) ? make_float4(ym[h][0].y, ym[h][1].y, ym[h][2].y, ym[h][3].y)
+                               : make_float4(ym[h][0].x, ym[h][1].x, ym[h][2].x, ym[h][3].x);
+            };
+            float4* xw = reinterpret_cast<float4*>(xch + (p & 1) * WD_XCH) + (gs * 2 + kh) * 4 * 64 + lane;
+            const float4* xr = reinterpret_cast<const float4*>(xch + (p & 1) * WD_XCH) + (gs * 2 + (kh ^ 1)) * 4 * 64 + lane;
+            // park the M block the partner finishes (kh = 0 finishes ci 0..15, kh = 1 ci 16..31)
+            if (kh == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[0], r);
+            }
+            lds_barrier();
+            typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+            auto finish = [&](const f2 (&ym)[2][4], int mb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float4 a = row(ym, r), o = xr[r * 64];
+                    const float4 tot = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
+                    const int ci = 16 * mb + 4 * lk + r;
+                    const int off = t < WD_NT ? 4 * (ci * A_PIX + 2 * ty * A_HW + 2 * tx) : 0x7ffffff0;
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(tot.x), __float_as_uint(tot.y)}, grs, off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(tot.z), __float_as_uint(tot.w)}, grs, off + 4 * A_HW, 0, 0);
+                }
+            };
+            if (kh == 0) finish(y[0], 0);
+            else finish(y[1], 1);
+        }
+        buf ^= 1;
+    }
+}
+
+extern "C" int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const float* W2,
+                               float* cut_grad, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(dpooled && code && W2 && cut_grad);
+    conv2_dgrad_wino_kernel<<<B < WD_GRID ? B : WD_GRID, WD_THREADS, 0, slk_stream(stream)>>>(
+        dpooled, code, W2, cut_grad, B);
     return slk_launch_status();
 }

@@ -37,6 +37,7 @@ _SIGS = {
     "slk_fc_wgrad": [_P, _P, _P, _I, _P],
     "slk_fc_wgrad_nslab": [_I],
     "slk_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_conv2_dgrad_direct": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad_nslab": [_I],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],

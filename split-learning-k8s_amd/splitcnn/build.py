@@ -10,6 +10,7 @@ import os
 import shutil
 import subprocess
 import sys
+import tempfile
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
@@ -18,6 +19,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
 SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip", "slk_wide.hip",
            "slk_wide_head.hip", "slk_wino.hip"]
 ARCH = "gfx950"
+# Per-source extra hipcc flags (none needed at present; profiling variants pass -D defines).
+EXTRA_FLAGS: dict = {}
 
 
 def _hipcc() -> str:
@@ -42,21 +45,45 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in srcs + hdrs)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    """Compile every HIP source for gfx950 and link libslk.so next to this file."""
-    if not force and not needs_build():
+def _compile_cmd(src: str, obj: str, defines) -> list:
+    return [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE_DIR, *defines,
+            *EXTRA_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+
+
+def build_library(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Compile every HIP source for gfx950 (one object per source, in parallel, with its per-source
+    flags) and link libslk.so next to this file — or `out` with extra `defines` (profiling variants)."""
+    target = out or LIB_PATH
+    if out is None and not force and not needs_build():
         return LIB_PATH
     srcs, _ = _inputs()
-    tmp = LIB_PATH + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", INCLUDE_DIR, *srcs, "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    tmpdir = tempfile.mkdtemp(prefix="slk_build_")
+    try:
+        jobs = []
+        for src in srcs:
+            obj = os.path.join(tmpdir, os.path.basename(src) + ".o")
+            cmd = _compile_cmd(src, obj, list(defines))
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            jobs.append((src, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+        failed = []
+        for src, _, proc in jobs:
+            _, err = proc.communicate()
+            if proc.returncode != 0:
+                failed.append(f"{os.path.basename(src)} ({proc.returncode}):\n{err[-4000:]}")
+        if failed:
+            raise RuntimeError("hipcc failed: " + "\n".join(failed))
+        tmp = target + ".tmp"
+        link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[obj for _, obj, _ in jobs], "-o", tmp]
+        if verbose:
+            print(" ".join(link), file=sys.stderr)
+        res = subprocess.run(link, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-4000:]}")
+        os.replace(tmp, target)
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    return target
 
 
 if __name__ == "__main__":
