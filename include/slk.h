@@ -119,10 +119,15 @@ int slk_conv2_dgrad_direct(const float* dpooled, const uint8_t* code, const floa
                            int B, void* stream);
 
 /* conv2 weight/bias gradient partials: slabs [slk_conv2_wgrad_nslab(B)][18496] laid out as
- * [dW2 (64*288) | db2 (64)], i.e. the head of the server flat block. MFMA f32. */
+ * [dW2 (64*288) | db2 (64)], i.e. the head of the server flat block; their fixed-order sum is the
+ * gradient. Winograd F(2x2,3x3) filter gradient on the f32 MFMA (G^T dU G applied per slab). */
 int slk_conv2_wgrad(const float* act, const float* dpooled, const uint8_t* code, float* slabs,
                     int B, void* stream);
 int slk_conv2_wgrad_nslab(int B);
+/* The same op as a direct implicit GEMM (A/B and cross-check path), with its own slab count. */
+int slk_conv2_wgrad_direct(const float* act, const float* dpooled, const uint8_t* code, float* slabs,
+                           int B, void* stream);
+int slk_conv2_wgrad_direct_nslab(int B);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
     }
 }
 
-extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
+extern "C" int slk_conv2_wgrad_direct_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
 
 // ============================================================================ fc1 + cross-entropy
 // 8 samples per 512-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy
@@ -724,12 +724,12 @@ extern "C" int slk_conv2_dgrad_direct(const float* dpooled, const uint8_t* code,
     return slk_launch_status();
 }
 
-extern "C" int slk_conv2_wgrad(const float* act, const float* dpooled, const uint8_t* code,
+extern "C" int slk_conv2_wgrad_direct(const float* act, const float* dpooled, const uint8_t* code,
                                float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(act && dpooled && code && slabs);
-    conv2_wgrad_kernel<<<slk_conv2_wgrad_nslab(B), C2W_THREADS, 0, slk_stream(stream)>>>(
+    conv2_wgrad_kernel<<<slk_conv2_wgrad_direct_nslab(B), C2W_THREADS, 0, slk_stream(stream)>>>(
         act, dpooled, code, slabs, B);
     return slk_launch_status();
 }

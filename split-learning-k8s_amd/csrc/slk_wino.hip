@@ -562,3 +562,241 @@ extern "C" int slk_conv2_dgrad(const float* dpooled, const uint8_t* code, const 
         dpooled, code, W2, cut_grad, B);
     return slk_launch_status();
 }
+
+// ============================================================================ wgrad (conv2 weights)
+// dW2[co][ci][a][b] = sum_{b,y,x} dc[co][y][x] * act[ci][y+a][x+b];  db2[co] = sum dc.
+// Winograd F(2x2,3x3) filter gradient: with U = G g G^T linear in g, per 2x2 output tile t (= one
+// pool window)  dU[ij][co][ci] += Z_t[ij][co] * V_t[ij][ci],  Z_t = A dY_t A^T (the routed window:
+// one nonzero, so Z_t = v * ZT[code], a lookup and 8 packed multiplies), V_t = B^T d_t B (the
+// forward's input transform of the act patch), and dW = G^T dU G once per workgroup slab (linear, so
+// the slabs keep the [dW2 | db2] layout slk_sgd_from_slabs sums in fixed order).
+// GEMM per (i,j): M = 64 co, N = 32 ci, K = tiles x samples; v_mfma_f32_16x16x4_f32 with A = Z
+// (lane: co = l&15, tile = l>>4) and B = V (tile = l>>4, ci = l&15); no filter registers.
+// Persistent, one 4-wave workgroup per CU: wave w owns the output channels 32*(w&1) .. +31 (2 M
+// blocks) x all 32 input channels (2 N blocks) = 64 accumulator tiles (256 AGPRs), and the K steps
+// (4 tiles each) of parity w>>1. Unit = (sample, band of 4 tile rows = 48 tiles = 12 K steps): the
+// act band (as the forward) + the dpooled/code band of the same windows, double-buffered by LDS-DMA.
+// At the end the two K-parity waves of each M half meet in LDS (fixed order), apply G^T . G and
+// write the workgroup's slab; db2 rides along as ZT[c][1][1] = 1 for every routed window.
+constexpr int WW_WAVES = 4;
+constexpr int WW_THREADS = WW_WAVES * 64;
+constexpr int WW_DSTR = 52;                           // dpooled band row stride (48 used; 2-way banks)
+constexpr int WW_DP_OFF = WF_BSTR;                    // float offset of the dpooled band in a buffer
+constexpr int WW_DP_CH = 64 * 13 / 64;                // 13 chunks (13 sixteen-byte pieces per row)
+constexpr int WW_CSTR = 64;                           // code band row stride in bytes (48 used)
+constexpr int WW_CD_OFF = WW_DP_OFF + 64 * WW_DSTR;   // float offset of the code band
+constexpr int WW_CD_CH = 64 * 4 / 64;                 // 4 chunks (4 pieces per row)
+constexpr int WW_NCH = WF_CHUNKS + WW_DP_CH + WW_CD_CH;
+constexpr int WW_BSTR = WW_CD_OFF + 64 * WW_CSTR / 4; // 12800 floats = 51,200 B per buffer
+constexpr int WW_GRID = 256;
+constexpr int WW_SLAB = W2_N + C2;
+static_assert(WW_DP_OFF * 4 == WF_CHUNKS * 1024 && WW_CD_OFF * 4 == (WF_CHUNKS + WW_DP_CH) * 1024,
+              "the three staging regions are consecutive KiB chunks");
+
+__device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const float* __restrict__ dpool,
+                                            const uint8_t* __restrict__ code, int u, const float* dst, int wave,
+                                            int lane) {
+    const int b = u / 3, band = u - 3 * (u / 3);
+    const uint32_t base = (uint32_t)(uintptr_t)dst;
+    const float* asrc = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
+    const float* dsrc = dpool + (size_t)b * P_SAMPLE + band * 48;
+    const uint8_t* csrc = code + (size_t)b * P_SAMPLE + band * 48;
+#pragma unroll 1
+    for (int c = wave; c < WW_NCH; c += WW_WAVES) {
+        const void* src;
+        if (c < WF_CHUNKS) {
+            const int p = min(c * 64 + lane, WF_PIECES - 1);
+            const int ci = p / 65, k = p - 65 * (p / 65);
+            src = asrc + ci * A_PIX + 4 * k;
+        } else if (c < WF_CHUNKS + WW_DP_CH) {
+            const int p = (c - WF_CHUNKS) * 64 + lane;
+            const int co = p / 13, k = min(p - 13 * (p / 13), 11);
+            src = dsrc + co * P_WIN + 4 * k;
+        } else {
+            const int p = (c - WF_CHUNKS - WW_DP_CH) * 64 + lane;
+            const int co = p >> 2, k = min(p & 3, 2);
+            src = csrc + co * P_WIN + 16 * k;
+        }
+        glds16(src, __builtin_amdgcn_readfirstlane(base + c * 1024));
+    }
+}
+
+// dW = G^T dU G (adjoint of wino_filter), dw row-major dw[3*k + l]
+__device__ __forceinline__ void wino_filter_grad(const float (&du)[16], float (&dw)[9]) {
+    float t[12];  // t = G^T dU : 3 x 4
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float s = du[4 + j] + du[8 + j];
+        t[0 * 4 + j] = du[j] + 0.5f * s;
+        t[1 * 4 + j] = 0.5f * (du[4 + j] - du[8 + j]);
+        t[2 * 4 + j] = 0.5f * s + du[12 + j];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float s = t[k * 4 + 1] + t[k * 4 + 2];
+        dw[k * 3 + 0] = t[k * 4 + 0] + 0.5f * s;
+        dw[k * 3 + 1] = 0.5f * (t[k * 4 + 1] - t[k * 4 + 2]);
+        dw[k * 3 + 2] = 0.5f * s + t[k * 4 + 3];
+    }
+}
+
+__global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
+    const float* __restrict__ act, const float* __restrict__ dpool, const uint8_t* __restrict__ code,
+    float* __restrict__ slabs, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * WW_BSTR + 5 * 16];
+    float* lutz = smem + 2 * WW_BSTR;  // ZT[c][16]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int mh = wave & 1, tp = wave >> 1;
+    const int nunit = 3 * B;
+
+    int u = blockIdx.x;
+    if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wave, lane);
+    if (tid < 5 * 16) {
+        const int c = tid >> 4, i = (tid >> 2) & 3, j = tid & 3;
+        const float ai = (c & 2) ? (i == 0 ? 0.f : (i == 1 ? 1.f : -1.f)) : (i == 3 ? 0.f : 1.f);
+        const float aj = (c & 1) ? (j == 0 ? 0.f : (j == 1 ? 1.f : -1.f)) : (j == 3 ? 0.f : 1.f);
+        lutz[tid] = c < 4 ? ai * aj : 0.f;
+    }
+    f32x4 acc[2][2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int ij = 0; ij < 16; ++ij) acc[m][n][ij] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dbp[2] = {0.f, 0.f};
+    wg_wait_vmcnt<0>();
+
+    int buf = 0;
+#pragma unroll 1
+    for (; u < nunit; u += gridDim.x) {
+        // this unit's band landed (no stores in this loop: vmcnt(0) is that DMA alone) and every wave
+        // is done with the other buffer
+        wg_wait_vmcnt<0>();
+        lds_barrier();
+        const int nu = u + gridDim.x;
+        if (nu < nunit) ww_dma_unit(act, dpool, code, nu, smem + (buf ^ 1) * WW_BSTR, wave, lane);
+        const float* img = smem + buf * WW_BSTR;
+        const float* dpb = img + WW_DP_OFF + (32 * mh + li) * WW_DSTR;
+        const uint8_t* cdb = reinterpret_cast<const uint8_t*>(img + WW_CD_OFF) + (32 * mh + li) * WW_CSTR;
+        const int band = u - 3 * (u / 3);
+
+        // K step j (tiles 4ks + lk of the band, ks = tp + 2j): raw act patches of ci = li, 16 + li
+        // and the routed windows of co = 32mh + li, 32mh + 16 + li
+        f2 Rlo[2][2][4], Rhi[2][2][4];
+        float dv[2][2];
+        int cd[2][2];
+        auto load = [&](int j, f2 (&lo)[2][4], f2 (&hi)[2][4], float (&v)[2], int (&c)[2]) {
+            const int tl = 4 * (tp + 2 * j) + lk;
+            const int t = 48 * band + tl;
+            const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
+            const float* pa = img + li * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
+            lds_patch_pk(pa, lo[0], hi[0]);
+            lds_patch_pk(pa + 16 * WF_CSTR, lo[1], hi[1]);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                v[m] = dpb[m * 16 * WW_DSTR + tl];
+                c[m] = cdb[m * 16 * WW_CSTR + tl];
+            }
+        };
+        f2 v01[2][4], v23[2][4], z01[2][4], z23[2][4];
+        auto xform = [&](const f2 (&lo)[2][4], const f2 (&hi)[2][4], const float (&v)[2], const int (&c)[2]) {
+            pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
+            pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const float4* zt = reinterpret_cast<const float4*>(lutz) + 4 * c[m];
+                const f2 vv = {v[m], v[m]};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 e = zt[i];
+                    z01[m][i] = vv * f2{e.x, e.y};
+                    z23[m][i] = vv * f2{e.z, e.w};
+                }
+                dbp[m] += z01[m][1].y;  // ZT[c][1][1] = 1 for a routed window, 0 for code 4
+            }
+        };
+        load(0, Rlo[0], Rhi[0], dv[0], cd[0]);
+        load(1, Rlo[1], Rhi[1], dv[1], cd[1]);
+        xform(Rlo[0], Rhi[0], dv[0], cd[0]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // under these MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[m][n][4 * i + 0] = mfma16x16x4(z01[m][i].x, v01[n][i].x, acc[m][n][4 * i + 0]);
+                        acc[m][n][4 * i + 1] = mfma16x16x4(z01[m][i].y, v01[n][i].y, acc[m][n][4 * i + 1]);
+                        acc[m][n][4 * i + 2] = mfma16x16x4(z23[m][i].x, v23[n][i].x, acc[m][n][4 * i + 2]);
+                        acc[m][n][4 * i + 3] = mfma16x16x4(z23[m][i].y, v23[n][i].y, acc[m][n][4 * i + 3]);
+                    }
+            __builtin_amdgcn_sched_barrier(0);
+            if (j < 5) xform(Rlo[(j + 1) & 1], Rhi[(j + 1) & 1], dv[(j + 1) & 1], cd[(j + 1) & 1]);
+        }
+        buf ^= 1;
+    }
+
+    // ---- combine the K parities, transform, write this workgroup's [dW2 | db2] slab
+    float* slab = slabs + (size_t)blockIdx.x * WW_SLAB;
+    float* park = smem;  // [mh][n][ij][r][lane] for one M block m at a time (16384 floats)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        lds_barrier();  // previous readers of `park` (or of the staging buffers) are done
+        if (tp == 1) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int ij = 0; ij < 16; ++ij)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) park[(((mh * 2 + n) * 16 + ij) * 4 + r) * 64 + lane] = acc[m][n][ij][r];
+        }
+        lds_barrier();
+        if (tp == 0) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float du[16], dw[9];
+#pragma unroll
+                    for (int ij = 0; ij < 16; ++ij) du[ij] = acc[m][n][ij][r] + park[(((mh * 2 + n) * 16 + ij) * 4 + r) * 64 + lane];
+                    wino_filter_grad(du, dw);
+                    const int co = 32 * mh + 16 * m + 4 * lk + r, ci = 16 * n + li;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) slab[co * K2 + ci * 9 + k] = dw[k];
+                }
+        }
+    }
+    // db2: lanes of one co hold partials over tiles (lk) -> butterfly, then K parity 0 + 1
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        dbp[m] += __shfl_xor(dbp[m], 16, 64);
+        dbp[m] += __shfl_xor(dbp[m], 32, 64);
+    }
+    lds_barrier();
+    if (tp == 1 && lk == 0) {
+        park[(mh * 2 + 0) * 16 + li] = dbp[0];
+        park[(mh * 2 + 1) * 16 + li] = dbp[1];
+    }
+    lds_barrier();
+    if (tp == 0 && lk == 0) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) slab[W2_N + 32 * mh + 16 * m + li] = dbp[m] + park[(mh * 2 + m) * 16 + li];
+    }
+}
+
+extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (3 * B < WW_GRID ? 3 * B : WW_GRID) : 0; }
+
+extern "C" int slk_conv2_wgrad(const float* act, const float* dpooled, const uint8_t* code,
+                               float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(act && dpooled && code && slabs);
+    conv2_wgrad_wino_kernel<<<slk_conv2_wgrad_nslab(B), WW_THREADS, 0, slk_stream(stream)>>>(act, dpooled, code, slabs, B);
+    return slk_launch_status();
+}

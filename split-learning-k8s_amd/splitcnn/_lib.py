@@ -40,6 +40,8 @@ _SIGS = {
     "slk_conv2_dgrad_direct": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad_nslab": [_I],
+    "slk_conv2_wgrad_direct": [_P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad_direct_nslab": [_I],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
     "slk_sgd": [_P, _P, _I, _F, _P],

@@ -88,13 +88,14 @@ def conv1_wgrad_remask_slabs(x, W1, b1, cut_grad, slabs=None):
 
 
 # ------------------------------------------------------------------------------------ server stage
-def conv2_fwd_pool(act, W2, b2, pooled=None, code=None):
+def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False):
+    """Winograd F(2x2,3x3) kernel; direct=True runs the direct implicit-GEMM kernel (cross-check)."""
     B = batch_of(act, (32, 26, 26), "act")
     pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
     code = _out(code, (B, 64, 12, 12), act, torch.uint8, "code")
-    _lib.call("slk_conv2_fwd_pool", _dev(act, "act"), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
-              _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"), _dev(code, "code", dtype=torch.uint8),
-              B, _stream(act))
+    _lib.call("slk_conv2_fwd_pool_direct" if direct else "slk_conv2_fwd_pool", _dev(act, "act"),
+              _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
+              _dev(code, "code", dtype=torch.uint8), B, _stream(act))
     return pooled, code
 
 
@@ -168,24 +169,25 @@ def _dpooled_batch(dpooled):
     return _pooled_batch(dpooled)
 
 
-def conv2_dgrad(dpooled, code, W2, out=None):
+def conv2_dgrad(dpooled, code, W2, out=None, direct=False):
     B = _dpooled_batch(dpooled)
     cut_grad = _out(out, (B, 32, 26, 26), dpooled, name="cut_grad")
-    _lib.call("slk_conv2_dgrad", _dev(dpooled, "dpooled"), _dev(code, "code", (B, 64, 12, 12), torch.uint8),
-              _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(cut_grad, "cut_grad"), B, _stream(dpooled))
+    _lib.call("slk_conv2_dgrad_direct" if direct else "slk_conv2_dgrad", _dev(dpooled, "dpooled"),
+              _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+              _dev(cut_grad, "cut_grad"), B, _stream(dpooled))
     return cut_grad
 
 
-def conv2_wgrad_nslab(B: int) -> int:
-    return _lib.query("slk_conv2_wgrad_nslab", B)
+def conv2_wgrad_nslab(B: int, direct: bool = False) -> int:
+    return _lib.query("slk_conv2_wgrad_direct_nslab" if direct else "slk_conv2_wgrad_nslab", B)
 
 
-def conv2_wgrad_slabs(act, dpooled, code, slabs=None):
+def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False):
     B = batch_of(act, (32, 26, 26), "act")
     if _dpooled_batch(dpooled) != B:
         raise ValueError("act / dpooled batch mismatch")
-    slabs = _out(slabs, (conv2_wgrad_nslab(B), CONV2_SLAB), act, name="slabs")
-    _lib.call("slk_conv2_wgrad", _dev(act, "act"), _dev(dpooled, "dpooled"),
+    slabs = _out(slabs, (conv2_wgrad_nslab(B, direct), CONV2_SLAB), act, name="slabs")
+    _lib.call("slk_conv2_wgrad_direct" if direct else "slk_conv2_wgrad", _dev(act, "act"), _dev(dpooled, "dpooled"),
               _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(act))
     return slabs
 

@@ -1,0 +1,76 @@
+"""GPU: the Winograd F(2x2,3x3) conv2 kernels (the production path behind slk_conv2_fwd_pool /
+slk_conv2_dgrad / slk_conv2_wgrad) against the direct implicit-GEMM kernels kept in the library
+(slk_conv2_*_direct) and against the numpy oracle, on identical inputs: ragged batches (1, 5, 64,
+130), the padded 12th tile group of dgrad, determinism.
+
+Tolerances: Winograd and direct are both f32 with different summation orders; measured and simulated
+differences are ~3e-7 relative, asserted at 1e-5 (max |diff| / max |ref|). Max-pool routing may differ
+only at numerical ties of the fp64 conv output (tie_discrepancies, 1e-5)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(gpu, B, seed):
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage
+    a, b = init_models(seed=seed)
+    x, y = SyntheticMNIST(seed + 1).batch(B)
+    act = ClientStage(a, device=gpu).forward(x.to(gpu)).clone()
+    p = {k: v.detach().to(gpu).contiguous() for k, v in
+         {"W2": b.conv2.weight, "b2": b.conv2.bias, "W3": b.fc1.weight, "b3": b.fc1.bias}.items()}
+    return act, p, y.to(gpu)
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 130])
+def test_winograd_matches_direct_and_oracle(gpu, B):
+    from oracle.split_step import conv3x3, conv3x3_dgrad, conv3x3_wgrad, maxpool2_bwd, relu, tie_discrepancies
+    from splitcnn import ops
+    act, p, y = _inputs(gpu, B, seed=B)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    pd, cd = ops.conv2_fwd_pool(act, p["W2"], p["b2"], direct=True)
+    a64 = act.double().cpu().numpy()
+    r = relu(conv3x3(a64, p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
+    codes_w, codes_d = cw.cpu().numpy().astype(np.int64), cd.cpu().numpy().astype(np.int64)
+    n, ok = tie_discrepancies(r, codes_d, codes_w)
+    assert ok, f"{n} routing differences that are not ties"
+    same = torch.from_numpy(codes_w == codes_d).to(gpu)
+    assert rel_err(pw[same].cpu().numpy(), pd[same].cpu().numpy()) <= 1e-5
+    pr = r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))
+    assert rel_err(pw.cpu().numpy(), pr) <= 1e-5
+
+    # backward on identical inputs (the Winograd forward's routing for both paths)
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    gw = ops.conv2_dgrad(dp, cw, p["W2"])
+    gd = ops.conv2_dgrad(dp, cw, p["W2"], direct=True)
+    assert rel_err(gw.cpu().numpy(), gd.cpu().numpy()) <= 1e-5
+    # oracle: dc from the GPU routing, then the fp64 input / weight gradients
+    dp64 = dp.double().cpu().numpy().reshape(B, 64, 12, 12)
+    dc = maxpool2_bwd(np.where(codes_w < 4, dp64, 0.0), np.minimum(codes_w, 3), (B, 64, 24, 24))
+    assert rel_err(gw.cpu().numpy(), conv3x3_dgrad(dc, p["W2"].double().cpu().numpy())) <= 1e-5
+    sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw))
+    sd = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, direct=True))
+    assert ops.conv2_wgrad_nslab(B) == min(3 * B, 256)
+    assert rel_err(sw[:18432].cpu().numpy(), sd[:18432].cpu().numpy()) <= 1e-5
+    assert rel_err(sw[18432:].cpu().numpy(), sd[18432:].cpu().numpy()) <= 1e-5
+    dW, db = conv3x3_wgrad(a64, dc)
+    assert rel_err(sw[:18432].cpu().numpy(), dW.reshape(-1)) <= 1e-5
+    assert rel_err(sw[18432:].cpu().numpy(), db) <= 1e-5
+
+
+def test_winograd_kernels_deterministic(gpu):
+    from splitcnn import ops
+    B = 300
+    act, p, y = _inputs(gpu, B, seed=3)
+    runs = []
+    for _ in range(2):
+        pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+        _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+        runs.append((pw.clone(), cw.clone(), ops.conv2_dgrad(dp, cw, p["W2"]).clone(),
+                     ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw)).clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
