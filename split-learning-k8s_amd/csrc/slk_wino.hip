@@ -150,6 +150,31 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 template <int N>
 __device__ __forceinline__ void wg_wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// v_mfma_f32_16x16x4_f32 with the A operand read straight from an AGPR (legal on gfx950, but hipcc
+// copies AGPR-resident operands to a VGPR first — one v_accvgpr_read + s_nop per MFMA, and every
+// VALU instruction costs its issue cycles on top of the f32 MFMA stream). B and C/D in VGPRs.
+// Wait states: B comes from the colstep asm (ends with s_nop 1); the accumulators are read by VALU only
+// after mfma_drain(); AGPRs are written once per launch, long before the first MFMA.
+__device__ __forceinline__ void mfma_a(f32x4& acc, float a, float b) {
+#if SLK_ABL & 1
+    acc[0] += b;
+    asm volatile("" ::"a"(a));
+#else
+    asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "a"(a), "v"(b));
+#endif
+}
+// first k step: C = 0 (an inline constant), so the accumulators need no zeroing instructions
+__device__ __forceinline__ void mfma_a0(f32x4& acc, float a, float b) {
+#if SLK_ABL & 1
+    acc = f32x4{b, 0.f, 0.f, 0.f};
+    asm volatile("" ::"a"(a));
+#else
+    asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=v"(acc) : "a"(a), "v"(b));
+#endif
+}
+// MFMA result -> VALU read: the 8-pass XDL op needs >= 11 wait states before hipcc's code reads acc
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15" ::: "memory"); }
+
 // barrier that retires this wave's LDS traffic but leaves VMEM (LDS-DMA prefetch, stores) in flight
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -458,11 +483,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                 wok[w] = py >= 0 && py < P_HW && px >= 0 && px < P_HW;
                 woff[w] = min(max(py, 0), P_HW - 1) * P_HW + min(max(px, 0), P_HW - 1);
             }
-            f32x4 acc[2][16];
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int ij = 0; ij < 16; ++ij) acc[m][ij] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 acc[2][16];  // written first by the C = 0 MFMAs of k step 0
 
             // k step s = channel co = 32kh + 4s + lk: raw (value, code) of the 4 windows
             float dv[2][4];
@@ -471,7 +492,11 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
                     v[w] = dps[s * 4 * P_WIN + woff[w]];
-                    c[w] = wok[w] ? (int)cds[s * 4 * P_WIN + woff[w]] : 4;
+                    c[w] = cds[s * 4 * P_WIN + woff[w]];  // clamped address: always a valid read
+                }
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    c[w] = wok[w] ? c[w] : 4;
                 }
             };
             auto expand = [&](const float (&v)[4], const int (&c)[4], f2 (&v01)[4], f2 (&v23)[4]) {
@@ -499,14 +524,22 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                 for (int m = 0; m < 2; ++m)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        acc[m][4 * i + 0] = mfma16x16x4(uw[m][s][4 * i + 0], v01[i].x, acc[m][4 * i + 0]);
-                        acc[m][4 * i + 1] = mfma16x16x4(uw[m][s][4 * i + 1], v01[i].y, acc[m][4 * i + 1]);
-                        acc[m][4 * i + 2] = mfma16x16x4(uw[m][s][4 * i + 2], v23[i].x, acc[m][4 * i + 2]);
-                        acc[m][4 * i + 3] = mfma16x16x4(uw[m][s][4 * i + 3], v23[i].y, acc[m][4 * i + 3]);
+                        if (s == 0) {
+                            mfma_a0(acc[m][4 * i + 0], uw[m][s][4 * i + 0], v01[i].x);
+                            mfma_a0(acc[m][4 * i + 1], uw[m][s][4 * i + 1], v01[i].y);
+                            mfma_a0(acc[m][4 * i + 2], uw[m][s][4 * i + 2], v23[i].x);
+                            mfma_a0(acc[m][4 * i + 3], uw[m][s][4 * i + 3], v23[i].y);
+                        } else {
+                            mfma_a(acc[m][4 * i + 0], uw[m][s][4 * i + 0], v01[i].x);
+                            mfma_a(acc[m][4 * i + 1], uw[m][s][4 * i + 1], v01[i].y);
+                            mfma_a(acc[m][4 * i + 2], uw[m][s][4 * i + 2], v23[i].x);
+                            mfma_a(acc[m][4 * i + 3], uw[m][s][4 * i + 3], v23[i].y);
+                        }
                     }
                 __builtin_amdgcn_sched_barrier(0);
                 if (s < 7) expand(dv[(s + 1) & 1], cd[(s + 1) & 1], v01, v23);
             }
+            mfma_drain();
             // partial output transform (rows ci = 16m + 4lk + r, pairs r = 2h, 2h+1)
             f2 y[2][2][4];
 #pragma unroll
