@@ -172,6 +172,21 @@ __device__ __forceinline__ void mfma_a0(f32x4& acc, float a, float b) {
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=v"(acc) : "a"(a), "v"(b));
 #endif
 }
+// accumulators kept in AGPRs (A, B in VGPRs): the weight gradient's 256 accumulator registers
+__device__ __forceinline__ void mfma_acc(f32x4& acc, float a, float b) {
+#if SLK_ABL & 1
+    acc[0] += a * b;
+#else
+    asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+#endif
+}
+__device__ __forceinline__ void mfma_acc0(f32x4& acc, float a, float b) {
+#if SLK_ABL & 1
+    acc = f32x4{a * b, 0.f, 0.f, 0.f};
+#else
+    asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+#endif
+}
 // MFMA result -> VALU read: the 8-pass XDL op needs >= 11 wait states before hipcc's code reads acc
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15" ::: "memory"); }
 
@@ -764,10 +779,10 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
                 for (int n = 0; n < 2; ++n)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        acc[m][n][4 * i + 0] = mfma16x16x4(z01[m][i].x, v01[n][i].x, acc[m][n][4 * i + 0]);
-                        acc[m][n][4 * i + 1] = mfma16x16x4(z01[m][i].y, v01[n][i].y, acc[m][n][4 * i + 1]);
-                        acc[m][n][4 * i + 2] = mfma16x16x4(z23[m][i].x, v23[n][i].x, acc[m][n][4 * i + 2]);
-                        acc[m][n][4 * i + 3] = mfma16x16x4(z23[m][i].y, v23[n][i].y, acc[m][n][4 * i + 3]);
+                        mfma_acc(acc[m][n][4 * i + 0], z01[m][i].x, v01[n][i].x);
+                        mfma_acc(acc[m][n][4 * i + 1], z01[m][i].y, v01[n][i].y);
+                        mfma_acc(acc[m][n][4 * i + 2], z23[m][i].x, v23[n][i].x);
+                        mfma_acc(acc[m][n][4 * i + 3], z23[m][i].y, v23[n][i].y);
                     }
             __builtin_amdgcn_sched_barrier(0);
             if (j < 5) xform(Rlo[(j + 1) & 1], Rhi[(j + 1) & 1], dv[(j + 1) & 1], cd[(j + 1) & 1]);
@@ -775,6 +790,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         buf ^= 1;
     }
 
+    mfma_drain();
     // ---- combine the K parities, transform, write this workgroup's [dW2 | db2] slab
     float* slab = slabs + (size_t)blockIdx.x * WW_SLAB;
     float* park = smem;  // [mh][n][ij][r][lane] for one M block m at a time (16384 floats)
