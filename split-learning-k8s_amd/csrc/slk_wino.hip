@@ -285,9 +285,7 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
             const int t = 48 * band + 16 * g + li;       // tile = pooling window index
             const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
             const float* pp = img + lk * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
-            f32x4 acc[16];
-#pragma unroll
-            for (int ij = 0; ij < 16; ++ij) acc[ij] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 acc[16];  // written first by the C = 0 MFMAs of k step 0
             f2 Rlo[4], Rhi[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -316,13 +314,21 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    acc[4 * i + 0] = mfma16x16x4(uw[s][4 * i + 0], v01[i].x, acc[4 * i + 0]);
-                    acc[4 * i + 1] = mfma16x16x4(uw[s][4 * i + 1], v01[i].y, acc[4 * i + 1]);
-                    acc[4 * i + 2] = mfma16x16x4(uw[s][4 * i + 2], v23[i].x, acc[4 * i + 2]);
-                    acc[4 * i + 3] = mfma16x16x4(uw[s][4 * i + 3], v23[i].y, acc[4 * i + 3]);
+                    if (s == 0) {
+                        mfma_a0(acc[4 * i + 0], uw[s][4 * i + 0], v01[i].x);
+                        mfma_a0(acc[4 * i + 1], uw[s][4 * i + 1], v01[i].y);
+                        mfma_a0(acc[4 * i + 2], uw[s][4 * i + 2], v23[i].x);
+                        mfma_a0(acc[4 * i + 3], uw[s][4 * i + 3], v23[i].y);
+                    } else {
+                        mfma_a(acc[4 * i + 0], uw[s][4 * i + 0], v01[i].x);
+                        mfma_a(acc[4 * i + 1], uw[s][4 * i + 1], v01[i].y);
+                        mfma_a(acc[4 * i + 2], uw[s][4 * i + 2], v23[i].x);
+                        mfma_a(acc[4 * i + 3], uw[s][4 * i + 3], v23[i].y);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
+            mfma_drain();
             // output transform, two rows (co = 16w + 4lk + r, r = 2h, 2h+1) per packed op; + bias
             f2 z[2][4];
 #pragma unroll
