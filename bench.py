@@ -137,6 +137,16 @@ def kernel_pass(run_eager, K, device):
         TIMER.enabled = False
 
 
+def pmc_traffic(name, B):
+    """HBM bytes per launch of kernel `name` at batch B from profiles/traffic.json (rocprofv3 --pmc
+    FETCH_SIZE x2 + WRITE_SIZE, tools/pmc.sh + tools/pmc_summary.py), or None if not collected."""
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        return json.load(open(tpath)).get(name, {}).get(str(B))
+    except (OSError, ValueError):
+        return None
+
+
 def roofline_from(kern, B):
     conv = {k: v for k, v in kern.items() if k.startswith("conv2_")}
     if not conv:
@@ -145,13 +155,7 @@ def roofline_from(kern, B):
     flops = WINO_FLOP_PER_SAMPLE[name] * B
     ach = flops / (conv[name]["avg_ms"] * 1e-3) / 1e12
     direct_eq = CONV2_FLOP_PER_SAMPLE * B / (conv[name]["avg_ms"] * 1e-3) / 1e12
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get(name, {}).get(str(B))
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(name, B)
     return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": flops, "avg_ms": round(conv[name]["avg_ms"], 4),
@@ -214,7 +218,7 @@ def run_wide(args, B, steps, warmup, kernel_pass_on=True):
         name = max(conv, key=lambda k: conv[k]["avg_ms"])
         ach = WIDE_CONV_FLOP[name] * B / (conv[name]["avg_ms"] * 1e-3) / 1e12
         r["roofline"] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(name, B),
                          "flop_per_launch": WIDE_CONV_FLOP[name] * B, "avg_ms": round(conv[name]["avg_ms"], 4)}
         r["conv_tflops"] = {k: round(WIDE_CONV_FLOP[k] * B / (v["avg_ms"] * 1e-3) / 1e12, 1) for k, v in conv.items()}
     return r

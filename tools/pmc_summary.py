@@ -44,11 +44,27 @@ for k, cs in vals.items():
 if args.traffic_out:
     names = {"conv2_fwd_pool_kernel": "conv2_fwd_pool", "conv2_dgrad_kernel": "conv2_dgrad",
              "conv2_wgrad_kernel": "conv2_wgrad", "conv1_fwd_kernel": "conv1_fwd",
-             "conv1_wgrad_kernel": "conv1_wgrad", "fc_head_kernel<7>": "fc_xent", "fc_wgrad_kernel": "fc_wgrad"}
+             "conv1_wgrad_kernel": "conv1_wgrad", "conv1_wgrad_kernel<true>": "conv1_wgrad",
+             "fc_head_kernel<7>": "fc_xent", "fc_wgrad_kernel": "fc_wgrad"}
     prev = json.load(open(args.traffic_out)) if os.path.exists(args.traffic_out) else {}
+    names.update({"conv2_fwd_pool_wino_kernel": "conv2_fwd_pool", "conv2_dgrad_wino_kernel": "conv2_dgrad",
+                  "conv2_wgrad_wino_kernel": "conv2_wgrad", "fc_head_kernel<8>": "fc_xent"})
+    # widened (K5) template instantiations -> bench.py's kernel names (csrc/slk_wide.hip:824-836, 1055)
+    wide = [("wide_conv32_kernel<Conv32Cfg<64, 128, 32", "wide_conv2_fwd"),
+            ("wide_conv_kernel<ConvCfg<64, 128, 32", "wide_conv2_fwd"),
+            ("wide_conv32_kernel<Conv32Cfg<128, 256, 16", "wide_conv3_fwd"),
+            ("wide_conv_kernel<ConvCfg<128, 256, 16", "wide_conv3_fwd"),
+            ("wide_conv32_kernel<Conv32Cfg<256, 128, 16", "wide_conv3_dgrad"),
+            ("wide_conv_kernel<ConvCfg<256, 128, 16", "wide_conv3_dgrad"),
+            ("wide_conv_kernel<ConvCfg<128, 64, 32", "wide_conv2_dgrad"),
+            ("wide_wgrad_kernel<WgCfg<64, 128, 32", "wide_conv2_wgrad"),
+            ("wide_wgrad_kernel<WgCfg<128, 256, 16", "wide_conv3_wgrad"),
+            ("wide_conv1_wgrad_kernel", "wide_conv1_wgrad"), ("wide_conv1_fwd_kernel", "wide_conv1_fwd"),
+            ("wide_unpool_kernel", "wide_unpool")]
     for k, m in out.items():
-        if k in names and "hbm_bytes_corrected" in m:
-            prev.setdefault(names[k], {})[str(args.batch)] = int(m["hbm_bytes_corrected"])
+        short = names.get(k) or next((v for pfx, v in wide if k.startswith(pfx)), None)
+        if short and "hbm_bytes_corrected" in m:
+            prev.setdefault(short, {})[str(args.batch)] = int(m["hbm_bytes_corrected"])
     prev["_note"] = ("HBM bytes per launch from rocprofv3 --pmc (separate FETCH_SIZE and WRITE_SIZE passes, "
                      "tools/pmc.sh); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts wide reads at half)")
     json.dump(prev, open(args.traffic_out, "w"), indent=1, sort_keys=True)
