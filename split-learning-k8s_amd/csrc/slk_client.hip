@@ -59,107 +59,113 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
     }
 }
 
-// conv1 weight gradient. Grid (ngroups of 16 samples, 8 channel groups of 4). Thread t owns pixels
-// t, t+256, t+512; per sample it loads its 3x3 input windows once and, for each of the block's 8
-// channels, the cut gradient and the activation (relu-bwd mask act > 0) as coalesced rows, keeping
-// 8 x 10 accumulators. A fixed-order block reduction writes the group's slab row
-// [dW1 c*9+tap (288) | db1 c (32)] (the client flat layout) for those 8 channels.
-// REMASK = true: the ReLU mask is recomputed from x, W1, b1 with conv1_fwd_kernel's exact FMA order
-// (s = fma chain over taps from 0, then + bias; act > 0 <=> s > 0), so act is never read: the kernel
-// moves 89.6 KB per sample instead of 176 KB. Valid whenever W1/b1 are the weights of the forward
-// (true inside a split step: the client's SGD comes after its backward).
 constexpr int C1W_G = 16;
 constexpr int C1W_CG = 4;
+// conv1 weight gradient (ReLU backward + dW1, db1). Grid (ngroups of 16 samples, 8 channel groups
+// of 4), 256 threads; each workgroup writes its group's slab row [dW1 c*9+tap (288) | db1 c (32)] (the
+// client flat layout) for its 4 channels after a fixed-order block reduction. The work of a group
+// (16 samples x 338 horizontal pixel PAIRS per channel plane; 26 is even, so a pair never straddles a
+// row) is flattened over the threads: item = (sample, pair). A pair's operands are float2 loads (cut
+// gradient of 4 channels, the 3x4 input window as 3 row loads) and every FMA is a v_pk_fma_f32 over
+// the two pixels: ~150 VALU instructions per pair x 4 channels instead of ~350 pixel-at-a-time.
+// REMASK = true: the ReLU mask is recomputed from x, W1, b1 with conv1_fwd_kernel's exact per-pixel
+// FMA order (fma over taps from 0, then + bias; act > 0 <=> s > 0), so act is never read (89.6 KB
+// moved per sample instead of 176 KB). Valid whenever W1/b1 are the weights of the forward (true
+// inside a split step: the client's SGD comes after its backward). REMASK = false reads act.
+// Both produce bit-identical slabs (same summation order; tested).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int C1W_PAIRS = A_PIX / 2;     // 338
+constexpr int C1W_PROW = A_HW / 2;       // 13 pairs per row
 template <bool REMASK>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ act,
-                                                          const float* __restrict__ W1,
-                                                          const float* __restrict__ b1,
-                                                          const float* __restrict__ gcut,
-                                                          float* __restrict__ slabs, int B) {
+                                                             const float* __restrict__ act,
+                                                             const float* __restrict__ W1,
+                                                             const float* __restrict__ b1,
+                                                             const float* __restrict__ gcut,
+                                                             float* __restrict__ slabs, int B) {
     __shared__ float red[4][C1W_CG * 10];
     const int grp = blockIdx.x;
     const int c0 = blockIdx.y * C1W_CG;
     const int tid = threadIdx.x;
     const int b0 = grp * C1W_G;
     const int nb = min(C1W_G, B - b0);
+    const int nitem = nb * C1W_PAIRS;
 
-    float acc[C1W_CG][10];
+    float w[C1W_CG][10];  // wave-uniform: scalar loads
+#pragma unroll
+    for (int c = 0; c < C1W_CG; ++c) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) w[c][k] = REMASK ? W1[(c0 + c) * 9 + k] : 0.f;
+        w[c][9] = REMASK ? b1[c0 + c] : 0.f;
+    }
+    f32x2 acc[C1W_CG][10];
 #pragma unroll
     for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
-        for (int k = 0; k < 10; ++k) acc[c][k] = 0.f;
-    // pixel slots: loads always use a clamped (valid) pixel; invalid slots are zeroed by `valid`
-    // (a per-load branch would make hipcc wait vmcnt(0) around every load)
-    int pix[C1F_PPT], xo[C1F_PPT];
-    float valid[C1F_PPT];
-#pragma unroll
-    for (int u = 0; u < C1F_PPT; ++u) {
-        const int p = tid + 256 * u;
-        const int pc = p < A_PIX ? p : A_PIX - 1;
-        pix[u] = pc;
-        valid[u] = p < A_PIX ? 1.f : 0.f;
-        xo[u] = (pc / A_HW) * IN_HW + pc % A_HW;
-    }
+        for (int k = 0; k < 10; ++k) acc[c][k] = f32x2{0.f, 0.f};
+
+    constexpr int U = 2;  // items in flight per thread
 #pragma unroll 1
-    for (int bl = 0; bl < nb; ++bl) {
-        const int bb = b0 + bl;
-        const float* xi = x + (size_t)bb * IN_HW * IN_HW;
-        const float* ab = act + ((size_t)bb * C1 + c0) * A_PIX;
-        const float* gb = gcut + ((size_t)bb * C1 + c0) * A_PIX;
-        // issue every load of this sample first, then pin them (an empty asm that "uses" each value
-        // keeps hipcc from sinking gv's load into a branch on av > 0 with a vmcnt(0) per element)
-        float gv[C1W_CG][C1F_PPT], av[C1W_CG][C1F_PPT];
+    for (int base = tid; base < nitem; base += 256 * U) {
+        f32x2 gv[U][C1W_CG], av[U][C1W_CG], xr[U][3][2];
+        bool ok[U];
 #pragma unroll
-        for (int c = 0; c < C1W_CG; ++c)
+        for (int u = 0; u < U; ++u) {
+            const int it0 = base + 256 * u;
+            ok[u] = it0 < nitem;
+            const int it = ok[u] ? it0 : nitem - 1;
+            const int sl = it / C1W_PAIRS, q = it - sl * C1W_PAIRS;
+            const int row = q / C1W_PROW, col = 2 * (q - row * C1W_PROW);
+            const int bb = b0 + sl;
+            const float* gb = gcut + ((size_t)bb * C1 + c0) * A_PIX + row * A_HW + col;
+            const float* xi = x + (size_t)bb * IN_HW * IN_HW + row * IN_HW + col;
 #pragma unroll
-            for (int u = 0; u < C1F_PPT; ++u) {
-                gv[c][u] = gb[c * A_PIX + pix[u]];
-                av[c][u] = REMASK ? 0.f : ab[c * A_PIX + pix[u]];
+            for (int c = 0; c < C1W_CG; ++c) gv[u][c] = *reinterpret_cast<const f32x2*>(gb + c * A_PIX);
+            if (!REMASK) {
+                const float* ab = act + ((size_t)bb * C1 + c0) * A_PIX + row * A_HW + col;
+#pragma unroll
+                for (int c = 0; c < C1W_CG; ++c) av[u][c] = *reinterpret_cast<const f32x2*>(ab + c * A_PIX);
             }
-        float xv[C1F_PPT][9];
 #pragma unroll
-        for (int u = 0; u < C1F_PPT; ++u)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) xv[u][k] = xi[xo[u] + (k / 3) * IN_HW + k % 3];
-#pragma unroll
-        for (int c = 0; c < C1W_CG; ++c)
-#pragma unroll
-            for (int u = 0; u < C1F_PPT; ++u) asm volatile("" : "+v"(gv[c][u]), "+v"(av[c][u]));
-        if (REMASK) {
-#pragma unroll
-            for (int c = 0; c < C1W_CG; ++c) {
-                const float* w = W1 + (c0 + c) * 9;
-#pragma unroll
-                for (int u = 0; u < C1F_PPT; ++u) {
-                    float t = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) t = fmaf(xv[u][k], w[k], t);
-                    av[c][u] = t + b1[c0 + c];
-                }
+            for (int r = 0; r < 3; ++r) {
+                xr[u][r][0] = *reinterpret_cast<const f32x2*>(xi + r * IN_HW);
+                xr[u][r][1] = *reinterpret_cast<const f32x2*>(xi + r * IN_HW + 2);
             }
         }
-        float gm[C1W_CG][C1F_PPT];
 #pragma unroll
-        for (int c = 0; c < C1W_CG; ++c)
+        for (int u = 0; u < U; ++u) {
+            f32x2 xp[9];  // tap (r, k) operand pair: pixels (col, col+1) -> x[row+r][col+k], x[row+r][col+1+k]
 #pragma unroll
-            for (int u = 0; u < C1F_PPT; ++u)
-                gm[c][u] = av[c][u] > 0.f ? gv[c][u] * valid[u] : 0.f;  // threshold_backward mask
-#pragma unroll
-        for (int c = 0; c < C1W_CG; ++c)
-#pragma unroll
-            for (int u = 0; u < C1F_PPT; ++u) {
-#pragma unroll
-                for (int k = 0; k < 9; ++k) acc[c][k] = fmaf(gm[c][u], xv[u][k], acc[c][k]);
-                acc[c][9] += gm[c][u];
+            for (int r = 0; r < 3; ++r) {
+                xp[3 * r + 0] = xr[u][r][0];
+                xp[3 * r + 1] = f32x2{xr[u][r][0].y, xr[u][r][1].x};
+                xp[3 * r + 2] = xr[u][r][1];
             }
+#pragma unroll
+            for (int c = 0; c < C1W_CG; ++c) {
+                f32x2 t = f32x2{0.f, 0.f};
+                if (REMASK) {
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) t = __builtin_elementwise_fma(xp[k], f32x2{w[c][k], w[c][k]}, t);
+                    t = t + f32x2{w[c][9], w[c][9]};
+                } else {
+                    t = av[u][c];
+                }
+                f32x2 gm;
+                gm.x = (ok[u] && t.x > 0.f) ? gv[u][c].x : 0.f;  // threshold_backward mask
+                gm.y = (ok[u] && t.y > 0.f) ? gv[u][c].y : 0.f;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc[c][k] = __builtin_elementwise_fma(gm, xp[k], acc[c][k]);
+                acc[c][9] = acc[c][9] + gm;
+            }
+        }
     }
     const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int c = 0; c < C1W_CG; ++c)
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
-            const float v = wave_sum(acc[c][k]);
+            const float v = wave_sum(acc[c][k].x + acc[c][k].y);
             if (lane == 0) red[wave][c * 10 + k] = v;
         }
     __syncthreads();

@@ -518,15 +518,27 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
 extern "C" int slk_conv2_wgrad_direct_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
 
 // ============================================================================ fc1 + cross-entropy
-// 8 samples per 512-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy
+// FC_S = 4 samples per 256-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy
 // fwd+bwd, 4 = fc input gradient (dpooled = dlogits @ W3). W3 (368 KB) is L2/MALL-resident and is
-// re-read once per 8 samples per phase; pooled is streamed from HBM once.
-constexpr int FC_S = 8;
-constexpr int FC_T = 512;
+// re-read once per FC_S samples per phase; pooled is streamed from HBM once. Measured at B = 4096
+// (tools/ablate.py, threads x samples): 512x8 0.106 ms (134 VGPRs: one workgroup per CU, two dispatch
+// rounds), 512x8 forced to 2/CU 0.087 (spills), 256x4 0.074, 512x4 0.087, 128x4 0.093, 256x2 0.116
+// (W3 re-reads double): 1024 four-wave workgroups all resident at once is the sweet spot.
+#ifndef SLK_FC_S
+#define SLK_FC_S 4
+#endif
+#ifndef SLK_FC_T
+#define SLK_FC_T 256
+#endif
+#ifndef SLK_FC_WPE
+#define SLK_FC_WPE 1
+#endif
+constexpr int FC_S = SLK_FC_S;
+constexpr int FC_T = SLK_FC_T;
 constexpr int FC_K4 = P_SAMPLE / 4;  // 2304
 
 template <int MODE>
-__global__ __launch_bounds__(FC_T) void fc_head_kernel(
+__global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
     const float* __restrict__ pooled, const float* __restrict__ W3, const float* __restrict__ b3,
     const int64_t* __restrict__ labels, float* __restrict__ logits, float* __restrict__ loss_i,
     float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B) {

@@ -20,7 +20,7 @@ libs = []
 for path in args.libs:
     L = ctypes.CDLL(path)
     for n in ("slk_conv2_fwd_pool", "slk_conv2_dgrad", "slk_conv2_wgrad", "slk_conv1_fwd", "slk_conv1_wgrad",
-              "slk_fc_xent", "slk_fc_wgrad"):
+              "slk_fc_xent", "slk_fc_wgrad", "slk_conv1_wgrad_remask"):
         getattr(L, n).restype = ctypes.c_int
     L.slk_conv2_wgrad_nslab.restype = ctypes.c_int
     L.slk_conv1_wgrad_nslab.restype = ctypes.c_int
@@ -76,6 +76,7 @@ def calls(L):
         "conv2_wgrad": lambda: L.slk_conv2_wgrad(p(act), p(dp), p(code), p(slabs), B, P(s)),
         "conv1_fwd": lambda: L.slk_conv1_fwd(p(x), p(W1), p(b1), p(act), B, P(s)),
         "conv1_wgrad": lambda: L.slk_conv1_wgrad(p(x), p(act), p(gcut), p(slabs), B, P(s)),
+        "conv1_wgrad_remask": lambda: L.slk_conv1_wgrad_remask(p(x), p(W1), p(b1), p(gcut), p(slabs), B, P(s)),
         "fc_wgrad": lambda: L.slk_fc_wgrad(p(dl), p(pooled), p(slabs), B, P(s)),
     }
 
