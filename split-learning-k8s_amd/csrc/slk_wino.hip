@@ -68,17 +68,23 @@ __device__ __forceinline__ void pk_wino_in(const f2 (&Rlo)[4], const f2 (&Rhi)[4
 
 // Y = A^T m A for two output channels at once (pairs = 2 accumulator rows r, r+1 of the same
 // (i,j)): y[q] for q = 00, 01, 10, 11.
+// a - b as ONE v_pk_add_f32 (hipcc splits a packed subtraction into two scalar v_sub_f32)
+__device__ __forceinline__ f2 pk_sub(f2 a, f2 b) {
+    f2 d;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
 __device__ __forceinline__ void pk_wino_out(const f2 (&m)[16], f2 (&y)[4]) {
     f2 s0[4], s1[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         s0[c] = (m[0 * 4 + c] + m[1 * 4 + c]) + m[2 * 4 + c];
-        s1[c] = (m[1 * 4 + c] - m[2 * 4 + c]) - m[3 * 4 + c];
+        s1[c] = pk_sub(pk_sub(m[1 * 4 + c], m[2 * 4 + c]), m[3 * 4 + c]);
     }
     y[0] = (s0[0] + s0[1]) + s0[2];
-    y[1] = (s0[1] - s0[2]) - s0[3];
+    y[1] = pk_sub(pk_sub(s0[1], s0[2]), s0[3]);
     y[2] = (s1[0] + s1[1]) + s1[2];
-    y[3] = (s1[1] - s1[2]) - s1[3];
+    y[3] = pk_sub(pk_sub(s1[1], s1[2]), s1[3]);
 }
 
 // ---------------------------------------------------------------- 4x4 transforms (in registers)
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
     }
 }
 
-extern "C" int slk_conv2_fwd_pool(const float* act, const float* W2, const float* b2, float* pooled,
+extern "C" int slk_conv2_fwd_pool_v1(const float* act, const float* W2, const float* b2, float* pooled,
                                   uint8_t* code, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
@@ -384,6 +390,173 @@ __device__ __forceinline__ void lds_patch_pk(const float* ps, f2 (&lo)[4], f2 (&
         lo[r] = *reinterpret_cast<const f2*>(ps + r * A_HW);
         hi[r] = *reinterpret_cast<const f2*>(ps + r * A_HW + 2);
     }
+}
+
+// ---------------------------------------------------------------------------- forward, v2
+// Same transform-domain GEMMs, but wave w owns 32 output channels (2 M blocks: co 32*(w&1) .. +31)
+// instead of 16, so one transformed input patch feeds 32 MFMAs instead of 16: the input transform
+// (16 packed adds + 8 ds_read_b64 per k step) is paid half as often per MFMA, and on gfx950 every
+// VALU instruction between f32 MFMAs costs its issue cycles (tools/ubench/fillers.hip). The two
+// wave pairs (w>>1) each run their own band stream (2 bands in flight per workgroup, 4 LDS buffers
+// = 135 KB); transformed filters of both M blocks stay AGPR-resident (256 AGPRs, the MFMA A operand).
+// The bias rides in the C operand of the first MFMA of transform position (1,1): A^T E11 A = all
+// ones, so it reaches all four outputs of the window with coefficient +1 (no bias adds in the
+// epilogue).
+__device__ __forceinline__ void mfma_ac(f32x4& acc, float a, float b, const f32x4& c) {
+#if SLK_ABL & 1
+    acc = c;
+    acc[0] += b;
+    asm volatile("" ::"a"(a));
+#else
+    asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=v"(acc) : "a"(a), "v"(b), "v"(c));
+#endif
+}
+
+__device__ __forceinline__ void wf2_dma_band(const float* __restrict__ act, int band, const float* dst, int half, int lane) {
+    const int b = band / 3, bs = band - 3 * (band / 3);
+    const float* src = act + (size_t)b * A_SAMPLE + bs * 8 * A_HW;
+    const uint32_t base = (uint32_t)(uintptr_t)dst;
+#pragma unroll 1
+    for (int c = half; c < WF_CHUNKS; c += 2) {
+        const int p = min(c * 64 + lane, WF_PIECES - 1);
+        const int ci = p / 65, k = p - 65 * (p / 65);
+        glds16(src + ci * A_PIX + 4 * k, __builtin_amdgcn_readfirstlane(base + c * 1024));
+    }
+}
+
+__global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino2_kernel(
+    const float* __restrict__ act, const float* __restrict__ W2, const float* __restrict__ b2,
+    float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
+    __shared__ __attribute__((aligned(16))) float smem[4 * WF_BSTR];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (buffer descriptors, DMA bases)
+    const int mh = wu & 1, pr = wu >> 1;
+    const int nband = 3 * B, nsu = (nband + 1) >> 1;
+    float* bufs = smem + 2 * pr * WF_BSTR;
+
+    int su = blockIdx.x;
+    if (2 * su + pr < nband) wf2_dma_band(act, 2 * su + pr, bufs, mh, lane);
+
+    // transformed filters (co = 32mh + 16m + li, ci = 4s + lk) and the bias of this lane's rows
+    float uw[2][8][16];
+    f32x4 bias4[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int co = 32 * mh + 16 * m + li;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const float* gp = W2 + (size_t)co * K2 + (4 * s + lk) * 9;
+            float g[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) g[k] = gp[k];
+            float u[16];
+            wino_filter(g, u);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(uw[m][s][k]) : "v"(u[k]));
+        }
+        const float* bp = b2 + 32 * mh + 16 * m + 4 * lk;  // (a view into the flat parameters: no
+        bias4[m] = f32x4{bp[0], bp[1], bp[2], bp[3]};        //  16-byte alignment assumed)
+    }
+    wg_wait_vmcnt<0>();  // first band + filters landed
+
+    int buf = 0;
+#pragma unroll 1
+    for (; su < nsu; su += gridDim.x) {
+        // this band landed: its DMA was issued before the previous band's 48 epilogue stores of this
+        // wave — and every wave is done reading the other buffers
+        wg_wait_vmcnt<48>();
+        lds_barrier();
+        const int nb = 2 * (su + gridDim.x) + pr;
+        if (nb < nband) wf2_dma_band(act, nb, bufs + (buf ^ 1) * WF_BSTR, mh, lane);
+        const int band = 2 * su + pr;
+        if (band < nband) {
+            const float* img = bufs + buf * WF_BSTR;
+            const int b = band / 3, bs = band - 3 * (band / 3);
+            const auto prs = __builtin_amdgcn_make_buffer_rsrc(pooled + (size_t)b * P_SAMPLE, 0, P_SAMPLE * 4, 0x00020000);
+            const auto crs = __builtin_amdgcn_make_buffer_rsrc(code + (size_t)b * P_SAMPLE, 0, P_SAMPLE, 0x00020000);
+#pragma unroll 1
+            for (int g = 0; g < 3; ++g) {
+                const int t = 48 * bs + 16 * g + li;  // tile = pooling window index
+                const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
+                const float* pp = img + lk * WF_CSTR + (2 * ty - 8 * bs) * A_HW + 2 * tx;
+                f32x4 acc[2][16];  // written first by the k step 0 MFMAs (C = 0, or the bias at (1,1))
+                f2 Rlo[4], Rhi[4];
+                lds_patch_pk(pp, Rlo, Rhi);
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    f2 v01[4], v23[4];
+                    pk_wino_in(Rlo, Rhi, v01, v23);
+                    if (s < 7) lds_patch_pk(pp + 4 * (s + 1) * WF_CSTR, Rlo, Rhi);  // under these MFMAs
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int m = 0; m < 2; ++m)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            if (s == 0) {
+                                mfma_a0(acc[m][4 * i + 0], uw[m][s][4 * i + 0], v01[i].x);
+                                if (i == 1) mfma_ac(acc[m][4 * i + 1], uw[m][s][4 * i + 1], v01[i].y, bias4[m]);
+                                else mfma_a0(acc[m][4 * i + 1], uw[m][s][4 * i + 1], v01[i].y);
+                                mfma_a0(acc[m][4 * i + 2], uw[m][s][4 * i + 2], v23[i].x);
+                                mfma_a0(acc[m][4 * i + 3], uw[m][s][4 * i + 3], v23[i].y);
+                            } else {
+                                mfma_a(acc[m][4 * i + 0], uw[m][s][4 * i + 0], v01[i].x);
+                                mfma_a(acc[m][4 * i + 1], uw[m][s][4 * i + 1], v01[i].y);
+                                mfma_a(acc[m][4 * i + 2], uw[m][s][4 * i + 2], v23[i].x);
+                                mfma_a(acc[m][4 * i + 3], uw[m][s][4 * i + 3], v23[i].y);
+                            }
+                        }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                mfma_drain();
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    // output transform, two rows (co = 32mh + 16m + 4lk + r, r = 2h, 2h+1) per packed op
+                    f2 z[2][4];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        f2 mm[16];
+#pragma unroll
+                        for (int ij = 0; ij < 16; ++ij) mm[ij] = h ? acc[m][ij].zw : acc[m][ij].xy;
+                        pk_wino_out(mm, z[h]);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int h = r >> 1;
+                        float yq[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) yq[q] = (r & 1) ? z[h][q].y : z[h][q].x;
+                        // max over the raw window, first max wins; = torch's relu-then-pool scan.
+                        // Branch-free (hipcc turns the ternary chain into exec-mask branches): the
+                        // max as v_max3 + v_max (no NaN-quieting copies), the index as selects.
+                        float mx;
+                        asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4"
+                            : "=&v"(mx) : "v"(yq[0]), "v"(yq[1]), "v"(yq[2]), "v"(yq[3]));
+                        int idx = yq[2] == mx ? 2 : 3;
+                        idx = yq[1] == mx ? 1 : idx;
+                        idx = yq[0] == mx ? 0 : idx;
+                        const bool pos = mx > 0.f;
+                        const int o = (32 * mh + 16 * m + 4 * lk + r) * P_WIN + t;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pos ? mx : 0.f), prs, 4 * o, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pos ? idx : CODE_NONE), crs, o, 0, 0);
+                    }
+                }
+            }
+        }
+        buf ^= 1;
+    }
+}
+
+extern "C" int slk_conv2_fwd_pool(const float* act, const float* W2, const float* b2, float* pooled,
+                                  uint8_t* code, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(act && W2 && b2 && pooled && code);
+    const int nsu = (3 * B + 1) / 2;
+    conv2_fwd_pool_wino2_kernel<<<nsu < WF_GRID ? nsu : WF_GRID, WF_THREADS, 0, slk_stream(stream)>>>(
+        act, W2, b2, pooled, code, B);
+    return slk_launch_status();
 }
 
 // Routing lookup tables, built once per workgroup in LDS (float4 entries, code c = 0..4):
@@ -452,17 +625,18 @@ __device__ __forceinline__ void wd_dma_sample(const float* __restrict__ dpool, c
 __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
     const float* __restrict__ dpool, const uint8_t* __restrict__ code, const float* __restrict__ W2,
     float* __restrict__ gcut, int B) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * WD_BSTR + 2 * WD_XCH + 32];
+    __shared__ __attribute__((aligned(16))) float smem[2 * WD_BSTR + 2 * WD_XCH + 40];
     float* xch = smem + 2 * WD_BSTR;
-    float* lut = xch + 2 * WD_XCH;  // EXP table, 5 float4
+    float* lut = xch + 2 * WD_XCH;  // EXP table, 5 float4, then 5 zero float4 (out-of-range windows)
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int kh = wave & 1, gs = wave >> 1;
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar branches on kh
+    const int kh = wu & 1, gs = wu >> 1;
 
     int b = blockIdx.x;
     if (b < B) wd_dma_sample(dpool, code, b, smem, wave, lane);
-    if (tid < 20) lut[tid] = (tid >> 2) == (tid & 3) ? 1.f : 0.f;
+    if (tid < 40) lut[tid] = (tid < 20 && (tid >> 2) == (tid & 3)) ? 1.f : 0.f;
 
     // transformed flipped filters: lane (ci = 16m + li, co = 32kh + 4s + lk)
     float uw[2][8][16];
@@ -496,13 +670,15 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             const int tc = t < WD_NT ? t : WD_NT - 1;
             const int ty = tc / 13, tx = tc - 13 * (tc / 13);
             // windows (ty-1+wy, tx-1+wx), clamped in range; out-of-range ones use code 4 (zeros)
+            // (an out-of-range window reads the zero half of the table: no per-step select)
             int woff[4];
-            bool wok[4];
+            const float4* lutw[4];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const int py = ty - 1 + (w >> 1), px = tx - 1 + (w & 1);
-                wok[w] = py >= 0 && py < P_HW && px >= 0 && px < P_HW;
+                const bool ok = py >= 0 && py < P_HW && px >= 0 && px < P_HW;
                 woff[w] = min(max(py, 0), P_HW - 1) * P_HW + min(max(px, 0), P_HW - 1);
+                lutw[w] = reinterpret_cast<const float4*>(lut) + (ok ? 0 : 5);
             }
             f32x4 acc[2][16];  // written first by the C = 0 MFMAs of k step 0
 
@@ -515,16 +691,12 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                     v[w] = dps[s * 4 * P_WIN + woff[w]];
                     c[w] = cds[s * 4 * P_WIN + woff[w]];  // clamped address: always a valid read
                 }
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    c[w] = wok[w] ? c[w] : 4;
-                }
             };
             auto expand = [&](const float (&v)[4], const int (&c)[4], f2 (&v01)[4], f2 (&v23)[4]) {
                 f2 Rlo[4], Rhi[4];
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
-                    const float4 e = reinterpret_cast<const float4*>(lut)[c[w]];
+                    const float4 e = lutw[w][c[w]];
                     const f2 vv = {v[w], v[w]};
                     const f2 r0 = vv * f2{e.x, e.y}, r1 = vv * f2{e.z, e.w};
                     const int wy = w >> 1;
@@ -702,7 +874,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int mh = wave & 1, tp = wave >> 1;
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar branches on tp
+    const int mh = wu & 1, tp = wu >> 1;
     const int nunit = 3 * B;
 
     int u = blockIdx.x;
