@@ -635,7 +635,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
     const int kh = wu & 1, gs = wu >> 1;
 
     int b = blockIdx.x;
-    if (b < B) wd_dma_sample(dpool, code, b, smem, wave, lane);
+    if (b < B) wd_dma_sample(dpool, code, b, smem, wu, lane);
     if (tid < 40) lut[tid] = (tid < 20 && (tid >> 2) == (tid & 3)) ? 1.f : 0.f;
 
     // transformed flipped filters: lane (ci = 16m + li, co = 32kh + 4s + lk)
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
         wg_wait_vmcnt<8>();
         lds_barrier();
         const int nb = b + gridDim.x;
-        if (nb < B) wd_dma_sample(dpool, code, nb, smem + (buf ^ 1) * WD_BSTR, wave, lane);
+        if (nb < B) wd_dma_sample(dpool, code, nb, smem + (buf ^ 1) * WD_BSTR, wu, lane);
         const float* dps = smem + buf * WD_BSTR + (32 * kh + lk) * P_WIN;
         const uint8_t* cds = reinterpret_cast<const uint8_t*>(smem + buf * WD_BSTR + WD_CD_OFF) + (32 * kh + lk) * P_WIN;
         const auto grs = __builtin_amdgcn_make_buffer_rsrc(gcut + (size_t)b * A_SAMPLE, 0, A_SAMPLE * 4, 0x00020000);
@@ -692,11 +692,17 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                     c[w] = cds[s * 4 * P_WIN + woff[w]];  // clamped address: always a valid read
                 }
             };
-            auto expand = [&](const float (&v)[4], const int (&c)[4], f2 (&v01)[4], f2 (&v23)[4]) {
+            // table rows of a step's 4 windows: issued one step ahead (the code arrived a step
+            // earlier), so the dependent LDS read is not exposed in front of the expansion
+            auto lutload = [&](const int (&c)[4], float4 (&E)[4]) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) E[w] = lutw[w][c[w]];
+            };
+            auto expand = [&](const float (&v)[4], const float4 (&E)[4], f2 (&v01)[4], f2 (&v23)[4]) {
                 f2 Rlo[4], Rhi[4];
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
-                    const float4 e = lutw[w][c[w]];
+                    const float4 e = E[w];
                     const f2 vv = {v[w], v[w]};
                     const f2 r0 = vv * f2{e.x, e.y}, r1 = vv * f2{e.z, e.w};
                     const int wy = w >> 1;
@@ -708,10 +714,13 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             load(0, dv[0], cd[0]);
             load(1, dv[1], cd[1]);
             f2 v01[4], v23[4];
-            expand(dv[0], cd[0], v01, v23);
+            float4 E[4];
+            lutload(cd[0], E);
+            expand(dv[0], E, v01, v23);
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                if (s < 6) load(s + 2, dv[s & 1], cd[s & 1]);  // in flight under this step's MFMAs
+                if (s < 7) lutload(cd[(s + 1) & 1], E);        // in flight under this step's MFMAs
+                if (s < 6) load(s + 2, dv[s & 1], cd[s & 1]);  // likewise
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int m = 0; m < 2; ++m)
@@ -730,7 +739,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                         }
                     }
                 __builtin_amdgcn_sched_barrier(0);
-                if (s < 7) expand(dv[(s + 1) & 1], cd[(s + 1) & 1], v01, v23);
+                if (s < 7) expand(dv[(s + 1) & 1], E, v01, v23);
             }
             mfma_drain();
             // partial output transform (rows ci = 16m + 4lk + r, pairs r = 2h, 2h+1)
@@ -879,7 +888,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
     const int nunit = 3 * B;
 
     int u = blockIdx.x;
-    if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wave, lane);
+    if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wu, lane);
     if (tid < 5 * 16) {
         const int c = tid >> 4, i = (tid >> 2) & 3, j = tid & 3;
         const float ai = (c & 2) ? (i == 0 ? 0.f : (i == 1 ? 1.f : -1.f)) : (i == 3 ? 0.f : 1.f);
@@ -904,7 +913,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         wg_wait_vmcnt<0>();
         lds_barrier();
         const int nu = u + gridDim.x;
-        if (nu < nunit) ww_dma_unit(act, dpool, code, nu, smem + (buf ^ 1) * WW_BSTR, wave, lane);
+        if (nu < nunit) ww_dma_unit(act, dpool, code, nu, smem + (buf ^ 1) * WW_BSTR, wu, lane);
         const float* img = smem + buf * WW_BSTR;
         const float* dpb = img + WW_DP_OFF + (32 * mh + li) * WW_DSTR;
         const uint8_t* cdb = reinterpret_cast<const uint8_t*>(img + WW_CD_OFF) + (32 * mh + li) * WW_CSTR;
@@ -929,28 +938,40 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             }
         };
         f2 v01[2][4], v23[2][4], z01[2][4], z23[2][4];
-        auto xform = [&](const f2 (&lo)[2][4], const f2 (&hi)[2][4], const float (&v)[2], const int (&c)[2]) {
+        // ZT rows of a step's two windows, issued one step ahead (the codes arrived a step earlier)
+        // so the dependent LDS read is not exposed in front of the multiplies
+        auto zload = [&](const int (&c)[2], float4 (&E)[2][4]) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const float4* zt = reinterpret_cast<const float4*>(lutz) + 4 * c[m];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) E[m][i] = zt[i];
+            }
+        };
+        auto xform = [&](const f2 (&lo)[2][4], const f2 (&hi)[2][4], const float (&v)[2], const float4 (&E)[2][4]) {
             pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
             pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                const float4* zt = reinterpret_cast<const float4*>(lutz) + 4 * c[m];
                 const f2 vv = {v[m], v[m]};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float4 e = zt[i];
+                    const float4 e = E[m][i];
                     z01[m][i] = vv * f2{e.x, e.y};
                     z23[m][i] = vv * f2{e.z, e.w};
                 }
                 dbp[m] += z01[m][1].y;  // ZT[c][1][1] = 1 for a routed window, 0 for code 4
             }
         };
+        float4 E[2][4];
         load(0, Rlo[0], Rhi[0], dv[0], cd[0]);
         load(1, Rlo[1], Rhi[1], dv[1], cd[1]);
-        xform(Rlo[0], Rhi[0], dv[0], cd[0]);
+        zload(cd[0], E);
+        xform(Rlo[0], Rhi[0], dv[0], E);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
-            if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // under these MFMAs
+            if (j < 5) zload(cd[(j + 1) & 1], E);                                  // under these MFMAs
+            if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // likewise
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < 2; ++m)
@@ -964,7 +985,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
                         mfma_acc(acc[m][n][4 * i + 3], z23[m][i].y, v23[n][i].y);
                     }
             __builtin_amdgcn_sched_barrier(0);
-            if (j < 5) xform(Rlo[(j + 1) & 1], Rhi[(j + 1) & 1], dv[(j + 1) & 1], cd[(j + 1) & 1]);
+            if (j < 5) xform(Rlo[(j + 1) & 1], Rhi[(j + 1) & 1], dv[(j + 1) & 1], E);
         }
         buf ^= 1;
     }
