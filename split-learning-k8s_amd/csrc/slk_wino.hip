@@ -638,13 +638,14 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
     if (b < B) wd_dma_sample(dpool, code, b, smem, wu, lane);
     if (tid < 40) lut[tid] = (tid < 20 && (tid >> 2) == (tid & 3)) ? 1.f : 0.f;
 
-    // transformed flipped filters: lane (ci = 16m + li, co = 32kh + 4s + lk)
+    // transformed flipped filters: lane (ci = 16(m ^ kh) + li, co = 32kh + 4s + lk); slot m = 0 is the
+    // ci block this wave finishes, m = 1 the one it hands to its partner
     float uw[2][8][16];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            const float* gp = W2 + (size_t)(32 * kh + 4 * s + lk) * K2 + (16 * m + li) * 9;
+            const float* gp = W2 + (size_t)(32 * kh + 4 * s + lk) * K2 + (16 * (m ^ kh) + li) * 9;
             float g[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) g[k] = gp[8 - k];
@@ -742,7 +743,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                 if (s < 7) expand(dv[(s + 1) & 1], E, v01, v23);
             }
             mfma_drain();
-            // partial output transform (rows ci = 16m + 4lk + r, pairs r = 2h, 2h+1)
+            // partial output transform (rows ci = 16(m ^ kh) + 4lk + r, pairs r = 2h, 2h+1)
             f2 y[2][2][4];
 #pragma unroll
             for (int m = 0; m < 2; ++m)
@@ -760,14 +761,10 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             };
             float4* xw = reinterpret_cast<float4*>(xch + (p & 1) * WD_XCH) + (gs * 2 + kh) * 4 * 64 + lane;
             const float4* xr = reinterpret_cast<const float4*>(xch + (p & 1) * WD_XCH) + (gs * 2 + (kh ^ 1)) * 4 * 64 + lane;
-            // park the M block the partner finishes (kh = 0 finishes ci 0..15, kh = 1 ci 16..31)
-            if (kh == 0) {
+            // park the M block the partner finishes (slot 1 = ci block 1 - kh; kh = 0 finishes ci 0..15,
+            // kh = 1 ci 16..31 — slot 0 is always the wave's own block: no selects on kh)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[0], r);
-            }
+            for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
             lds_barrier();
             typedef unsigned int u2v __attribute__((ext_vector_type(2)));
             auto finish = [&](const f2 (&ym)[2][4], int mb) {
@@ -781,8 +778,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                     __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(tot.z), __float_as_uint(tot.w)}, grs, off + 4 * A_HW, 0, 0);
                 }
             };
-            if (kh == 0) finish(y[0], 0);
-            else finish(y[1], 1);
+            finish(y[0], kh);
         }
         buf ^= 1;
     }
@@ -925,10 +921,11 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         float dv[2][2];
         int cd[2][2];
         auto load = [&](int j, f2 (&lo)[2][4], f2 (&hi)[2][4], float (&v)[2], int (&c)[2]) {
+            // band-local tile tl = 12 qy + qx (< 48): patch at rows 2qy, cols 2qx of the band image,
+            // i.e. 2 tl + 28 qy floats; qy = tl / 12 = (43 tl) >> 9 exactly for tl < 128
             const int tl = 4 * (tp + 2 * j) + lk;
-            const int t = 48 * band + tl;
-            const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
-            const float* pa = img + li * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
+            const int qy = (tl * 43) >> 9;
+            const float* pa = img + li * WF_CSTR + 2 * tl + 28 * qy;
             lds_patch_pk(pa, lo[0], hi[0]);
             lds_patch_pk(pa + 16 * WF_CSTR, lo[1], hi[1]);
 #pragma unroll

@@ -23,7 +23,7 @@ x = x.to(dev)
 W1, b1 = a.conv1.weight.detach().to(dev), a.conv1.bias.detach().to(dev)
 W2, b2 = b.conv2.weight.detach().to(dev).contiguous(), b.conv2.bias.detach().to(dev)
 act = ops.conv1_fwd(x, W1, b1) if hasattr(ops, "conv1_fwd") else None
-lib = _lib.load()
+lib = _lib.load(os.environ["AB_LIB"]) if os.environ.get("AB_LIB") else _lib.load()
 st = torch.cuda.current_stream(dev)
 sp = ctypes.c_void_p(st.cuda_stream)
 P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -62,4 +62,5 @@ for k, v in times.items():
     ms = sorted(e0.elapsed_time(e1) for e0, e1 in v)
     out[k + "_ms_median"] = round(ms[len(ms) // 2], 4)
     out[k + "_ms_min"] = round(ms[0], 4)
+out["lib"] = os.environ.get("AB_LIB", "production")
 print(json.dumps(out))
