@@ -59,12 +59,13 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
     }
 }
 
-constexpr int C1W_G = 16;
+constexpr int C1W_NG = 96;  // sample ranges: x 8 channel groups = 768 workgroups = 3 per CU (occupancy 3)
 constexpr int C1W_CG = 4;
-// conv1 weight gradient (ReLU backward + dW1, db1). Grid (ngroups of 16 samples, 8 channel groups
-// of 4), 256 threads; each workgroup writes its group's slab row [dW1 c*9+tap (288) | db1 c (32)] (the
+// conv1 weight gradient (ReLU backward + dW1, db1). Grid (G = min(B, 96) contiguous sample ranges of
+// B/G (+-1) samples, 8 channel groups of 4) = one full wave of workgroups at occupancy 3 (no tail
+// round), 256 threads; each workgroup writes its group's slab row [dW1 c*9+tap (288) | db1 c (32)] (the
 // client flat layout) for its 4 channels after a fixed-order block reduction. The work of a group
-// (16 samples x 338 horizontal pixel PAIRS per channel plane; 26 is even, so a pair never straddles a
+// (B/G samples x 338 horizontal pixel PAIRS per channel plane; 26 is even, so a pair never straddles a
 // row) is flattened over the threads: item = (sample, pair). A pair's operands are float2 loads (cut
 // gradient of 4 channels, the 3x4 input window as 3 row loads) and every FMA is a v_pk_fma_f32 over
 // the two pixels: ~150 VALU instructions per pair x 4 channels instead of ~350 pixel-at-a-time.
@@ -87,8 +88,9 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
     const int grp = blockIdx.x;
     const int c0 = blockIdx.y * C1W_CG;
     const int tid = threadIdx.x;
-    const int b0 = grp * C1W_G;
-    const int nb = min(C1W_G, B - b0);
+    const int G = gridDim.x;
+    const int b0 = (int)((long long)grp * B / G);
+    const int nb = (int)((long long)(grp + 1) * B / G) - b0;
     const int nitem = nb * C1W_PAIRS;
 
     float w[C1W_CG][10];  // wave-uniform: scalar loads
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
     }
 }
 
-extern "C" int slk_conv1_wgrad_nslab(int B) { return B > 0 ? (B + C1W_G - 1) / C1W_G : 0; }
+extern "C" int slk_conv1_wgrad_nslab(int B) { return B > 0 ? (B < C1W_NG ? B : C1W_NG) : 0; }
 
 extern "C" int slk_conv1_fwd(const float* x, const float* W1, const float* b1, float* act, int B,
                              void* stream) {
