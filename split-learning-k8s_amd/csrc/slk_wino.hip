@@ -653,25 +653,47 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
         }
     wg_wait_vmcnt<0>();
 
-    int buf = 0;
+    // Rolling tile stream: this workgroup's samples k = 0 .. nloc-1 (b = blockIdx.x + k * gridDim.x)
+    // are one stream of 169-tile blocks; iteration i gives group slot gs the 16 tiles
+    // T = 32 i + 16 gs + li (a group may straddle two samples: a lane reads the buffer of ITS sample),
+    // so no group slot computes padding: ceil(169 nloc / 32) iterations instead of 6 nloc.
+    // Sample k lives in buffer k & 1; its DMA is issued once every tile of sample k - 2 is done (a
+    // whole iteration ahead of any use: >= 4 iterations, >= 32 stores of this wave, before it).
+    const int nloc = b < B ? (B - 1 - b) / (int)gridDim.x + 1 : 0;
+    if (nloc > 1) wd_dma_sample(dpool, code, b + gridDim.x, smem + WD_BSTR, wu, lane);
+    wg_wait_vmcnt<0>();  // samples 0 and 1 + filters landed
+    lds_barrier();
+    const int ntile = WD_NT * nloc;
+    const int nit = (ntile + 31) >> 5;
+    int next_dma = 2, resident = nloc > 1 ? 1 : 0;
 #pragma unroll 1
-    for (; b < B; b += gridDim.x) {
-        // this sample's staging has landed (its DMA preceded this wave's 48 stores of the previous
-        // sample) and every wave is done with the other buffer
-        wg_wait_vmcnt<8>();
-        lds_barrier();
-        const int nb = b + gridDim.x;
-        if (nb < B) wd_dma_sample(dpool, code, nb, smem + (buf ^ 1) * WD_BSTR, wu, lane);
-        const float* dps = smem + buf * WD_BSTR + (32 * kh + lk) * P_WIN;
-        const uint8_t* cds = reinterpret_cast<const uint8_t*>(smem + buf * WD_BSTR + WD_CD_OFF) + (32 * kh + lk) * P_WIN;
-        const auto grs = __builtin_amdgcn_make_buffer_rsrc(gcut + (size_t)b * A_SAMPLE, 0, A_SAMPLE * 4, 0x00020000);
-#pragma unroll 1
-        for (int p = 0; p < WD_PAIRS; ++p) {
-            const int t = 16 * (2 * p + gs) + li;
-            const int tc = t < WD_NT ? t : WD_NT - 1;
+    for (int it = 0; it < nit; ++it) {
+        // a new sample enters this iteration: its DMA (>= 32 stores of this wave ago) has landed
+        const int khi = min((32 * it + 31) / WD_NT, nloc - 1);
+        if (khi > resident) {
+            wg_wait_vmcnt<8>();
+            lds_barrier();
+            resident = khi;
+        }
+        // every tile before this iteration was read before the previous iteration's exchange
+        // barrier: sample next_dma - 2 is free once its last tile is behind us
+        if (next_dma < nloc && WD_NT * (next_dma - 1) <= 32 * it) {
+            wd_dma_sample(dpool, code, b + next_dma * (int)gridDim.x, smem + (next_dma & 1) * WD_BSTR, wu, lane);
+            ++next_dma;
+        }
+        const int p = it;
+        const int T = 32 * it + 16 * gs + li;
+        const bool valid = T < ntile;
+        const int Tc = valid ? T : ntile - 1;
+        const int k = Tc / WD_NT;
+        const int tc = Tc - WD_NT * k;
+        const float* dps = smem + (k & 1) * WD_BSTR + (32 * kh + lk) * P_WIN;
+        const uint8_t* cds = reinterpret_cast<const uint8_t*>(smem + (k & 1) * WD_BSTR + WD_CD_OFF) + (32 * kh + lk) * P_WIN;
+        float* gsm = gcut + (size_t)(b + k * (int)gridDim.x) * A_SAMPLE;
+        {
             const int ty = tc / 13, tx = tc - 13 * (tc / 13);
-            // windows (ty-1+wy, tx-1+wx), clamped in range; out-of-range ones use code 4 (zeros)
-            // (an out-of-range window reads the zero half of the table: no per-step select)
+            // windows (ty-1+wy, tx-1+wx), clamped in range; an out-of-range window reads the zero
+            // half of the table (no per-step select)
             int woff[4];
             const float4* lutw[4];
 #pragma unroll
@@ -766,21 +788,21 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
 #pragma unroll
             for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
             lds_barrier();
-            typedef unsigned int u2v __attribute__((ext_vector_type(2)));
             auto finish = [&](const f2 (&ym)[2][4], int mb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float4 a = row(ym, r), o = xr[r * 64];
                     const float4 tot = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
                     const int ci = 16 * mb + 4 * lk + r;
-                    const int off = t < WD_NT ? 4 * (ci * A_PIX + 2 * ty * A_HW + 2 * tx) : 0x7ffffff0;
-                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(tot.x), __float_as_uint(tot.y)}, grs, off, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(tot.z), __float_as_uint(tot.w)}, grs, off + 4 * A_HW, 0, 0);
+                    float* op = gsm + ci * A_PIX + 2 * ty * A_HW + 2 * tx;
+                    if (valid) {
+                        *reinterpret_cast<f2*>(op) = f2{tot.x, tot.y};
+                        *reinterpret_cast<f2*>(op + A_HW) = f2{tot.z, tot.w};
+                    }
                 }
             };
             finish(y[0], kh);
         }
-        buf ^= 1;
     }
 }
 

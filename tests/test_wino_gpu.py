@@ -74,3 +74,31 @@ def test_winograd_kernels_deterministic(gpu):
                      ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw)).clone()))
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [257, 300, 777])
+def test_winograd_multi_unit_per_workgroup(gpu, B):
+    """Batches past one unit per workgroup: the forward's two band streams per workgroup (odd band
+    count at B = 777), and dgrad's rolling 169-tile stream whose 32-tile iterations straddle
+    samples held in different LDS buffers (B = 257: one workgroup with 2 samples). Winograd vs direct
+    kernels on identical inputs."""
+    from splitcnn import ops
+    act, p, y = _inputs(gpu, B, seed=B)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    pd, cd = ops.conv2_fwd_pool(act, p["W2"], p["b2"], direct=True)
+    same = cw == cd
+    assert same.float().mean().item() > 0.9999
+    assert rel_err(pw[same].cpu().numpy(), pd[same].cpu().numpy()) <= 1e-5
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    gw = ops.conv2_dgrad(dp, cw, p["W2"])
+    gd = ops.conv2_dgrad(dp, cw, p["W2"], direct=True)
+    assert torch.isfinite(gw).all()
+    assert rel_err(gw.cpu().numpy(), gd.cpu().numpy()) <= 1e-5
+    # every sample's cut gradient individually (a misrouted straddling group would hit one sample)
+    num = (gw - gd).abs().flatten(1).max(dim=1).values
+    den = gd.abs().flatten(1).max(dim=1).values.clamp_min(1e-30)
+    assert (num / den).max().item() <= 1e-5
+    sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw))
+    sd = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, direct=True))
+    assert rel_err(sw[:18432].cpu().numpy(), sd[:18432].cpu().numpy()) <= 1e-5
+    assert rel_err(sw[18432:].cpu().numpy(), sd[18432:].cpu().numpy()) <= 1e-5
