@@ -260,6 +260,7 @@ def run_distributed(args, out, rank, world, local):
         raise ValueError(topology)
 
     fn, t, global_batch = build(topo)
+    progress(f"{topo} x{world}: timing {args.steps} steps")
     dt = timed(fn, args.steps, args.warmup, dev)
     out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
     out["config"] = {"workload": {"replicated": "K4-style SplitFed-V1: every GPU one client + one server "
@@ -290,6 +291,7 @@ def run_distributed(args, out, rank, world, local):
                 wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=wgrp, micro=args.micro)
                 wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
             Kw = max(3, min(args.steps, 10))
+            progress(f"widened hub x{world}: timing {Kw} steps")
             dtw = timed(wfn, Kw, 2, dev)
             Gw = (world - 1) * Bk
             out["widened_hub"] = {"workload": f"K5 SplitFed: {world - 1} client GPU(s) (widened conv stack, bf16) + "
@@ -305,7 +307,9 @@ def run_distributed(args, out, rank, world, local):
             ex = "pipeline" if world == 2 else "hub"
             fn2, t2, gb2 = build(ex)
             K2 = args.exchange_steps
+            progress(f"exchange phase ({ex}) x{world}: timing {K2} steps")
             dt2 = timed(fn2, K2, 2, dev)
+            progress("p2p peak")
             peak = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
             pk = torch.tensor([peak or 0.0], dtype=torch.float64, device=dev)
             dist.all_reduce(pk, op=dist.ReduceOp.MAX)
@@ -317,8 +321,17 @@ def run_distributed(args, out, rank, world, local):
             out["exchange"] = {"error": repr(e)[:300]}
 
 
+def progress(msg):
+    """Phase marker on stderr (long multi-rank runs stay visibly alive; stdout keeps the one JSON line)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
+    if os.environ.get("SLK_BENCH_TRACE_AFTER"):  # debugging aid: dump every thread's stack, then exit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["SLK_BENCH_TRACE_AFTER"]), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
