@@ -42,7 +42,7 @@ def test_argument_validation_without_gpu():
 def test_slab_counts_are_functions_of_batch_only():
     from splitcnn import ops
     assert ops.conv2_wgrad_nslab(4096) == 256 and ops.conv2_wgrad_nslab(3) == 9
-    assert ops.conv1_wgrad_nslab(4096) == 96 and ops.conv1_wgrad_nslab(50) == 50 and ops.conv1_wgrad_nslab(1) == 1
+    assert ops.conv1_wgrad_nslab(4096) == 128 and ops.conv1_wgrad_nslab(50) == 50 and ops.conv1_wgrad_nslab(1) == 1
     assert ops.fc_wgrad_nslab(4096) == 64 and ops.fc_wgrad_nslab(13) == 1
     assert ops.conv2_wgrad_nslab(0) == 0
 
