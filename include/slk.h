@@ -155,6 +155,17 @@ int slk_loss_sum(const float* values, int n, float scale, float* out, void* stre
 int slk_loss_log(const float* values, int n, float scale, float* ring, int capacity, int* counter,
                  void* stream);
 
+/* Every optimizer step of one split step in ONE launch: for each segment s < nseg (<= 4),
+ * slk_sgd_from_slabs(params[s], grads ? grads[s] : NULL, slabs[s], nslab[s], n[s], lr), and, when
+ * loss_values != NULL, slk_loss_log(loss_values, loss_n, loss_scale, ring, capacity, counter) —
+ * bit-identical to those separate launches. Replaces the server's optimizer.step() + log_metric
+ * (src/server_part.py:52,55) and the client's optimizer.step() (src/client_part.py:133) at the end
+ * of a fused split step. The pointer/size arrays are host memory. */
+int slk_sgd_multi_from_slabs(float* const* params, float* const* grads, const float* const* slabs,
+                             const int* nslab, const int* n, int nseg, float lr, const float* loss_values,
+                             int loss_n, float loss_scale, float* ring, int capacity, int* counter,
+                             void* stream);
+
 /* MNIST batch from the HBM-resident u8 dataset (replaces DataLoader(batch_size=64, shuffle=True)
  * over torchvision MNIST + ToTensor + Normalize((0.1307,),(0.3081,)), src/client_part.py:61-64,98):
  * x[s] = ((float)images[idx[s]] / 255 - mean) / std as f32 [B,1,28,28], y[s] = labels[idx[s]] (i64).

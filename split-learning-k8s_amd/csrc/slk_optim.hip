@@ -10,13 +10,12 @@
 // slabs w, w+16, w+32, ... of those columns in order (8 loads in flight), then wave 0 adds the 16
 // partials in wave order. The result is a fixed function of the inputs (no atomics).
 constexpr int RS_WAVES = 16;
-__global__ __launch_bounds__(1024) void sgd_from_slabs_kernel(float* __restrict__ param,
-                                                              float* __restrict__ grad,
-                                                              const float* __restrict__ slabs,
-                                                              int nslab, int n, float lr, int acc) {
+__device__ __forceinline__ void slab_reduce_sgd(float* __restrict__ param, float* __restrict__ grad,
+                                                const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                int acc, int blk) {
     __shared__ float part[RS_WAVES][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = blockIdx.x * 64 + lane;
+    const int i = blk * 64 + lane;
     float g = 0.f;
     if (i < n) {
         const float* s = slabs + i;
@@ -39,6 +38,13 @@ __global__ __launch_bounds__(1024) void sgd_from_slabs_kernel(float* __restrict_
         if (grad) grad[i] = t;
         if (param) param[i] = param[i] - lr * t;
     }
+}
+
+__global__ __launch_bounds__(1024) void sgd_from_slabs_kernel(float* __restrict__ param,
+                                                              float* __restrict__ grad,
+                                                              const float* __restrict__ slabs,
+                                                              int nslab, int n, float lr, int acc) {
+    slab_reduce_sgd(param, grad, slabs, nslab, n, lr, acc, blockIdx.x);
 }
 
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ param,
@@ -74,6 +80,64 @@ __global__ __launch_bounds__(256) void loss_log_kernel(const float* __restrict__
     }
 }
 
+// Every optimizer step of one split step in ONE launch (the last launches of the step are latency,
+// not bandwidth): block 0 (if loss_v) logs the loss, the next nblk0 blocks reduce + step segment 0,
+// the next nblk1 segment 1, .... Each block runs exactly the code of sgd_from_slabs_kernel /
+// loss_log_kernel on its slice, so the results are bit-identical to the separate launches.
+struct SgdSeg {
+    float* param;
+    float* grad;
+    const float* slabs;
+    int nslab, n, nblk;
+};
+constexpr int SGD_MAXSEG = 4;
+struct SgdMulti {
+    SgdSeg seg[SGD_MAXSEG];
+    int nseg;
+    float lr;
+    const float* loss_v;
+    int loss_n;
+    float loss_scale;
+    float* ring;
+    int capacity;
+    int* counter;
+};
+
+__global__ __launch_bounds__(1024) void sgd_multi_kernel(const SgdMulti a) {
+    int blk = blockIdx.x;
+    if (a.loss_v) {
+        // block 0 logs the loss (dispatched first: its serial sum overlaps the segments' blocks);
+        // threads 0..255 sum exactly as block_sum_256 (the other waves add nothing)
+        if (blk == 0) {
+            __shared__ float red[4];
+            float v = 0.f;
+            if (threadIdx.x < 256)
+                for (int i = threadIdx.x; i < a.loss_n; i += 256) v += a.loss_v[i];
+            v = wave_sum(v);
+            if (threadIdx.x < 256 && (threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const float tot = ((red[0] + red[1]) + red[2]) + red[3];
+                const int c = *a.counter;
+                a.ring[c % a.capacity] = tot * a.loss_scale;
+                *a.counter = c + 1;
+            }
+            return;
+        }
+        --blk;
+    }
+#pragma unroll
+    for (int s = 0; s < SGD_MAXSEG; ++s) {
+        if (s < a.nseg) {
+            if (blk < a.seg[s].nblk) {
+                slab_reduce_sgd(a.seg[s].param, a.seg[s].grad, a.seg[s].slabs, a.seg[s].nslab, a.seg[s].n, a.lr, 0, blk);
+                return;
+            }
+            blk -= a.seg[s].nblk;
+        }
+    }
+}
+
 static inline int grid_for(int n) {
     int g = (n + 255) / 256;
     return g > 2048 ? 2048 : (g < 1 ? 1 : g);
@@ -95,6 +159,33 @@ extern "C" int slk_sgd_from_slabs(float* param, float* grad, const float* slabs,
     if (n == 0) return 0;
     SLK_CHECK_ARG(param && (slabs || nslab == 0));
     sgd_from_slabs_kernel<<<(n + 63) / 64, 1024, 0, slk_stream(stream)>>>(param, grad, slabs, nslab, n, lr, 0);
+    return slk_launch_status();
+}
+
+extern "C" int slk_sgd_multi_from_slabs(float* const* params, float* const* grads, const float* const* slabs,
+                                        const int* nslab, const int* n, int nseg, float lr,
+                                        const float* loss_values, int loss_n, float loss_scale, float* ring,
+                                        int capacity, int* counter, void* stream) {
+    SLK_CHECK_ARG(nseg >= 0 && nseg <= SGD_MAXSEG && (nseg == 0 || (params && slabs && nslab && n)));
+    SLK_CHECK_ARG(!loss_values || (loss_n > 0 && capacity > 0 && ring && counter));
+    SgdMulti a{};
+    int nblk = 0;
+    for (int s = 0; s < nseg; ++s) {
+        SLK_CHECK_ARG(n[s] >= 0 && nslab[s] >= 0 && params[s] && (slabs[s] || nslab[s] == 0));
+        a.seg[s] = SgdSeg{params[s], grads ? grads[s] : nullptr, slabs[s], nslab[s], n[s], (n[s] + 63) / 64};
+        nblk += a.seg[s].nblk;
+    }
+    a.nseg = nseg;
+    a.lr = lr;
+    a.loss_v = loss_values;
+    a.loss_n = loss_n;
+    a.loss_scale = loss_scale;
+    a.ring = ring;
+    a.capacity = capacity;
+    a.counter = counter;
+    if (loss_values) ++nblk;
+    if (nblk == 0) return 0;
+    sgd_multi_kernel<<<nblk, 1024, 0, slk_stream(stream)>>>(a);
     return slk_launch_status();
 }
 

@@ -47,6 +47,7 @@ _SIGS = {
     "slk_sgd": [_P, _P, _I, _F, _P],
     "slk_loss_sum": [_P, _I, _F, _P, _P],
     "slk_loss_log": [_P, _I, _F, _P, _I, _P, _P],
+    "slk_sgd_multi_from_slabs": [_P, _P, _P, _P, _P, _I, _F, _P, _I, _F, _P, _I, _P, _P],
     "slk_mnist_batch": [_P, _P, _I, _P, _I, _F, _F, _P, _P, _P, _P],
     # widened split CNN (BASELINE config 5)
     "slk_wide_conv1_fwd": [_P, _P, _P, _P, _I, _P],

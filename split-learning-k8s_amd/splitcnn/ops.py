@@ -7,6 +7,8 @@ Nothing here synchronises, so a sequence of these calls can be captured in a HIP
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -209,6 +211,38 @@ def sgd_from_slabs(param, grad, slabs, lr):
     gptr = _dev(grad, "grad", (n,)) if grad is not None else None
     _lib.call("slk_sgd_from_slabs", param.data_ptr(), gptr, _dev(slabs, "slabs"), nslab, n, float(lr),
               _stream(param))
+
+
+def sgd_multi_from_slabs(segments, lr, loss=None):
+    """ONE launch for every optimizer step of a split step: for each (param, grad, slabs) in
+    `segments` (<= 4) sgd_from_slabs(param, grad, slabs, lr), plus loss_log(*loss) when
+    loss = (values, scale, ring, counter) — bit-identical to the separate launches."""
+    k = len(segments)
+    if not 0 <= k <= 4:
+        raise ValueError("sgd_multi_from_slabs: at most 4 segments")
+    P = ctypes.c_void_p
+    params, grads, slabs = (P * 4)(), (P * 4)(), (P * 4)()
+    nslab, ns = (ctypes.c_int * 4)(), (ctypes.c_int * 4)()
+    stream_of = None
+    for i, (param, grad, sl) in enumerate(segments):
+        nsl, n = sl.shape
+        params[i] = _dev(param, "param", (n,))
+        grads[i] = _dev(grad, "grad", (n,)) if grad is not None else None
+        slabs[i] = _dev(sl, "slabs")
+        nslab[i], ns[i] = nsl, n
+        stream_of = param if stream_of is None else stream_of
+    lv, ln, lsc, ring, cap, ctr = None, 0, 0.0, None, 0, None
+    if loss is not None:
+        values, lsc, ring_t, counter = loss
+        lv, ln = _dev(values, "values"), values.numel()
+        ring, cap = _dev(ring_t, "ring"), ring_t.numel()
+        ctr = _dev(counter, "counter", (1,), torch.int32)
+        stream_of = values if stream_of is None else stream_of
+    if stream_of is None:
+        return
+    cast = lambda a: ctypes.cast(a, P)  # noqa: E731
+    _lib.call("slk_sgd_multi_from_slabs", cast(params), cast(grads), cast(slabs), cast(nslab), cast(ns), k,
+              float(lr), lv, ln, float(lsc), ring, cap, ctr, _stream(stream_of))
 
 
 def sgd(param, grad, lr):

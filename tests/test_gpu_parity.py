@@ -287,3 +287,29 @@ def test_conv1_wgrad_remask_bit_identical_to_act_mask(gpu):
         s_act = ops.conv1_wgrad_slabs(x, act, g)
         s_rm = ops.conv1_wgrad_remask_slabs(x, W1, b1, g)
         assert torch.equal(s_act, s_rm), B
+
+
+def test_sgd_multi_bit_identical_to_separate_launches():
+    """slk_sgd_multi_from_slabs (every optimizer step + the loss log of a server step in one launch,
+    as ServerStage.step_request uses it) == slk_sgd_from_slabs per segment + slk_loss_log, bit for bit."""
+    from splitcnn import ops
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(5)
+    shapes = [(128, 320), (256, 18496), (64, 92170)]
+    slabs = [torch.randn(s, device=dev, generator=g) for s in shapes]
+    params = [torch.randn(s[1], device=dev, generator=g) for s in shapes]
+    loss_i = torch.rand(4093, device=dev, generator=g)
+    ref_p = [p.clone() for p in params]
+    ref_g = [torch.empty_like(p) for p in params]
+    ring_a, ring_b = torch.zeros(8, device=dev), torch.zeros(8, device=dev)
+    ctr_a, ctr_b = torch.full((1,), 3, dtype=torch.int32, device=dev), torch.full((1,), 3, dtype=torch.int32, device=dev)
+    for p, gr, s in zip(ref_p, ref_g, slabs):
+        ops.sgd_from_slabs(p, gr, s, 0.01)
+    ops.loss_log(loss_i, 1.0 / 4093, ring_a, ctr_a)
+    new_p = [p.clone() for p in params]
+    new_g = [torch.empty_like(p) for p in params]
+    ops.sgd_multi_from_slabs(list(zip(new_p, new_g, slabs)), 0.01, loss=(loss_i, 1.0 / 4093, ring_b, ctr_b))
+    torch.cuda.synchronize()
+    for a, b in zip(ref_p + ref_g, new_p + new_g):
+        assert torch.equal(a, b)
+    assert torch.equal(ring_a, ring_b) and int(ctr_b.item()) == 4
