@@ -70,7 +70,10 @@ __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restri
 #define SLK_C1W_U 1
 #endif
 constexpr int C1W_NG = SLK_C1W_NG;  // sample ranges: x 8 channel groups = 1024 workgroups = 4 per CU
-constexpr int C1W_CG = 4;
+#ifndef SLK_C1W_CG
+#define SLK_C1W_CG 4
+#endif
+constexpr int C1W_CG = SLK_C1W_CG;
 // conv1 weight gradient (ReLU backward + dW1, db1). Grid (G = min(B, 128) contiguous sample ranges of
 // B/G (+-1) samples, 8 channel groups of 4) = one round of workgroups (no tail round), 256 threads,
 // one item per thread in flight (measured at B = 4096, tools/ablate.py: G = 128 / 1 item 0.077 ms,
