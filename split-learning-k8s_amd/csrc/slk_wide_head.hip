@@ -130,12 +130,28 @@ __global__ __launch_bounds__(256) void wide_head_ce_kernel(const float* __restri
                                                            float* __restrict__ dlogits, int* __restrict__ err_flag, int B) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= B) return;
+    // partials of this sample: 32 x 10 contiguous floats, read 8 partials (20 float4) at a time so
+    // the loads are in flight together; summed per logit in partial order q = 0..31 from 0, then + bias
     float z[NC], m = -__builtin_inff();
 #pragma unroll
+    for (int j = 0; j < NC; ++j) z[j] = 0.f;
+    const float4* p4 = reinterpret_cast<const float4*>(part + (size_t)b * HPART * NC);
+#pragma unroll
+    for (int q0 = 0; q0 < HPART; q0 += 8) {
+        float pv[8 * NC];
+#pragma unroll
+        for (int i = 0; i < 2 * NC; ++i) {
+            const float4 t = p4[q0 * NC / 4 + i];
+            pv[4 * i] = t.x; pv[4 * i + 1] = t.y; pv[4 * i + 2] = t.z; pv[4 * i + 3] = t.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int j = 0; j < NC; ++j) z[j] += pv[q * NC + j];
+    }
+#pragma unroll
     for (int j = 0; j < NC; ++j) {
-        float v = 0.f;
-        for (int q = 0; q < HPART; ++q) v += part[((size_t)b * HPART + q) * NC + j];
-        z[j] = v + bf[j];
+        z[j] = z[j] + bf[j];
         m = fmaxf(m, z[j]);
     }
     float se = 0.f;
@@ -303,6 +319,7 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
                              float* slabs, float* work, int* err_flag, int b0, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && dcut &&
                   slabs && work);
+    SLK_CHECK_ARG(((uintptr_t)work & 15) == 0);  // the CE kernel reads the partials as float4
     if (B == 0) return 0;
     const int ng = slk_wide_head_nslab(B);
     hipStream_t st = slk_stream(stream);
