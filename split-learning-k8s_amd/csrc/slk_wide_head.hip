@@ -65,6 +65,11 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 constexpr int HSLICE = 8;            // 2048-feature slices (256 chunks each)
 constexpr int HSG = 64;              // samples per group
 constexpr int HPART = HSLICE * 4;    // partial logits per sample (slices x waves)
+#ifndef SLK_HSG_L
+#define SLK_HSG_L 32
+#endif
+constexpr int HSG_L = SLK_HSG_L;     // samples per group of the logits pass (no slab: free to differ;
+                                     // A/B via bench: 64 -> 0.193 ms head, 32 -> 0.177, 16 -> 0.175 but a slower step)
 
 __device__ __forceinline__ void load_w(const float* __restrict__ wf8, int fc, float (&w)[NC][8]) {
 #pragma unroll
@@ -99,10 +104,10 @@ __global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* _
     const uint32_t step = (uint32_t)*step_ptr;
     float w[NC][8];
     load_w(wf8, fc, w);
-    const int b1 = min(B, (grp + 1) * HSG);
-    uint4 vn = cut_chunk(cut, grp * HSG, fc, b1);
+    const int b1 = min(B, (grp + 1) * HSG_L);
+    uint4 vn = cut_chunk(cut, grp * HSG_L, fc, b1);
 #pragma unroll 1
-    for (int b = grp * HSG; b < b1; ++b) {
+    for (int b = grp * HSG_L; b < b1; ++b) {
         const uint4 v = vn;
         vn = cut_chunk(cut, b + 1, fc, b1);      // next sample's chunk in flight during this one
         float d[8];
@@ -323,7 +328,7 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
     if (B == 0) return 0;
     const int ng = slk_wide_head_nslab(B);
     hipStream_t st = slk_stream(stream);
-    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, step, seed,
+    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ((B + HSG_L - 1) / HSG_L)), dim3(256), 0, st, cut, wf8, step, seed,
                        keep_threshold, keep_scale, work, b0, B);
     hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + 255) / 256), dim3(256), 0, st, work, bf, labels, grad_scale,
                        logits, loss_i, dlogits, err_flag, B);
