@@ -1167,7 +1167,10 @@ __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __rest
 // buffered) and are read transposed (ds_read_b64_tr_b16); wave w takes row w of each block. Each
 // workgroup walks images blockIdx.x, +grid, ...; its 4 waves' partial sums are added in fixed order
 // into one slab [1792] = [dW1 (torch layout) | db1].
-constexpr int C1W_GRID = 256;
+#ifndef SLK_WC1W_GRID
+#define SLK_WC1W_GRID 512  // 2 workgroups per CU: twice the LDS-DMA bytes in flight (A/B: 0.182 -> 0.112 ms; 768: 0.112, 1024: 0.132)
+#endif
+constexpr int C1W_GRID = SLK_WC1W_GRID;
 constexpr int C1W_NPXP = 132;                                  // 128 px + 4 pad: plane stride 64 mod 256 B
 constexpr int C1W_BUF = 8 * C1W_NPXP * 16;                     // 16,896 B
 

@@ -63,7 +63,10 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 //   head_back   : same grid; per sample the cut gradient chunk (bf16) and the fc weight-gradient
 //                 accumulation (80 registers) -> one slab per sample group [dWf | dbf]
 constexpr int HSLICE = 8;            // 2048-feature slices (256 chunks each)
-constexpr int HSG = 64;              // samples per group
+#ifndef SLK_HSG
+#define SLK_HSG 64
+#endif
+constexpr int HSG = SLK_HSG;         // samples per group (= per fc weight-gradient slab)
 constexpr int HPART = HSLICE * 4;    // partial logits per sample (slices x waves)
 #ifndef SLK_HSG_L
 #define SLK_HSG_L 32
