@@ -71,6 +71,10 @@ constexpr int HPART = HSLICE * 4;    // partial logits per sample (slices x wave
 #ifndef SLK_HSG_L
 #define SLK_HSG_L 32
 #endif
+#ifndef SLK_HEAD_PF
+#define SLK_HEAD_PF 1
+#endif
+constexpr int HPF = SLK_HEAD_PF;     // samples' cut chunks in flight ahead of the one in use (A/B: 2 and 4 no gain)
 constexpr int HSG_L = SLK_HSG_L;     // samples per group of the logits pass (no slab: free to differ;
                                      // A/B via bench: 64 -> 0.193 ms head, 32 -> 0.177, 16 -> 0.175 but a slower step)
 
@@ -108,11 +112,15 @@ __global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* _
     float w[NC][8];
     load_w(wf8, fc, w);
     const int b1 = min(B, (grp + 1) * HSG_L);
-    uint4 vn = cut_chunk(cut, grp * HSG_L, fc, b1);
+    uint4 ring[HPF];
+#pragma unroll
+    for (int i = 0; i < HPF; ++i) ring[i] = cut_chunk(cut, grp * HSG_L + i, fc, b1);
 #pragma unroll 1
     for (int b = grp * HSG_L; b < b1; ++b) {
-        const uint4 v = vn;
-        vn = cut_chunk(cut, b + 1, fc, b1);      // next sample's chunk in flight during this one
+        const uint4 v = ring[0];
+#pragma unroll
+        for (int i = 0; i + 1 < HPF; ++i) ring[i] = ring[i + 1];
+        ring[HPF - 1] = cut_chunk(cut, b + HPF, fc, b1);  // later samples' chunks in flight during this one
         float d[8];
         dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
         float pj[NC];
@@ -194,11 +202,15 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
         for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
     float accb = 0.f;
     const int b1 = min(B, (grp + 1) * HSG);
-    uint4 vn = cut_chunk(cut, grp * HSG, fc, b1);
+    uint4 ring[HPF];
+#pragma unroll
+    for (int i = 0; i < HPF; ++i) ring[i] = cut_chunk(cut, grp * HSG + i, fc, b1);
 #pragma unroll 1
     for (int b = grp * HSG; b < b1; ++b) {
-        const uint4 v = vn;
-        vn = cut_chunk(cut, b + 1, fc, b1);
+        const uint4 v = ring[0];
+#pragma unroll
+        for (int i = 0; i + 1 < HPF; ++i) ring[i] = ring[i + 1];
+        ring[HPF - 1] = cut_chunk(cut, b + HPF, fc, b1);
         float d[8];
         const uint32_t kb = dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
         const float* dl = dlogits + (size_t)b * NC;
