@@ -233,6 +233,14 @@ int slk_wide_conv1_wgrad_nslab(int B);
  * widened config (the north star's "fused SGD/Adam"). */
 int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab, int n,
                         float lr, float beta1, float beta2, float eps, const int* step, void* stream);
+
+/* slk_adam_from_slabs over nseg (<= 4) parameter segments, each with its own slab set, in ONE launch
+ * (bit-identical to the separate launches); grads may be NULL or hold NULL entries. The pointer and
+ * size arrays are host memory. Replaces the per-parameter loop of the client's optimizer.step()
+ * (torch.optim.Adam) for the widened model (src/client_part.py:133's call site). */
+int slk_adam_multi_from_slabs(float* const* params, float* const* grads, float* const* m, float* const* v,
+                              const float* const* slabs, const int* nslab, const int* n, int nseg, float lr,
+                              float beta1, float beta2, float eps, const int* step, void* stream);
 /* Rebuild the bf16 weight shadows from the f32 masters: w1b [64][32] (W1 rows, k >= 27 zero) and the
  * MFMA layouts of W2 [128,64,3,3] and W3 [256,128,3,3]. */
 int slk_wide_shadows(const float* W1, const float* W2, const float* W3, uint16_t* w1b, uint16_t* w2f, uint16_t* w2d,

@@ -247,14 +247,14 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
 //   m = m + (1-b1)(g - m)  [lerp]; v = v*b2 + (1-b2) g*g  [mul_ + addcmul_];
 //   p = p - (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)  [addcdiv_].
 constexpr int AD_WAVES = 16;
-__global__ __launch_bounds__(1024) void adam_from_slabs_kernel(float* __restrict__ param, float* __restrict__ grad,
-                                                               float* __restrict__ m_, float* __restrict__ v_,
-                                                               const float* __restrict__ slabs, int nslab, int n,
-                                                               float lr, float b1, float b2, float eps,
-                                                               const int* __restrict__ step_ptr) {
+__device__ __forceinline__ void adam_slab_block(float* __restrict__ param, float* __restrict__ grad,
+                                                float* __restrict__ m_, float* __restrict__ v_,
+                                                const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                float b1, float b2, float eps, const int* __restrict__ step_ptr,
+                                                int blk) {
     __shared__ float part[AD_WAVES][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = blockIdx.x * 64 + lane;
+    const int i = blk * 64 + lane;
     float g = 0.f;
     if (i < n) {
         const float* s = slabs + i;
@@ -286,6 +286,46 @@ __global__ __launch_bounds__(1024) void adam_from_slabs_kernel(float* __restrict
         param[i] = param[i] + (-step_size) * (m / denom);
         m_[i] = m;
         v_[i] = v;
+    }
+}
+
+__global__ __launch_bounds__(1024) void adam_from_slabs_kernel(float* __restrict__ param, float* __restrict__ grad,
+                                                               float* __restrict__ m_, float* __restrict__ v_,
+                                                               const float* __restrict__ slabs, int nslab, int n,
+                                                               float lr, float b1, float b2, float eps,
+                                                               const int* __restrict__ step_ptr) {
+    adam_slab_block(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blockIdx.x);
+}
+
+// Several parameter segments (each with its own slab set) in ONE launch: consecutive block ranges,
+// each running adam_from_slabs_kernel's code on its segment — bit-identical to separate launches.
+constexpr int AD_MAXSEG = 4;
+struct AdamSeg {
+    float* param;
+    float* grad;
+    float* m;
+    float* v;
+    const float* slabs;
+    int nslab, n, nblk;
+};
+struct AdamMulti {
+    AdamSeg seg[AD_MAXSEG];
+    int nseg;
+    float lr, b1, b2, eps;
+    const int* step;
+};
+__global__ __launch_bounds__(1024) void adam_multi_kernel(const AdamMulti a) {
+    int blk = blockIdx.x;
+#pragma unroll
+    for (int s = 0; s < AD_MAXSEG; ++s) {
+        if (s < a.nseg) {
+            const AdamSeg& g = a.seg[s];
+            if (blk < g.nblk) {
+                adam_slab_block(g.param, g.grad, g.m, g.v, g.slabs, g.nslab, g.n, a.lr, a.b1, a.b2, a.eps, a.step, blk);
+                return;
+            }
+            blk -= g.nblk;
+        }
     }
 }
 
@@ -358,6 +398,29 @@ extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v
     if (n == 0) return 0;
     hipLaunchKernelGGL(adam_from_slabs_kernel, dim3((n + 63) / 64), dim3(1024), 0, slk_stream(stream), param, grad, m, v,
                        slabs, nslab, n, lr, beta1, beta2, eps, step);
+    return slk_launch_status();
+}
+extern "C" int slk_adam_multi_from_slabs(float* const* params, float* const* grads, float* const* m, float* const* v,
+                                         const float* const* slabs, const int* nslab, const int* n, int nseg,
+                                         float lr, float beta1, float beta2, float eps, const int* step,
+                                         void* stream) {
+    SLK_CHECK_ARG(nseg >= 0 && nseg <= AD_MAXSEG && step);
+    SLK_CHECK_ARG(nseg == 0 || (params && m && v && slabs && nslab && n));
+    AdamMulti a{};
+    int nblk = 0;
+    for (int s = 0; s < nseg; ++s) {
+        SLK_CHECK_ARG(params[s] && m[s] && v[s] && slabs[s] && nslab[s] > 0 && n[s] >= 0);
+        a.seg[s] = AdamSeg{params[s], grads ? grads[s] : nullptr, m[s], v[s], slabs[s], nslab[s], n[s], (n[s] + 63) / 64};
+        nblk += a.seg[s].nblk;
+    }
+    a.nseg = nseg;
+    a.lr = lr;
+    a.b1 = beta1;
+    a.b2 = beta2;
+    a.eps = eps;
+    a.step = step;
+    if (nblk == 0) return 0;
+    hipLaunchKernelGGL(adam_multi_kernel, dim3(nblk), dim3(1024), 0, slk_stream(stream), a);
     return slk_launch_status();
 }
 extern "C" int slk_wide_shadows(const float* W1, const float* W2, const float* W3, uint16_t* w1b, uint16_t* w2f,

@@ -66,6 +66,7 @@ _SIGS = {
     "slk_wide_conv1_wgrad": [_P, _P, _P, _I, _P],
     "slk_wide_conv1_wgrad_nslab": [_I],
     "slk_adam_from_slabs": [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _P, _P],
+    "slk_adam_multi_from_slabs": [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _P, _P],
     "slk_wide_shadows": [_P, _P, _P, _P, _P, _P, _P, _P, _P],
     "slk_wide_fc_shadow": [_P, _P, _P],
     "slk_tick": [_P, _P],

@@ -23,6 +23,7 @@ there is no CPU path. Activations live in HBM in the C8 layout [B][C/8][H][W][8]
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Optional
 
@@ -174,6 +175,7 @@ class WideClientStage:
         self.v = torch.zeros_like(self.params)
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.lr, self.betas, self.eps = lr, betas, eps
+        self.fuse_adam = True  # step_from_slabs: the three Adam segments in one launch
         self.w1b = torch.empty(64 * 32, dtype=_BF, device=self.device)
         self.w2f = torch.empty(73728, dtype=_BF, device=self.device)
         self.w2d = torch.empty(73728, dtype=_BF, device=self.device)
@@ -248,10 +250,22 @@ class WideClientStage:
                   self.step_ctr.data_ptr(), s)
 
     def step_from_slabs(self, s1, s2, s3):
-        """Adam on all client parameters from the three slab sets, then shadows + step counter."""
-        self._adam(0, 1792, s1)
-        self._adam(1792, 73856, s2)
-        self._adam(75648, 295168, s3)
+        """Adam on all client parameters from the three slab sets (ONE launch, bit-identical to one
+        slk_adam_from_slabs per set), then shadows + step counter."""
+        if self.fuse_adam:
+            P, I = ctypes.c_void_p, ctypes.c_int
+            segs = ((0, 1792, s1), (1792, 73856, s2), (75648, 295168, s3))
+            arr = lambda ts: ctypes.cast((P * 3)(*ts), P)  # noqa: E731
+            _k("adam_multi_from_slabs", arr([self.params[lo:].data_ptr() for lo, _, _ in segs]),
+               arr([self.grads[lo:].data_ptr() for lo, _, _ in segs]),
+               arr([self.m[lo:].data_ptr() for lo, _, _ in segs]), arr([self.v[lo:].data_ptr() for lo, _, _ in segs]),
+               arr([sl.data_ptr() for _, _, sl in segs]), ctypes.cast((I * 3)(*[sl.shape[0] for _, _, sl in segs]), P),
+               ctypes.cast((I * 3)(*[n for _, n, _ in segs]), P), 3, float(self.lr), float(self.betas[0]),
+               float(self.betas[1]), float(self.eps), self.step_ctr.data_ptr(), _stream(self.params))
+        else:
+            self._adam(0, 1792, s1)
+            self._adam(1792, 73856, s2)
+            self._adam(75648, 295168, s3)
         self.refresh_shadows()
         _k("tick", self.step_ctr.data_ptr(), _stream(self.params))
 

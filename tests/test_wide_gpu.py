@@ -268,3 +268,25 @@ def test_wide_hub_stage_interface_loopback(gpu):
         got = _np(stage.params)
         tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
         assert (np.abs(got - want) <= tol).all()
+
+
+def test_adam_multi_bit_identical_to_separate_launches():
+    """WideClientStage.step_from_slabs' single slk_adam_multi_from_slabs launch == one
+    slk_adam_from_slabs per slab set, bit for bit (params, grads, m, v)."""
+    from splitcnn.wide import WideClientStage, init_wide_models
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(11)
+    stages = []
+    for fuse in (True, False):
+        a, _ = init_wide_models(seed=0)
+        st = WideClientStage(a, device=dev)
+        st.fuse_adam = fuse
+        stages.append(st)
+    slabs = [torch.randn(n_s, n, device=dev, generator=g) * 1e-3 for n_s, n in ((7, 1792), (5, 73856), (3, 295168))]
+    for _ in range(2):  # two steps: the second reads m, v and the step counter the first wrote
+        for st in stages:
+            st.step_from_slabs(*slabs)
+    torch.cuda.synchronize()
+    for x, y in zip((stages[0].params, stages[0].grads, stages[0].m, stages[0].v),
+                    (stages[1].params, stages[1].grads, stages[1].m, stages[1].v)):
+        assert torch.equal(x, y)
