@@ -247,7 +247,13 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
 //   m = m + (1-b1)(g - m)  [lerp]; v = v*b2 + (1-b2) g*g  [mul_ + addcmul_];
 //   p = p - (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)  [addcdiv_].
 constexpr int AD_WAVES = 16;
-__device__ __forceinline__ void adam_slab_block(float* __restrict__ param, float* __restrict__ grad,
+// Few slabs (<= AD_COLS_MAX, the conv2/conv3/fc wgrad slab sets): thread = column, the slabs summed
+// in ascending order with 8 loads in flight, 1024 columns per block (coalesced rows); many slabs
+// (the conv1 set): 64 columns per block, 16 waves over the slab range, partials added in wave order.
+constexpr int AD_COLS_MAX = 64;
+__host__ __device__ constexpr int adam_cols_per_block(int nslab) { return nslab <= AD_COLS_MAX ? 1024 : 64; }
+
+__device__ __forceinline__ void adam_slab_block_rows(float* __restrict__ param, float* __restrict__ grad,
                                                 float* __restrict__ m_, float* __restrict__ v_,
                                                 const float* __restrict__ slabs, int nslab, int n, float lr,
                                                 float b1, float b2, float eps, const int* __restrict__ step_ptr,
@@ -287,6 +293,49 @@ __device__ __forceinline__ void adam_slab_block(float* __restrict__ param, float
         m_[i] = m;
         v_[i] = v;
     }
+}
+
+__device__ __forceinline__ void adam_slab_block_cols(float* __restrict__ param, float* __restrict__ grad,
+                                                     float* __restrict__ m_, float* __restrict__ v_,
+                                                     const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                     float b1, float b2, float eps, const int* __restrict__ step_ptr,
+                                                     int blk) {
+    const int i = blk * 1024 + threadIdx.x;
+    if (i >= n) return;
+    const float* s = slabs + i;
+    float t = 0.f;
+    int k = 0;
+    for (; k + 8 <= nslab; k += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(k + u) * n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t += v[u];
+    }
+    for (; k < nslab; ++k) t += s[(size_t)k * n];
+    if (grad) grad[i] = t;
+    const double tt = (double)(*step_ptr + 1);
+    const double bc1 = 1.0 - pow((double)b1, tt);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(1.0 - pow((double)b2, tt));
+    float m = m_[i], v = v_[i];
+    m = m + (1.f - b1) * (t - m);
+    v = v * b2 + t * t * (1.f - b2);
+    const float denom = sqrtf(v) / bc2s + eps;
+    param[i] = param[i] + (-step_size) * (m / denom);
+    m_[i] = m;
+    v_[i] = v;
+}
+
+__device__ __forceinline__ void adam_slab_block(float* __restrict__ param, float* __restrict__ grad,
+                                                float* __restrict__ m_, float* __restrict__ v_,
+                                                const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                float b1, float b2, float eps, const int* __restrict__ step_ptr,
+                                                int blk) {
+    if (adam_cols_per_block(nslab) == 1024)
+        adam_slab_block_cols(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blk);
+    else
+        adam_slab_block_rows(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blk);
 }
 
 __global__ __launch_bounds__(1024) void adam_from_slabs_kernel(float* __restrict__ param, float* __restrict__ grad,
@@ -396,7 +445,7 @@ extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v
                                    void* stream) {
     SLK_CHECK_ARG(param && m && v && slabs && step && nslab > 0 && n >= 0);
     if (n == 0) return 0;
-    hipLaunchKernelGGL(adam_from_slabs_kernel, dim3((n + 63) / 64), dim3(1024), 0, slk_stream(stream), param, grad, m, v,
+    hipLaunchKernelGGL(adam_from_slabs_kernel, dim3((n + adam_cols_per_block(nslab) - 1) / adam_cols_per_block(nslab)), dim3(1024), 0, slk_stream(stream), param, grad, m, v,
                        slabs, nslab, n, lr, beta1, beta2, eps, step);
     return slk_launch_status();
 }
@@ -410,7 +459,7 @@ extern "C" int slk_adam_multi_from_slabs(float* const* params, float* const* gra
     int nblk = 0;
     for (int s = 0; s < nseg; ++s) {
         SLK_CHECK_ARG(params[s] && m[s] && v[s] && slabs[s] && nslab[s] > 0 && n[s] >= 0);
-        a.seg[s] = AdamSeg{params[s], grads ? grads[s] : nullptr, m[s], v[s], slabs[s], nslab[s], n[s], (n[s] + 63) / 64};
+        a.seg[s] = AdamSeg{params[s], grads ? grads[s] : nullptr, m[s], v[s], slabs[s], nslab[s], n[s], (n[s] + adam_cols_per_block(nslab[s]) - 1) / adam_cols_per_block(nslab[s])};
         nblk += a.seg[s].nblk;
     }
     a.nseg = nseg;
