@@ -48,6 +48,9 @@ extern "C" {
 
 int slk_abi_version(void);
 const char* slk_error_string(int err);
+/* Hex sha256 of the sources this library was compiled from (csrc/*.hip, csrc/*.h, include/slk.h);
+ * splitcnn/_lib.py refuses a library whose id differs from the tree's. */
+const char* slk_build_id(void);
 
 /* ---------------------------------------------------------------- client stage (ModelPartA) */
 

@@ -251,6 +251,14 @@ extern "C" int slk_loss_log(const float* values, int n, float scale, float* ring
 
 extern "C" int slk_abi_version(void) { return SLK_ABI_VERSION; }
 
+// sha256 of the library's sources (splitcnn/build.py source_hash), baked in at compile time so the
+// loader can refuse a binary built from other sources; the tag is also searchable in the file.
+#ifndef SLK_BUILD_ID
+#define SLK_BUILD_ID "unknown"
+#endif
+extern "C" __attribute__((used, visibility("default"))) const char slk_build_id_tag[] = "SLK_BUILD_ID:" SLK_BUILD_ID;
+extern "C" const char* slk_build_id(void) { return slk_build_id_tag + 13; }
+
 extern "C" const char* slk_error_string(int err) {
     return hipGetErrorString(static_cast<hipError_t>(err));
 }

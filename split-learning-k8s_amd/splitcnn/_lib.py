@@ -12,7 +12,7 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before libslk.so)
 
-from .build import LIB_PATH
+from .build import CSRC_DIR, LIB_PATH, source_hash
 
 _c_float_p = ctypes.c_void_p  # device pointers travel as integers
 _P = ctypes.c_void_p
@@ -24,6 +24,7 @@ _U = ctypes.c_uint
 _SIGS = {
     "slk_abi_version": [],
     "slk_error_string": [_I],
+    "slk_build_id": [],
     "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],
     "slk_conv1_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv1_wgrad_nslab": [_I],
@@ -71,7 +72,7 @@ _SIGS = {
     "slk_wide_fc_shadow": [_P, _P, _P],
     "slk_tick": [_P, _P],
 }
-_RESTYPES = {"slk_error_string": ctypes.c_char_p}
+_RESTYPES = {"slk_error_string": ctypes.c_char_p, "slk_build_id": ctypes.c_char_p}
 
 SYMBOLS = tuple(_SIGS)
 
@@ -96,6 +97,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)  # AttributeError here means the .so does not match slk.h
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    # provenance: the library must have been built from exactly the sources in this tree
+    if os.path.isdir(CSRC_DIR):
+        built, want = lib.slk_build_id().decode(), source_hash()
+        if built != want:
+            raise ImportError(
+                f"splitcnn: {path} was built from other sources (build id {built[:12]}, tree {want[:12]}). "
+                "Rebuild it (python -c 'import __graft_entry__ as g; g.build()').")
     _lib = lib
     return lib
 

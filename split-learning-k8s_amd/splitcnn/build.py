@@ -6,7 +6,9 @@ GPU box (a JIT cache under ~/.cache would not). `python -m splitcnn.build` or
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -37,17 +39,40 @@ def _inputs():
     return srcs, hdrs
 
 
-def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return True
+def source_hash() -> str:
+    """sha256 over every input of the library (the HIP sources, csrc/*.h, include/slk.h), by name and
+    content. It is compiled into libslk.so (slk_build_id) so a binary can be tied to its sources."""
     srcs, hdrs = _inputs()
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(f) > t for f in srcs + hdrs)
+    h = hashlib.sha256()
+    for f in sorted(srcs + hdrs, key=os.path.basename):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+_TAG = re.compile(rb"SLK_BUILD_ID:([0-9a-f]{64})")
+
+
+def library_build_id(path: str = LIB_PATH):
+    """The source hash baked into a built library (read from the file, without loading it)."""
+    try:
+        with open(path, "rb") as fh:
+            m = _TAG.search(fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def needs_build() -> bool:
+    """True unless the library exists AND was built from exactly the current sources (hash, not mtime)."""
+    return library_build_id(LIB_PATH) != source_hash()
 
 
 def _compile_cmd(src: str, obj: str, defines) -> list:
     return [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE_DIR, *defines,
-            *EXTRA_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+            f'-DSLK_BUILD_ID="{source_hash()}"', *EXTRA_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
 
 
 def build_library(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:

@@ -174,18 +174,28 @@ class Hub:
         return t
 
     def client_step(self, x, y):
+        """Client k: forward each of `micro` micro-batches and send it (+ labels) while computing the
+        next; back-propagate each returned cut-gradient slice as it lands; all-reduce; SGD."""
         c = self.stage
-        B = x.shape[0]
+        B, m = x.shape[0], self.micro
+        assert B % m == 0, "batch must be divisible by the micro-batch count"
+        b = B // m
         act = self._buf("act", (B, 32, 26, 26), torch.float32, x.device)
-        c.forward(x, out=act)
         cut = self._buf("cut", (B, 32, 26, 26), torch.float32, x.device)
-        w1 = dist.isend(act, self.server_rank)
-        w2 = dist.isend(y, self.server_rank)
-        r = dist.irecv(cut, self.server_rank)
-        r.wait()
-        c.backward(cut, x=x, act=act)
-        w1.wait()
-        w2.wait()
+        sends, recvs = [], []
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            c.forward(x[sl], out=act[sl])
+            sends.append(dist.isend(act[sl], self.server_rank))
+            sends.append(dist.isend(y[sl], self.server_rank))
+        for k in range(m):
+            recvs.append(dist.irecv(cut[k * b:(k + 1) * b], self.server_rank))
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            recvs[k].wait()
+            c.backward(cut[sl], x=x[sl], act=act[sl], accumulate=k > 0)
+        for w in sends:
+            w.wait()
         if self.nclients > 1:
             dist.all_reduce(c.grads, group=self.client_group)
         c.step()
@@ -193,25 +203,30 @@ class Hub:
         self.global_step += 1
 
     def server_step(self, B: int, device):
-        """B = per-client batch; the server step covers (N-1)*B samples."""
+        """B = per-client batch; the server step covers (N-1)*B samples, consumed part by part in
+        (micro-batch, client) order as they arrive, gradient accumulated, ONE SGD step."""
         s = self.stage
-        G = self.nclients * B
+        m, nc = self.micro, self.nclients
+        b, G = B // m, nc * B
         acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
-        parts = self._buf("loss_parts", (self.nclients,), torch.float32, device)
-        recvs = []
-        for c in range(self.nclients):
-            sl = slice(c * B, (c + 1) * B)
-            recvs.append((dist.irecv(acts[sl], c), dist.irecv(labels[sl], c)))
-        sends = []
-        for c in range(self.nclients):
-            sl = slice(c * B, (c + 1) * B)
-            recvs[c][0].wait()
-            recvs[c][1].wait()
-            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=c > 0, cut_grad=cuts[sl])
-            _loss_sum(loss_i, 1.0 / G, parts[c:c + 1])
-            sends.append(dist.isend(cuts[sl], c))
+        parts = self._buf("loss_parts", (m * nc,), torch.float32, device)
+        reqs = {}
+        for c in range(nc):
+            for k in range(m):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                reqs[c, k] = (dist.irecv(acts[sl], c), dist.irecv(labels[sl], c))
+        sends, part = [], 0
+        for k in range(m):
+            for c in range(nc):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                for r in reqs[c, k]:
+                    r.wait()
+                _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=part > 0, cut_grad=cuts[sl])
+                _loss_sum(loss_i, 1.0 / G, parts[part:part + 1])
+                sends.append(dist.isend(cuts[sl], c))
+                part += 1
         s.step()
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:

@@ -84,16 +84,20 @@ def _flatten_params(params: List[nn.Parameter], device) -> Tuple[torch.Tensor, t
 
 
 class _Buffers:
-    """Per-batch-size scratch owned by a stage (allocated once, reused every step)."""
+    """Per-batch-size scratch owned by a stage (allocated once, reused every step).
+
+    Keyed by (name, shape, dtype, device): a buffer is never replaced, so a HIP graph captured at one
+    batch size keeps valid pointers after another size has run (a ragged loader alternates 64 / 32)."""
 
     def __init__(self):
         self._b = {}
 
     def get(self, name, shape, dtype, device):
-        t = self._b.get(name)
-        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != device:
+        key = (name, tuple(shape), dtype, torch.device(device))
+        t = self._b.get(key)
+        if t is None:
             t = torch.empty(shape, dtype=dtype, device=device)
-            self._b[name] = t
+            self._b[key] = t
         return t
 
 

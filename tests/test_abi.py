@@ -111,3 +111,12 @@ def test_forward_never_calls_torch_conv(monkeypatch):
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1, 28, 28))
     assert not called
+
+
+def test_library_build_id_matches_tree():
+    """Binary provenance: libslk.so carries the sha256 of the sources it was compiled from; the
+    loader refuses a library built from other sources, and needs_build() compares hashes."""
+    from splitcnn import _lib, build
+    lib = _lib.load()
+    assert lib.slk_build_id().decode() == build.source_hash() == build.library_build_id()
+    assert not build.needs_build()

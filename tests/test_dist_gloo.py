@@ -98,17 +98,18 @@ def _worker(rank, world, port, topo, outdir):
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"), dtype=torch.float64)
                 res = t.stage.named()
-        elif topo == "hub":
+        elif topo in ("hub", "hub_m2"):
             batches = _batches((world - 1) * B)
             grp = sd.client_group_for(world)
+            micro = 2 if topo == "hub_m2" else 1
             if rank < world - 1:
-                t = sd.Hub(OracleClient(P), rank, world, client_group=grp)
+                t = sd.Hub(OracleClient(P), rank, world, client_group=grp, micro=micro)
                 for x, y in batches:
                     sl = slice(rank * B, (rank + 1) * B)
                     t.client_step(x[sl].contiguous(), y[sl].contiguous())
                 res = t.stage.named()
             else:
-                t = sd.Hub(OracleServer(P), rank, world, client_group=grp)
+                t = sd.Hub(OracleServer(P), rank, world, client_group=grp, micro=micro)
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"))
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
@@ -146,7 +147,7 @@ def _reference(global_batch):
 
 
 @pytest.mark.parametrize("topo,world,gb", [("replicated", 2, 2 * B), ("pipeline", 2, B), ("hub", 3, 2 * B),
-                                           ("ushaped", 2, B)])
+                                           ("hub_m2", 4, 3 * B), ("ushaped", 2, B)])
 def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
     mp.spawn(_worker, args=(world, _port(), topo, str(tmp_path)), nprocs=world, join=True)
     P, losses = _reference(gb)
@@ -154,7 +155,7 @@ def test_topology_equals_single_process_step(tmp_path, topo, world, gb):
     if topo == "ushaped":   # labels, fc1 and the loss live on the client (rank 0)
         want = {0: ["W1", "b1", "W3", "b3", "losses"], 1: ["W2", "b2"]}
     else:
-        client_ranks = range(world) if topo == "replicated" else range(world - 1)
+        client_ranks = range(world) if topo == "replicated" else range(world - 1)  # hub: server = last
         server_ranks = range(world) if topo == "replicated" else [world - 1]
         want = {r: [] for r in range(world)}
         for r in client_ranks:

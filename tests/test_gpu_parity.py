@@ -313,3 +313,23 @@ def test_sgd_multi_bit_identical_to_separate_launches():
     for a, b in zip(ref_p + ref_g, new_p + new_g):
         assert torch.equal(a, b)
     assert torch.equal(ring_a, ring_b) and int(ctr_b.item()) == 4
+
+
+def test_graph_alternating_batch_sizes_equal_eager(gpu):
+    """A ragged loader alternates batch sizes (60000 % 64 = 32): one HIP graph per size, each with
+    its own scratch buffers (a graph must never replay into buffers another size replaced). Graph
+    replays of 64 / 32 / 64 / 32 / 64 must equal the eager steps bit for bit."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    data = SyntheticMNIST(7)
+    batches = [data.batch(B) for B in (64, 32, 64, 32, 64)]
+    results = []
+    for graph in (False, True):
+        tr = SplitTrainer(*init_models(seed=3), device=gpu, graph=graph)
+        for x, y in batches:
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        results.append((tr.client.params.cpu(), tr.server.params.cpu(), [l for _, l in tr.loss_log.flush()]))
+    assert torch.equal(results[0][0], results[1][0])
+    assert torch.equal(results[0][1], results[1][1])
+    assert results[0][2] == results[1][2]

@@ -290,3 +290,21 @@ def test_adam_multi_bit_identical_to_separate_launches():
     for x, y in zip((stages[0].params, stages[0].grads, stages[0].m, stages[0].v),
                     (stages[1].params, stages[1].grads, stages[1].m, stages[1].v)):
         assert torch.equal(x, y)
+
+
+def test_wide_graph_alternating_batch_sizes_equal_eager(gpu):
+    """WideTrainer: one HIP graph per batch size with its own scratch; 16 / 8 / 16 / 8 graph replays
+    equal the eager steps bit for bit (the dropout mask follows the device step counter in both)."""
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    data = SyntheticCIFAR(9)
+    batches = [data.batch(B) for B in (16, 8, 16, 8)]
+    results = []
+    for graph in (False, True):
+        tr = WideTrainer(*init_wide_models(seed=1), device=gpu, graph=graph)
+        for x, y in batches:
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        results.append((tr.client.params.cpu(), tr.server.params.cpu(), [l for _, l in tr.loss_log.flush()]))
+    assert torch.equal(results[0][0], results[1][0])
+    assert torch.equal(results[0][1], results[1][1])
+    assert results[0][2] == results[1][2]
