@@ -40,6 +40,47 @@ CLIENT_N = 320
 SERVER_N = 110666
 
 
+class _Staged:
+    """A gloo point-to-point op on a device tensor, staged through host memory. Gloo moves only host
+    buffers (the CPU protocol tests and the 1-GPU multi-rank rehearsal use it); RCCL ("nccl") moves
+    device memory directly over xGMI, so with it these helpers are plain isend/irecv."""
+
+    def __init__(self, work, host=None, dev=None):
+        self.work, self.host, self.dev = work, host, dev
+
+    def wait(self):
+        self.work.wait()
+        if self.dev is not None:
+            self.dev.copy_(self.host)   # ordered on the current stream, before any consumer
+        return True
+
+
+def _host_staged(t, group) -> bool:
+    return t.device.type == "cuda" and dist.get_backend(group) == "gloo"
+
+
+def isend(t, dst, group=None):
+    if _host_staged(t, group):
+        h = t.detach().to("cpu")        # waits for the producer on the current stream
+        return _Staged(dist.isend(h, dst, group=group), host=h)
+    return dist.isend(t, dst, group=group)
+
+
+def irecv(t, src, group=None):
+    if _host_staged(t, group):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        return _Staged(dist.irecv(h, src, group=group), host=h, dev=t)
+    return dist.irecv(t, src, group=group)
+
+
+def send(t, dst, group=None):
+    isend(t, dst, group).wait()
+
+
+def recv(t, src, group=None):
+    irecv(t, src, group).wait()
+
+
 def _loss_sum(values, scale, out):
     """scale*sum(values) -> out (the stage's own kernel when it has one)."""
     if values.device.type == "cuda":
@@ -105,11 +146,11 @@ class Pipeline:
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
             c.forward(x[sl], out=acts[sl])
-            sends.append(dist.isend(acts[sl], self.peer, group=self.group))
-            sends.append(dist.isend(y[sl], self.peer, group=self.group))
+            sends.append(isend(acts[sl], self.peer, group=self.group))
+            sends.append(isend(y[sl], self.peer, group=self.group))
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
-            recvs.append(dist.irecv(cuts[sl], self.peer, group=self.group))
+            recvs.append(irecv(cuts[sl], self.peer, group=self.group))
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
             recvs[k].wait()
@@ -131,8 +172,8 @@ class Pipeline:
         recvs = []
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
-            recvs.append((dist.irecv(acts[sl], self.peer, group=self.group),
-                          dist.irecv(labels[sl], self.peer, group=self.group)))
+            recvs.append((irecv(acts[sl], self.peer, group=self.group),
+                          irecv(labels[sl], self.peer, group=self.group)))
         sends = []
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
@@ -140,7 +181,7 @@ class Pipeline:
             recvs[k][1].wait()
             _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / B, accumulate=k > 0, cut_grad=cuts[sl])
             _loss_sum(loss_i, 1.0 / B, parts[k:k + 1])
-            sends.append(dist.isend(cuts[sl], self.peer, group=self.group))
+            sends.append(isend(cuts[sl], self.peer, group=self.group))
         s.step()
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:
@@ -186,10 +227,10 @@ class Hub:
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             c.forward(x[sl], out=act[sl])
-            sends.append(dist.isend(act[sl], self.server_rank))
-            sends.append(dist.isend(y[sl], self.server_rank))
+            sends.append(isend(act[sl], self.server_rank))
+            sends.append(isend(y[sl], self.server_rank))
         for k in range(m):
-            recvs.append(dist.irecv(cut[k * b:(k + 1) * b], self.server_rank))
+            recvs.append(irecv(cut[k * b:(k + 1) * b], self.server_rank))
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             recvs[k].wait()
@@ -216,7 +257,7 @@ class Hub:
         for c in range(nc):
             for k in range(m):
                 sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                reqs[c, k] = (dist.irecv(acts[sl], c), dist.irecv(labels[sl], c))
+                reqs[c, k] = (irecv(acts[sl], c), irecv(labels[sl], c))
         sends, part = [], 0
         for k in range(m):
             for c in range(nc):
@@ -225,7 +266,7 @@ class Hub:
                     r.wait()
                 _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=part > 0, cut_grad=cuts[sl])
                 _loss_sum(loss_i, 1.0 / G, parts[part:part + 1])
-                sends.append(dist.isend(cuts[sl], c))
+                sends.append(isend(cuts[sl], c))
                 part += 1
         s.step()
         s.log_loss(parts, scale=1.0, step=self.global_step)
@@ -309,13 +350,13 @@ class UShaped:
     def client_step(self, x, y):
         B, dev, c = x.shape[0], x.device, self.stage
         act = c.forward(x)
-        dist.send(act, self.peer, group=self.group)
+        send(act, self.peer, group=self.group)
         pooled = self._buf("pooled", (B, 64, 12, 12), act.dtype, dev)
-        dist.recv(pooled, self.peer, group=self.group)
+        recv(pooled, self.peer, group=self.group)
         dpooled = c.head_step(pooled, y, step=self.global_step)
-        dist.send(dpooled, self.peer, group=self.group)
+        send(dpooled, self.peer, group=self.group)
         cut = self._buf("cut", (B, 32, 26, 26), act.dtype, dev)
-        dist.recv(cut, self.peer, group=self.group)
+        recv(cut, self.peer, group=self.group)
         c.backward_step(cut)
         self.exchange_bytes = 2 * (act.numel() + pooled.numel()) * act.element_size()
         self.global_step += 1
@@ -323,13 +364,13 @@ class UShaped:
     def server_step(self, B: int, device, dtype=torch.float32):
         s = self.stage
         act = self._buf("act", (B, 32, 26, 26), dtype, device)
-        dist.recv(act, self.peer, group=self.group)
+        recv(act, self.peer, group=self.group)
         pooled = s.forward(act)
-        dist.send(pooled, self.peer, group=self.group)
+        send(pooled, self.peer, group=self.group)
         dpooled = self._buf("dpooled", (B, 64, 12, 12), dtype, device)
-        dist.recv(dpooled, self.peer, group=self.group)
+        recv(dpooled, self.peer, group=self.group)
         cut = s.backward_step(dpooled)
-        dist.send(cut, self.peer, group=self.group)
+        send(cut, self.peer, group=self.group)
         self.exchange_bytes = 2 * (act.numel() + pooled.numel()) * act.element_size()
         self.global_step += 1
 
@@ -373,10 +414,10 @@ class WideHub:
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             cut = c.forward(x[sl], tag=k)
-            sends.append(dist.isend(cut, self.server_rank))
-            sends.append(dist.isend(y[sl], self.server_rank))
+            sends.append(isend(cut, self.server_rank))
+            sends.append(isend(y[sl], self.server_rank))
         for k in range(m):
-            recvs.append(dist.irecv(dcut[k * b:(k + 1) * b], self.server_rank))
+            recvs.append(irecv(dcut[k * b:(k + 1) * b], self.server_rank))
         for k in range(m):
             recvs[k].wait()
             c.backward_grads(dcut[k * b:(k + 1) * b], tag=k, accumulate=k > 0)
@@ -400,7 +441,7 @@ class WideHub:
         for c in range(nc):
             for k in range(m):
                 sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                reqs[c, k] = (dist.irecv(cuts[sl], c), dist.irecv(labels[sl], c))
+                reqs[c, k] = (irecv(cuts[sl], c), irecv(labels[sl], c))
         sends, part = [], 0
         for k in range(m):
             for c in range(nc):
@@ -408,7 +449,7 @@ class WideHub:
                 for r in reqs[c, k]:
                     r.wait()
                 s.accumulate(cuts[sl], labels[sl], 1.0 / G, c * B + k * b, part, m * nc, dcut=dcuts[sl])
-                sends.append(dist.isend(dcuts[sl], c))
+                sends.append(isend(dcuts[sl], c))
                 part += 1
         s.finish_step(m * nc, step=self.global_step)
         for w in sends:
@@ -439,9 +480,9 @@ def measure_p2p(nbytes: int, src: int, dst: int, device, iters: int = 5, group=N
                 torch.cuda.synchronize(device)
             t0 = time.perf_counter()
         if rank == src:
-            dist.send(t, dst, group=group)
+            send(t, dst, group=group)
         elif rank == dst:
-            dist.recv(t, src, group=group)
+            recv(t, src, group=group)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
