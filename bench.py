@@ -8,11 +8,14 @@ fp32, the whole step (client fwd -> cut hand-off -> server fwd/CE/bwd/SGD -> cli
 replayed as one HIP graph. Inputs are resident in HBM before the timed region (a pool of batches,
 copied into the graph's static input buffers inside each step).
 
-N > 1: --topology replicated (default; SplitFed-V1: each rank one client + one server replica,
-one 444 KB gradient all-reduce per step, weak scaling), pipeline (N=2: client GPU <-> server GPU,
-micro-batched RCCL send/recv) or hub (N-1 client GPUs -> 1 server GPU). With the default topology
-a short second phase runs the exchange topology (pipeline at N=2, hub at N>=3) and reports the
-cut-exchange rate beside a measured RCCL p2p peak ("exchange" object).
+N > 1: `value` is --topology replicated (default: data-parallel SplitFed-V1 replicas, each rank one
+client + one server replica, one 444 KB gradient all-reduce per step, weak scaling — NOT one of
+BASELINE.json's configs, and labelled so). The BASELINE topologies follow as labelled objects:
+"k3_pipeline" (N = 2: client GPU <-> server GPU, micro-batched RCCL send/recv), "k4_hub" (N >= 3:
+N-1 client GPUs -> 1 server GPU on the reference cut) and "k5_splitfed" (the widened model's
+client-heavy cut on the same hub topology), each with its cut-exchange GB/s per link and direction
+against a measured RCCL p2p peak ("p2p_peak_GBps_measured") and the vendor link figure.
+--topology pipeline / hub makes that topology the headline instead.
 
 One JSON line on rank 0 with the driver's contract plus "roofline" (dominant kernel, measured live
 with HIP events on the launch stream in an eager pass after the timed region) and "cpu_baseline"
@@ -55,7 +58,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU (per-client) batch")
     ap.add_argument("--topology", default="auto", choices=["auto", "replicated", "pipeline", "hub"])
-    ap.add_argument("--micro", type=int, default=4, help="micro-batches for the pipeline topology")
+    ap.add_argument("--micro", type=int, default=4, help="micro-batches of the pipeline / hub topologies")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -224,7 +227,15 @@ def run_wide(args, B, steps, warmup, kernel_pass_on=True):
     return r
 
 
+XGMI_LINK_GBPS = 153.6   # vendor per-link xGMI figure (task brief: 7 links x ~153 GB/s per GPU); convention unstated
+
+
 def run_distributed(args, out, rank, world, local):
+    """N > 1. Headline `value`: data-parallel SplitFed-V1 replicas of the K2 step (linear weak scaling
+    by construction; NOT one of BASELINE.json's configs — labelled so). Then the BASELINE topologies,
+    each as its own labelled object: K3 = Pipeline (N = 2), K4 = Hub (N >= 3: N-1 client GPUs -> 1
+    server GPU), K5-SplitFed = WideHub (the widened, client-heavy cut), with cut-exchange GB/s per
+    direction against a measured RCCL p2p peak and the vendor link figure."""
     import torch
     import torch.distributed as dist
 
@@ -236,10 +247,9 @@ def run_distributed(args, out, rank, world, local):
     B = args.batch
     topo = args.topology if args.topology != "auto" else "replicated"
     X, Y = make_pool(B, 4, dev, seed=42 + rank)
-    a, b = init_models(seed=0)
-    grp = sd.client_group_for(world) if topo == "hub" or (topo == "replicated" and not args.no_exchange_phase) else None
+    grp = sd.client_group_for(world)   # every rank creates it (collective), used by hub topologies
 
-    def build(topology):
+    def build(topology, micro):
         a, b = init_models(seed=0)
         if topology == "replicated":
             t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev))
@@ -247,78 +257,102 @@ def run_distributed(args, out, rank, world, local):
         if topology == "pipeline":
             assert world == 2
             if rank == 0:
-                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=args.micro)
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
-            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=args.micro)
+            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro)
             return (lambda i: t.server_step(B, dev)), t, B
         if topology == "hub":
             if rank < world - 1:
-                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp)
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
-            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp)
+            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro)
             return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
         raise ValueError(topology)
 
-    fn, t, global_batch = build(topo)
+    labels = {
+        "replicated": "data-parallel SplitFed-V1 replicas (not a BASELINE config): every GPU hosts one client + "
+                      "one server replica of the reference split CNN, cut in place, one 444 KB gradient "
+                      "all-reduce per step (= the reference step at the concatenated N*B batch)",
+        "pipeline": "K3: 2xMI355X client-stage GPU <-> server-stage GPU, micro-batched RCCL send/recv of "
+                    "activations and cut gradients",
+        "hub": "K4: SplitFed, N-1 client GPUs feeding 1 server GPU (reference cut), micro-batched RCCL "
+               "send/recv, client-gradient all-reduce"}
+    fn, t, global_batch = build(topo, args.micro)
     progress(f"{topo} x{world}: timing {args.steps} steps")
     dt = timed(fn, args.steps, args.warmup, dev)
     out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
-    out["config"] = {"workload": {"replicated": "K4-style SplitFed-V1: every GPU one client + one server "
-                                                "replica, gradient all-reduce per step",
-                                  "pipeline": "K3: 2xMI355X client-stage/server-stage pipeline, micro-batched "
-                                              "RCCL send/recv",
-                                  "hub": "K4: SplitFed N-1 client GPUs + 1 server GPU, client all-reduce"}[topo],
-                     "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
-                     "parallelism": f"{topo}{world}"}
+    out["config"] = {"workload": labels[topo], "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
+                     "parallelism": f"{topo}{world}", "graph": False}
     out["scaling"] = "weak"
-    if topo in ("pipeline", "hub"):
-        out["exchange"] = {"topology": topo, "bytes_per_step": t.exchange_bytes,
-                           "GBps_effective": round(t.exchange_bytes / (dt / args.steps) / 1e9, 2)}
-    if not args.no_k5 and world >= 2:
+    if topo != "replicated":
+        out["config"]["micro_batches"] = args.micro
+        out["exchange"] = {"bytes_per_step_each_direction": B * CUT_BYTES * (1 if topo == "pipeline" else world - 1),
+                           "GBps_per_direction": round(t.exchange_bytes / 2 / (dt / args.steps) / 1e9, 2)}
+
+    peak = None
+    if not args.no_exchange_phase:
+        try:
+            progress("p2p peak")
+            p = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
+            pk = torch.tensor([p or 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+            peak = float(pk.item())
+            out["p2p_peak_GBps_measured"] = round(peak, 2)
+        except Exception as e:
+            out["p2p_peak_GBps_measured"] = {"error": repr(e)[:300]}
+    if topo == "replicated" and not args.no_exchange_phase:
+        # the BASELINE topology of this N on the reference cut
+        ex = "pipeline" if world == 2 else "hub"
+        key = "k3_pipeline" if world == 2 else "k4_hub"
+        try:
+            fn2, t2, gb2 = build(ex, args.micro)
+            K2 = args.exchange_steps
+            progress(f"{key} x{world}: timing {K2} steps")
+            dt2 = timed(fn2, K2, 2, dev)
+            per_dir = B * CUT_BYTES          # one client link, one direction, per step
+            gbps = per_dir / (dt2 / K2) / 1e9
+            r = {"workload": labels[ex], "samples_per_s": round(K2 * gb2 / dt2, 1), "ms_per_step": round(dt2 / K2 * 1e3, 3),
+                 "global_batch": gb2, "per_client_batch": B, "micro_batches": args.micro,
+                 "cut_bytes_per_link_per_direction_per_step": per_dir,
+                 "exchange_GBps_per_link_per_direction": round(gbps, 2),
+                 "exchange_frac_of_measured_p2p_peak": round(gbps / peak, 3) if peak else None,
+                 "exchange_frac_of_vendor_link": round(gbps / XGMI_LINK_GBPS, 3)}
+            if ex == "hub":
+                r["server_inbound_GBps_all_links"] = round(gbps * (world - 1), 2)
+            out[key] = r
+        except Exception as e:  # the headline number stands on its own
+            out[key] = {"error": repr(e)[:300]}
+    if not args.no_k5:
         # BASELINE config 5 SplitFed: N-1 client GPUs run the widened conv stack, GPU N-1 the head
         try:
             from splitcnn.wide import SyntheticCIFAR, WideClientStage, WideServerStage, init_wide_models
             Bk = args.k5_batch
-            wgrp = sd.client_group_for(world)
             wa, wb = init_wide_models(seed=0)
             if rank < world - 1:
                 data = SyntheticCIFAR(42 + rank)
                 xs, ys = zip(*(data.batch(Bk) for _ in range(2)))
                 WX, WY = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
-                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=wgrp, micro=args.micro)
+                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=grp, micro=args.micro)
                 wfn = lambda i: wt.client_step(WX[i % 2], WY[i % 2])  # noqa: E731
             else:
-                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=wgrp, micro=args.micro)
+                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=grp, micro=args.micro)
                 wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
             Kw = max(3, min(args.steps, 10))
-            progress(f"widened hub x{world}: timing {Kw} steps")
+            progress(f"k5_splitfed x{world}: timing {Kw} steps")
             dtw = timed(wfn, Kw, 2, dev)
             Gw = (world - 1) * Bk
-            out["widened_hub"] = {"workload": f"K5 SplitFed: {world - 1} client GPU(s) (widened conv stack, bf16) + "
-                                              f"1 server GPU (dropout/fc/CE head), {args.micro} micro-batches, "
-                                              "client all-reduce",
-                                  "samples_per_s": round(Kw * Gw / dtw, 1), "ms_per_step": round(dtw / Kw * 1e3, 3),
-                                  "global_batch": Gw, "exchange_bytes_per_step": wt.exchange_bytes,
-                                  "exchange_GBps_effective": round(wt.exchange_bytes / (dtw / Kw) / 1e9, 2)}
+            per_dir = Bk * 32768
+            gbps = per_dir / (dtw / Kw) / 1e9
+            out["k5_splitfed"] = {
+                "workload": f"K5 SplitFed: {world - 1} client GPU(s) (widened conv stack, bf16) + 1 server GPU "
+                            f"(dropout/fc/CE head), {args.micro} micro-batches, client all-reduce",
+                "samples_per_s": round(Kw * Gw / dtw, 1), "ms_per_step": round(dtw / Kw * 1e3, 3),
+                "global_batch": Gw, "per_client_batch": Bk,
+                "cut_bytes_per_link_per_direction_per_step": per_dir,
+                "exchange_GBps_per_link_per_direction": round(gbps, 2),
+                "exchange_frac_of_measured_p2p_peak": round(gbps / peak, 3) if peak else None}
         except Exception as e:
-            out["widened_hub"] = {"error": repr(e)[:300]}
-    if topo == "replicated" and not args.no_exchange_phase:
-        try:
-            ex = "pipeline" if world == 2 else "hub"
-            fn2, t2, gb2 = build(ex)
-            K2 = args.exchange_steps
-            progress(f"exchange phase ({ex}) x{world}: timing {K2} steps")
-            dt2 = timed(fn2, K2, 2, dev)
-            progress("p2p peak")
-            peak = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
-            pk = torch.tensor([peak or 0.0], dtype=torch.float64, device=dev)
-            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
-            out["exchange"] = {"topology": ex, "samples_per_s": round(K2 * gb2 / dt2, 1),
-                               "bytes_per_step": t2.exchange_bytes,
-                               "GBps_effective": round(t2.exchange_bytes / (dt2 / K2) / 1e9, 2),
-                               "p2p_peak_GBps_measured": round(float(pk.item()), 2)}
-        except Exception as e:  # the headline number stands on its own
-            out["exchange"] = {"error": repr(e)[:300]}
+            out["k5_splitfed"] = {"error": repr(e)[:300]}
 
 
 def progress(msg):
