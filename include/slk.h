@@ -135,7 +135,11 @@ int slk_conv2_wgrad_direct_nslab(int B);
 /* ---------------------------------------------------------------- reductions / optimizer */
 
 /* out[i] = (accumulate ? out[i] : 0) + sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed slab order).
- * accumulate = 1 sums micro-batches into one gradient (pipeline topologies). */
+ * accumulate = 1 sums micro-batches into one gradient (pipeline topologies).
+ * Summation order (all slab reductions, incl. SGD / Adam from slabs): nslab <= 64 -> slabs in
+ * ascending order per column; nslab > 64 -> 16 partial sums over slabs w, w+16, w+32, ... (w = 0..15)
+ * added in w order. Either is a fixed function of (slabs, nslab): bit-stable run to run, but a result
+ * at nslab <= 64 is not bitwise comparable with one at nslab > 64. */
 int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, int accumulate, void* stream);
 
 /* Fused deterministic slab reduction + SGD (lr, no momentum, no weight decay):

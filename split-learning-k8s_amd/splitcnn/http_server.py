@@ -21,6 +21,7 @@ Differences by design:
 
 import asyncio
 import io
+import logging
 import os
 import pickle
 import threading
@@ -58,10 +59,18 @@ def safe_loads(data: bytes):
     return SafeUnpickler(io.BytesIO(data)).load()
 
 
+log = logging.getLogger("splitcnn.http")
+
+
 def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = None,
              sink: Optional[Callable[[int, float], None]] = None, flush_every: int = 100,
-             fed_clients: int = 1):
-    """Build the FastAPI app. `server` defaults to a seeded ServerStage on `device`."""
+             fed_clients: int = 1, fed_timeout: float = 600.0):
+    """Build the FastAPI app. `server` defaults to a seeded ServerStage on `device`.
+
+    Federated rounds (fed_clients = K > 1): a round closes when K states have arrived. A request may
+    carry an optional "client_id"; a second post from the same id in an open round is refused (409)
+    instead of being counted twice. A round that does not fill within `fed_timeout` seconds is
+    abandoned: every waiting client gets 504 and the next post opens a fresh round."""
     from fastapi import FastAPI, Request, Response
 
     from .engine import LossLog, ServerStage
@@ -105,8 +114,11 @@ def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = N
             out = cut_grad.detach().cpu()
             state["since_flush"] += 1
             if state["since_flush"] >= flush_every:
-                s.loss_log.flush()
                 state["since_flush"] = 0
+                try:
+                    s.loss_log.flush()
+                except Exception as e:  # the step is applied: a sink outage must not turn it into a 500
+                    log.warning("loss sink flush failed (metrics stay buffered in the sink): %r", e)
         return Response(content=pickle.dumps(out), media_type="application/octet-stream")
 
     fed = {"round": None}
@@ -120,15 +132,22 @@ def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = N
             data = safe_loads(await request.body())
             client_state = data["model_state"]
             epoch, client_loss, step = data["epoch"], data["loss"], data["step"]
+            client_id = data.get("client_id")
         except Exception as e:
             return Response(content=f"Error: bad payload ({e})", status_code=400)
         # A round closes when `fed_clients` states have arrived; every waiting client gets the mean.
         # fed_clients=1 is the reference's identity aggregation (server_part.py:81).
         rnd = fed["round"]
         if rnd is None:
-            rnd = fed["round"] = {"states": [], "losses": [], "done": asyncio.Event(), "out": None}
+            rnd = fed["round"] = {"states": [], "losses": [], "ids": set(), "done": asyncio.Event(),
+                                  "out": None}
+        if client_id is not None:
+            if client_id in rnd["ids"]:
+                return Response(content=f"Error: client {client_id!r} already posted to this round",
+                                status_code=409)
+            rnd["ids"].add(client_id)
         rnd["states"].append(client_state)
-        rnd["losses"].append((int(step), float(client_loss)))
+        rnd["losses"].append((int(step), float(client_loss), float(epoch)))
         if len(rnd["states"]) >= fed_clients:
             fed["round"] = None
             with lock:
@@ -139,12 +158,29 @@ def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = N
                        for k in rnd["states"][0]}
                 m.load_state_dict(avg)
                 if sink is not None:
-                    sink(max(s for s, _ in rnd["losses"]),
-                         sum(l for _, l in rnd["losses"]) / len(rnd["losses"]))
+                    # mlflow.log_metric("loss" / "epoch", ..., step=step)  (server_part.py:86-87)
+                    st = max(s for s, _, _ in rnd["losses"])
+                    mean_loss = sum(l for _, l, _ in rnd["losses"]) / len(rnd["losses"])
+                    try:
+                        if hasattr(sink, "log_metric"):
+                            sink.log_metric("loss", mean_loss, st)
+                            sink.log_metric("epoch", max(e for _, _, e in rnd["losses"]), st)
+                        else:
+                            sink(st, mean_loss)
+                        if hasattr(sink, "flush"):
+                            sink.flush()
+                    except Exception as e:
+                        log.warning("metric sink failed (metrics stay buffered in the sink): %r", e)
                 rnd["out"] = pickle.dumps(m.state_dict())
             rnd["done"].set()
         else:
-            await rnd["done"].wait()
+            try:
+                await asyncio.wait_for(rnd["done"].wait(), timeout=fed_timeout)
+            except asyncio.TimeoutError:
+                if fed["round"] is rnd:
+                    fed["round"] = None   # abandon the partial round
+                return Response(content=f"Error: federated round incomplete after {fed_timeout}s "
+                                        f"({len(rnd['states'])}/{fed_clients} clients)", status_code=504)
         return Response(content=rnd["out"], media_type="application/octet-stream")
 
     @app.get("/health")

@@ -17,9 +17,13 @@ class JsonlSink:
         self.path, self.key = path, key
         self._pending: List[dict] = []
 
-    def __call__(self, step: int, value: float):
-        self._pending.append({"key": self.key, "value": float(value), "step": int(step),
+    def log_metric(self, key: str, value: float, step: int):
+        """mlflow.log_metric(key, value, step=step) (server_part.py:55,86-87), buffered until flush."""
+        self._pending.append({"key": key, "value": float(value), "step": int(step),
                               "timestamp": int(time.time() * 1000)})
+
+    def __call__(self, step: int, value: float):
+        self.log_metric(self.key, value, step)
 
     def flush(self):
         if self._pending:
@@ -61,12 +65,18 @@ class MlflowRestSink:
         r.raise_for_status()
         return r.json()["run"]["info"]["run_id"]
 
-    def __call__(self, step: int, value: float):
-        self._pending.append({"key": self.key, "value": float(value), "step": int(step),
+    def log_metric(self, key: str, value: float, step: int):
+        self._pending.append({"key": key, "value": float(value), "step": int(step),
                               "timestamp": int(time.time() * 1000)})
 
+    def __call__(self, step: int, value: float):
+        self.log_metric(self.key, value, step)
+
     def flush(self):
+        """Post the buffered metrics in log-batch chunks. A chunk leaves the buffer only after the
+        tracking server accepted it, so a failed post (raised) is retried by the next flush."""
         while self._pending:
-            chunk, self._pending = self._pending[:self.BATCH], self._pending[self.BATCH:]
+            chunk = self._pending[:self.BATCH]
             r = self._api("POST", "runs/log-batch", json={"run_id": self.run_id, "metrics": chunk})
             r.raise_for_status()
+            del self._pending[:len(chunk)]

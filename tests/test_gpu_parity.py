@@ -333,3 +333,24 @@ def test_graph_alternating_batch_sizes_equal_eager(gpu):
     assert torch.equal(results[0][0], results[1][0])
     assert torch.equal(results[0][1], results[1][1])
     assert results[0][2] == results[1][2]
+
+
+@pytest.mark.parametrize("nslab", [16, 17, 64, 65, 256])
+def test_slab_reduction_both_orders_vs_float64(gpu, nslab):
+    """slk_reduce_slabs / slk_sgd_from_slabs pick their summation order by slab count (<= 64:
+    thread per column, ascending; > 64: 16 waves over slabs w, w+16, ..., combined in wave order —
+    include/slk.h). Both are fixed orders (run-to-run identical) and both match a float64 sum."""
+    from splitcnn import ops
+    g = torch.Generator(device=gpu).manual_seed(nslab)
+    n = 5000
+    slabs = torch.randn(nslab, n, device=gpu, generator=g)
+    got = ops.reduce_slabs(slabs)
+    again = ops.reduce_slabs(slabs)
+    want = slabs.double().sum(0)
+    assert torch.equal(got, again)
+    err = (got.double() - want).abs().max().item() / want.abs().max().item()
+    assert err <= 1e-6, err
+    param = torch.zeros(n, device=gpu)
+    grad = torch.empty(n, device=gpu)
+    ops.sgd_from_slabs(param, grad, slabs, 0.5)
+    assert torch.equal(grad, got) and torch.equal(param, -0.5 * got)

@@ -167,3 +167,78 @@ def test_federated_round_averages_k_clients():
     for k in sds[0]:
         want = (sds[0][k] + sds[1][k]) / 2
         assert torch.allclose(outs[0][k], want, rtol=0, atol=1e-7) and torch.equal(outs[0][k], outs[1][k])
+
+
+def test_federated_round_refuses_duplicate_client_and_times_out():
+    """A client id posting twice into one open round gets 409 (not counted twice); a round that
+    never fills answers 504 after fed_timeout and the next post starts a fresh round. The epoch is
+    logged next to the loss (server_part.py:86-87)."""
+    import asyncio
+
+    import httpx
+    from splitcnn.data import init_models
+    from splitcnn.http_server import make_app
+    from splitcnn.sinks import JsonlSink
+
+    class Rec(JsonlSink):
+        def __init__(self):
+            super().__init__(path="/dev/null")
+            self.seen = []
+
+        def log_metric(self, key, value, step):
+            self.seen.append((key, value, step))
+
+    rec = Rec()
+    app = make_app(device="cpu", learning_mode="federated", fed_clients=2, fed_timeout=0.5, sink=rec)
+    sd = init_models(seed=1, full=True).state_dict()
+    body = lambda cid, loss=1.0: pickle.dumps({"model_state": sd, "epoch": 3, "loss": loss, "step": 7,  # noqa: E731
+                                               "client_id": cid})
+
+    async def run():
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as c:
+            first = asyncio.create_task(c.post("/aggregate_weights", content=body("a")))
+            await asyncio.sleep(0.05)
+            dup = await c.post("/aggregate_weights", content=body("a"))
+            timed_out = await first
+            fresh = await asyncio.gather(c.post("/aggregate_weights", content=body("a", 1.0)),
+                                         c.post("/aggregate_weights", content=body("b", 3.0)))
+        return dup, timed_out, fresh
+
+    dup, timed_out, fresh = asyncio.run(run())
+    assert dup.status_code == 409
+    assert timed_out.status_code == 504
+    assert [r.status_code for r in fresh] == [200, 200]
+    assert rec.seen == [("loss", 2.0, 7), ("epoch", 3.0, 7)]
+
+
+def test_mlflow_sink_keeps_metrics_until_posted(monkeypatch):
+    """MlflowRestSink.flush drops a chunk only after the tracking server accepted it: a failed post
+    raises and the next flush re-sends the same metrics."""
+    from splitcnn import sinks
+
+    class Resp:
+        def __init__(self, ok):
+            self.ok = ok
+            self.status_code = 200 if ok else 503
+
+        def raise_for_status(self):
+            if not self.ok:
+                raise RuntimeError("503")
+
+    posts = []
+    outcomes = iter([False, True])
+
+    def fake_api(self, method, path, **kw):
+        posts.append([m["step"] for m in kw["json"]["metrics"]])
+        return Resp(next(outcomes))
+
+    monkeypatch.setattr(sinks.MlflowRestSink, "_api", fake_api)
+    s = sinks.MlflowRestSink.__new__(sinks.MlflowRestSink)
+    s.key, s.run_id, s._pending = "loss", "r", []
+    s(1, 0.5)
+    s(2, 0.4)
+    with pytest.raises(RuntimeError):
+        s.flush()
+    s.flush()
+    assert posts == [[1, 2], [1, 2]] and s._pending == []

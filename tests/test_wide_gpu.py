@@ -282,7 +282,8 @@ def test_adam_multi_bit_identical_to_separate_launches():
         st = WideClientStage(a, device=dev)
         st.fuse_adam = fuse
         stages.append(st)
-    slabs = [torch.randn(n_s, n, device=dev, generator=g) * 1e-3 for n_s, n in ((7, 1792), (5, 73856), (3, 295168))]
+    # slab counts on both sides of the 64-slab order switch (the production conv1 set has 512 slabs)
+    slabs = [torch.randn(n_s, n, device=dev, generator=g) * 1e-3 for n_s, n in ((512, 1792), (17, 73856), (65, 295168))]
     for _ in range(2):  # two steps: the second reads m, v and the step counter the first wrote
         for st in stages:
             st.step_from_slabs(*slabs)

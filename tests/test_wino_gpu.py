@@ -102,3 +102,53 @@ def test_winograd_multi_unit_per_workgroup(gpu, B):
     sd = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, direct=True))
     assert rel_err(sw[:18432].cpu().numpy(), sd[:18432].cpu().numpy()) <= 1e-5
     assert rel_err(sw[18432:].cpu().numpy(), sd[18432:].cpu().numpy()) <= 1e-5
+
+
+def test_full_size_b4096_vs_direct_and_oracle(gpu):
+    """K2 size (B = 4096, where every dgrad/wgrad workgroup runs 16 units of its persistent stream):
+    Winograd fwd / dgrad / wgrad against the independent direct implicit-GEMM kernels on identical
+    inputs — pooled outside tie-routed windows, the cut gradient per sample, dW2 / db2 — all at 1e-5;
+    then dW3 / db3 (fc wgrad) and dW1 / db1 (client conv1 wgrad) against the fp64 oracle on the
+    same GPU-produced operands at 1e-5 / 1e-4."""
+    from oracle.split_step import client_backward, cross_entropy
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage
+    B = 4096
+    a, b = init_models(seed=21)
+    x, y = SyntheticMNIST(22).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    client = ClientStage(a, device=gpu)
+    act = client.forward(x).clone()
+    p = {k: v.detach().to(gpu).contiguous() for k, v in
+         {"W2": b.conv2.weight, "b2": b.conv2.bias, "W3": b.fc1.weight, "b3": b.fc1.bias}.items()}
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    pd, cd = ops.conv2_fwd_pool(act, p["W2"], p["b2"], direct=True)
+    same = cw == cd
+    assert same.float().mean().item() > 0.9999
+    assert rel_err(pw[same].cpu().numpy(), pd[same].cpu().numpy()) <= 1e-5
+    logits, _, dlogits, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    gw = ops.conv2_dgrad(dp, cw, p["W2"])
+    gd = ops.conv2_dgrad(dp, cw, p["W2"], direct=True)
+    num = (gw - gd).abs().flatten(1).max(dim=1).values
+    den = gd.abs().flatten(1).max(dim=1).values.clamp_min(1e-30)
+    assert (num / den).max().item() <= 1e-5
+    sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw))
+    sd = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, direct=True))
+    assert rel_err(sw[:18432].cpu().numpy(), sd[:18432].cpu().numpy()) <= 1e-5
+    assert rel_err(sw[18432:].cpu().numpy(), sd[18432:].cpu().numpy()) <= 1e-5
+    # fc1: loss / dlogits / dW3 / db3 in fp64 from the GPU's pooled features
+    flat = pw.double().cpu().numpy().reshape(B, 9216)
+    z = flat @ p["W3"].double().cpu().numpy().T + p["b3"].double().cpu().numpy()
+    assert rel_err(logits.cpu().numpy(), z) <= 1e-4
+    _, _, dz = cross_entropy(z, y.cpu().numpy())
+    assert rel_err(dlogits.cpu().numpy(), dz) <= 1e-4
+    s3 = ops.reduce_slabs(ops.fc_wgrad_slabs(dlogits, pw)).cpu().numpy()
+    assert rel_err(s3[:92160], (dz.T @ flat).reshape(-1)) <= 1e-5
+    assert rel_err(s3[92160:], dz.sum(axis=0)) <= 1e-5
+    assert rel_err(dp.cpu().numpy().reshape(B, 9216), dz @ p["W3"].double().cpu().numpy()) <= 1e-5
+    # client conv1 wgrad (ReLU mask recomputed from x) vs the oracle on the GPU cut gradient
+    s1 = ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, client.W1.detach(), client.b1.detach(), gw)).cpu().numpy()
+    dW1, db1 = client_backward(x.double().cpu().numpy(), act.double().cpu().numpy(), gw.double().cpu().numpy())
+    assert rel_err(s1[:288], dW1.reshape(-1)) <= 1e-5
+    assert rel_err(s1[288:], db1) <= 1e-5
