@@ -219,6 +219,16 @@ int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const 
                   int B, void* stream);
 int slk_wide_head_nslab(int B);
 int slk_wide_head_work(int B);
+/* slk_wide_head split at the loss, for the module path (WideModelPartB.forward -> criterion ->
+ * loss.backward(), server_part.py:48-51): _fwd writes the logits (dropout + fc, same arithmetic and
+ * partial order as slk_wide_head); _bwd takes dlogits from any loss and writes dcut and the fc slabs
+ * exactly as slk_wide_head's last stage. */
+int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step, unsigned seed,
+                      unsigned keep_threshold, float keep_scale, float* logits, float* work, int b0, int B,
+                      void* stream);
+int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogits, const int* step, unsigned seed,
+                      unsigned keep_threshold, float keep_scale, uint16_t* dcut, float* slabs, int b0, int B,
+                      void* stream);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
  * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
  * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs

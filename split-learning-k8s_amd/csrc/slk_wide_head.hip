@@ -174,6 +174,11 @@ __global__ __launch_bounds__(256) void wide_head_ce_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < NC; ++j) se += expf(z[j] - m);
     const float lse = m + logf(se);
+    if (!labels) {  // forward only (the module path: WideModelPartB.forward, the loss comes later)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) logits[(size_t)b * NC + j] = z[j];
+        return;
+    }
     const int64_t y = labels[b];
     const bool ok = y >= 0 && y < NC;
     if (!ok && err_flag) atomicOr(err_flag, 1);
@@ -440,6 +445,30 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
                        keep_threshold, keep_scale, dcut, slabs, b0, B);
     return slk_launch_status();
 }
+extern "C" int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step,
+                                 unsigned seed, unsigned keep_threshold, float keep_scale, float* logits, float* work,
+                                 int b0, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && bf && step && logits && work);
+    SLK_CHECK_ARG(((uintptr_t)work & 15) == 0);
+    if (B == 0) return 0;
+    hipStream_t st = slk_stream(stream);
+    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ((B + HSG_L - 1) / HSG_L)), dim3(256), 0, st, cut, wf8, step, seed,
+                       keep_threshold, keep_scale, work, b0, B);
+    hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + 255) / 256), dim3(256), 0, st, work, bf, nullptr, 0.f, logits,
+                       nullptr, nullptr, nullptr, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogits, const int* step,
+                                 unsigned seed, unsigned keep_threshold, float keep_scale, uint16_t* dcut, float* slabs,
+                                 int b0, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && dlogits && step && dcut && slabs);
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * slk_wide_head_nslab(B)), dim3(256), 0, slk_stream(stream), cut,
+                       wf8, dlogits, step, seed, keep_threshold, keep_scale, dcut, slabs, b0, B);
+    return slk_launch_status();
+}
+
 extern "C" int slk_adam_from_slabs(float* param, float* grad, float* m, float* v, const float* slabs, int nslab,
                                    int n, float lr, float beta1, float beta2, float eps, const int* step,
                                    void* stream) {

@@ -48,8 +48,17 @@ _F32 = torch.float32
 
 
 # ------------------------------------------------------------------------------------ modules
+# The module contract of src/model_def.py:5-71 for the widened network: the halves are differentiable
+# (autograd Functions over the same kernels the stages launch), so the reference's own step code runs
+# on them — client: activations = model(x); activations.backward(grads); optimizer.step()
+# (src/client_part.py:112-133); server: client_activations.requires_grad_(True); outputs =
+# model(client_activations); loss = criterion(outputs, labels); loss.backward(); optimizer.step();
+# return client_activations.grad (src/server_part.py:45-57). The cut is bf16 in logical NCHW
+# [B,256,8,8] at this boundary (the kernels use C8 internally). The stages (WideClientStage /
+# WideServerStage / WideTrainer) are the fused fast path over the same kernels.
 class WideModelPartA(nn.Module):
-    """Client bottom stack of the widened split CNN (parameter container; kernels in WideClientStage)."""
+    """Client bottom stack: conv1 3->64 + ReLU, conv2 64->128 + ReLU + pool, conv3 128->256 + ReLU +
+    pool -> cut bf16 [B,256,8,8]."""
 
     def __init__(self):
         super().__init__()
@@ -60,22 +69,34 @@ class WideModelPartA(nn.Module):
         self.pool = nn.MaxPool2d(2)
 
     def forward(self, x):
-        raise RuntimeError("splitcnn.WideModelPartA runs through WideClientStage / WideTrainer on the "
-                           "MI355X HIP kernels; there is no CPU or eager-torch path")
+        _require_cuda(x, "WideModelPartA")
+        return _WideClientFn.apply(x, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
+                                   self.conv3.weight, self.conv3.bias)
 
 
 class WideModelPartB(nn.Module):
-    """Server top stack: Dropout(0.25) -> flatten -> Linear(16384, 10)."""
+    """Server top stack: Dropout(0.25) -> flatten -> Linear(16384, 10). In training mode each forward
+    draws a fresh dropout mask (the hash of seed, forward count, sample, feature — the stages' mask
+    at the same step); eval mode keeps every feature."""
 
     def __init__(self):
         super().__init__()
         self.dropout = nn.Dropout(P_DROP)
         self.flatten = nn.Flatten()
         self.fc = nn.Linear(256 * 8 * 8, 10)
+        self.dropout_seed = 0
+        self._drop_step = None   # device forward counter (not state: keeps the state_dict contract)
 
     def forward(self, x):
-        raise RuntimeError("splitcnn.WideModelPartB runs through WideServerStage / WideTrainer on the "
-                           "MI355X HIP kernels; there is no CPU or eager-torch path")
+        _require_cuda(x, "WideModelPartB")
+        if self._drop_step is None or self._drop_step.device != x.device:
+            self._drop_step = torch.zeros(1, dtype=torch.int32, device=x.device)
+        snap = self._drop_step.clone()
+        thresh, scale = (KEEP_THRESHOLD, KEEP_SCALE) if self.training else (0, 1.0)
+        logits = _WideHeadFn.apply(x, self.fc.weight, self.fc.bias, snap, self.dropout_seed, thresh, scale)
+        if self.training:
+            _lib.call("slk_tick", self._drop_step.data_ptr(), _stream(x))
+        return logits
 
 
 class WideFullModel(nn.Module):
@@ -86,9 +107,15 @@ class WideFullModel(nn.Module):
         a, b = WideModelPartA(), WideModelPartB()
         self.conv1, self.conv2, self.conv3 = a.conv1, a.conv2, a.conv3
         self.dropout, self.fc = b.dropout, b.fc
+        self._head = [b]   # shares fc / dropout; kept out of the module tree (state_dict keys)
 
     def forward(self, x):
-        raise RuntimeError("splitcnn.WideFullModel runs through WideTrainer on the MI355X HIP kernels")
+        _require_cuda(x, "WideFullModel")
+        cut = _WideClientFn.apply(x, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
+                                  self.conv3.weight, self.conv3.bias)
+        head = self._head[0]
+        head.train(self.training)
+        return head(cut)
 
 
 def get_wide_model(role="client"):
@@ -156,6 +183,149 @@ def _k(name, *args):
         _lib.call("slk_" + name, *args)
 
 
+
+def _require_cuda(x, who):
+    if x.device.type != "cuda":
+        raise RuntimeError(f"splitcnn.{who}: input is on {x.device}; the widened model runs on the MI355X HIP "
+                           "kernels only (move the module and its inputs to a ROCm device). There is no CPU fallback.")
+
+
+def _f32p(t, name, n):
+    """Device pointer of an f32 parameter (contiguous, n elements)."""
+    _dev(t, name)
+    if t.numel() != n:
+        raise ValueError(f"{name}: expected {n} elements, got {t.numel()}")
+    return t.data_ptr()
+
+
+def new_shadows(device):
+    return {"w1b": torch.empty(64 * 32, dtype=_BF, device=device), "w2f": torch.empty(73728, dtype=_BF, device=device),
+            "w2d": torch.empty(73728, dtype=_BF, device=device), "w3f": torch.empty(294912, dtype=_BF, device=device),
+            "w3d": torch.empty(294912, dtype=_BF, device=device)}
+
+
+def build_shadows(W1, W2, W3, sh, stream):
+    """bf16 MFMA layouts of the conv weights from their f32 masters (slk_wide_shadows)."""
+    _k("wide_shadows", _f32p(W1, "conv1.weight", 1728), _f32p(W2, "conv2.weight", 73728),
+       _f32p(W3, "conv3.weight", 294912), sh["w1b"].data_ptr(), sh["w2f"].data_ptr(), sh["w2d"].data_ptr(),
+       sh["w3f"].data_ptr(), sh["w3d"].data_ptr(), stream)
+
+
+def client_forward_kernels(x, sh, b1, b2, b3, a1, p2, code2, cut, code3):
+    """conv1 + ReLU -> conv2 + ReLU + pool -> conv3 + ReLU + pool (the cut), C8 bf16."""
+    B = x.shape[0]
+    _dev(x, "x", (B, 3, 32, 32))
+    s = _stream(x)
+    b1p, b2p, b3p = _f32p(b1, "conv1.bias", 64), _f32p(b2, "conv2.bias", 128), _f32p(b3, "conv3.bias", 256)
+    _k("wide_conv1_fwd", x.data_ptr(), sh["w1b"].data_ptr(), b1p, a1.data_ptr(), B, s)
+    _k("wide_conv2_fwd", a1.data_ptr(), sh["w2f"].data_ptr(), b2p, p2.data_ptr(), code2.data_ptr(), B, s)
+    _k("wide_conv3_fwd", p2.data_ptr(), sh["w3f"].data_ptr(), b3p, cut.data_ptr(), code3.data_ptr(), B, s)
+
+
+def client_backward_slab_shapes(B):
+    return ((_q("slk_wide_conv1_wgrad_nslab", B), 1728 + 64), (_q("slk_wide_conv2_wgrad_nslab", B), 73728 + 128),
+            (_q("slk_wide_conv3_wgrad_nslab", B), 294912 + 256))
+
+
+def client_backward_kernels(dcut, saved, w2d, w3d, scratch, s1, s2, s3):
+    """activations.backward(dcut) of the client stack into three slab sets [dW | db] (conv1, conv2,
+    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dc3, dc2, da1m)."""
+    B = dcut.shape[0]
+    _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
+    x, a1, p2, code2, code3 = saved
+    dc3, dc2, da1m = scratch
+    s = _stream(dcut)
+    _k("wide_unpool", dcut.data_ptr(), code3.data_ptr(), dc3.data_ptr(), B, s)
+    _k("wide_conv3_wgrad", dc3.data_ptr(), p2.data_ptr(), s3.data_ptr(), B, s)
+    _k("wide_conv3_dgrad", dc3.data_ptr(), w3d.data_ptr(), code2.data_ptr(), dc2.data_ptr(), B, s)
+    _k("wide_conv2_wgrad", dc2.data_ptr(), a1.data_ptr(), s2.data_ptr(), B, s)
+    _k("wide_conv2_dgrad", dc2.data_ptr(), w2d.data_ptr(), a1.data_ptr(), da1m.data_ptr(), B, s)
+    _k("wide_conv1_wgrad", x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
+
+
+def client_backward_scratch(B, get):
+    """(dc3, dc2, da1m) via get(name, shape, dtype)."""
+    return (get("dc3", (B, 32, 16, 16, 8), _BF), get("dc2", (B, 16, 32, 32, 8), _BF),
+            get("da1m", (B, 8, 32, 32, 8), _BF))
+
+
+def _reduce(slabs):
+    out = torch.empty(slabs.shape[1], dtype=_F32, device=slabs.device)
+    _lib.call("slk_reduce_slabs", slabs.data_ptr(), slabs.shape[0], slabs.shape[1], out.data_ptr(), 0, _stream(slabs))
+    return out
+
+
+class _WideClientFn(torch.autograd.Function):
+    """cut = WideModelPartA(x) (bf16, logical NCHW); backward = the client stack's weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3):
+        x = x.contiguous()
+        B, dev = x.shape[0], x.device
+        Ws = [t.detach().contiguous() for t in (W1, b1, W2, b2, W3, b3)]
+        sh = new_shadows(dev)
+        build_shadows(Ws[0], Ws[2], Ws[4], sh, _stream(x))
+        a1 = torch.empty((B, 8, 32, 32, 8), dtype=_BF, device=dev)
+        p2 = torch.empty((B, 16, 16, 16, 8), dtype=_BF, device=dev)
+        code2 = torch.empty((B, 16, 16, 16, 8), dtype=_U8, device=dev)
+        cut = torch.empty((B,) + CUT_SHAPE, dtype=_BF, device=dev)
+        code3 = torch.empty((B,) + CUT_SHAPE, dtype=_U8, device=dev)
+        client_forward_kernels(x, sh, Ws[1], Ws[3], Ws[5], a1, p2, code2, cut, code3)
+        ctx.save_for_backward(x, a1, p2, code2, code3, sh["w2d"], sh["w3d"])
+        return c8_to_nchw(cut)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("splitcnn: gradient w.r.t. the client's input images is not part of the "
+                                      "split step (src/client_part.py:110-114)")
+        x, a1, p2, code2, code3, w2d, w3d = ctx.saved_tensors
+        B, dev = x.shape[0], x.device
+        dcut = nchw_to_c8(g.to(_BF))
+        scratch = client_backward_scratch(B, lambda n, sh_, dt: torch.empty(sh_, dtype=dt, device=dev))
+        slabs = [torch.empty(sh_, dtype=_F32, device=dev) for sh_ in client_backward_slab_shapes(B)]
+        client_backward_kernels(dcut, (x, a1, p2, code2, code3), w2d, w3d, scratch, *slabs)
+        g1, g2, g3 = (_reduce(sl) for sl in slabs)
+        return (None, g1[:1728].view(64, 3, 3, 3), g1[1728:], g2[:73728].view(128, 64, 3, 3), g2[73728:],
+                g3[:294912].view(256, 128, 3, 3), g3[294912:])
+
+
+class _WideHeadFn(torch.autograd.Function):
+    """logits = fc(dropout(flatten(cut))) — WideModelPartB.forward; backward gives the cut gradient
+    (bf16, logical NCHW) and the fc weight gradient."""
+
+    @staticmethod
+    def forward(ctx, cut_nchw, Wf, bf, step, seed, thresh, scale):
+        B, dev = cut_nchw.shape[0], cut_nchw.device
+        if tuple(cut_nchw.shape[1:]) != (256, 8, 8):
+            raise ValueError(f"cut: expected [B,256,8,8], got {tuple(cut_nchw.shape)}")
+        cut = nchw_to_c8(cut_nchw.detach().to(_BF))
+        Wf, bf = Wf.detach().contiguous(), bf.detach().contiguous()
+        wf8 = torch.empty(163840, dtype=_F32, device=dev)
+        s = _stream(cut)
+        _k("wide_fc_shadow", _f32p(Wf, "fc.weight", 163840), wf8.data_ptr(), s)
+        logits = torch.empty((B, 10), dtype=_F32, device=dev)
+        work = torch.empty((_q("slk_wide_head_work", B),), dtype=_F32, device=dev)
+        _k("wide_head_fwd", cut.data_ptr(), wf8.data_ptr(), _f32p(bf, "fc.bias", 10), step.data_ptr(), int(seed),
+           int(thresh), float(scale), logits.data_ptr(), work.data_ptr(), 0, B, s)
+        ctx.save_for_backward(cut, wf8, step)
+        ctx.drop = (int(seed), int(thresh), float(scale))
+        ctx.in_dtype = cut_nchw.dtype
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        cut, wf8, step = ctx.saved_tensors
+        seed, thresh, scale = ctx.drop
+        B, dev = cut.shape[0], cut.device
+        dlogits = dlogits.to(_F32).contiguous()
+        dcut = torch.empty_like(cut)
+        slabs = torch.empty((_q("slk_wide_head_nslab", B), SERVER_NPARAM), dtype=_F32, device=dev)
+        _k("wide_head_bwd", cut.data_ptr(), wf8.data_ptr(), _dev(dlogits, "dlogits", (B, 10)), step.data_ptr(), seed,
+           thresh, scale, dcut.data_ptr(), slabs.data_ptr(), 0, B, _stream(dlogits))
+        g = _reduce(slabs)
+        return (c8_to_nchw(dcut).to(ctx.in_dtype), g[:163840].view(10, 16384), g[163840:], None, None, None, None)
+
 # ------------------------------------------------------------------------------------ stages
 class WideClientStage:
     """Client half: forward(x) -> cut (bf16 C8); backward_step(dcut) = activations.backward(grads) +
@@ -176,11 +346,7 @@ class WideClientStage:
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.lr, self.betas, self.eps = lr, betas, eps
         self.fuse_adam = True  # step_from_slabs: the three Adam segments in one launch
-        self.w1b = torch.empty(64 * 32, dtype=_BF, device=self.device)
-        self.w2f = torch.empty(73728, dtype=_BF, device=self.device)
-        self.w2d = torch.empty(73728, dtype=_BF, device=self.device)
-        self.w3f = torch.empty(294912, dtype=_BF, device=self.device)
-        self.w3d = torch.empty(294912, dtype=_BF, device=self.device)
+        self.sh = new_shadows(self.device)   # bf16 conv weight shadows (slk_wide_shadows layouts)
         self._buf = _Buffers()
         self._saved = {}
         self.refresh_shadows()
@@ -194,52 +360,32 @@ class WideClientStage:
 
     def refresh_shadows(self):
         """Rebuild the bf16 conv weight shadows from the f32 masters (after load_state_dict or Adam)."""
-        W2, W3 = self._p("W2", 73728), self._p("W3", 294912)
-        _k("wide_shadows", self._p("W1", 1728).data_ptr(), W2.data_ptr(), W3.data_ptr(), self.w1b.data_ptr(),
-           self.w2f.data_ptr(), self.w2d.data_ptr(),
-                  self.w3f.data_ptr(), self.w3d.data_ptr(), _stream(self.params))
+        build_shadows(self._p("W1", 1728), self._p("W2", 73728), self._p("W3", 294912), self.sh, _stream(self.params))
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, tag="") -> torch.Tensor:
         """cut = client forward of x; `tag` keeps separate saved tensors per micro-batch."""
         B = x.shape[0]
         _dev(x, "x", (B, 3, 32, 32))
-        s = _stream(x)
         a1 = self._b(f"a1{tag}", (B, 8, 32, 32, 8), _BF)
         p2 = self._b(f"p2{tag}", (B, 16, 16, 16, 8), _BF)
         code2 = self._b(f"code2{tag}", (B, 16, 16, 16, 8), _U8)
         cut = out if out is not None else self._b(f"cut{tag}", (B,) + CUT_SHAPE, _BF)
         _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
         code3 = self._b(f"code3{tag}", (B,) + CUT_SHAPE, _U8)
-        _k("wide_conv1_fwd", x.data_ptr(), self.w1b.data_ptr(), self._p("b1", 64).data_ptr(), a1.data_ptr(), B, s)
-        _k("wide_conv2_fwd", a1.data_ptr(), self.w2f.data_ptr(), self._p("b2", 128).data_ptr(),
-                  p2.data_ptr(), code2.data_ptr(), B, s)
-        _k("wide_conv3_fwd", p2.data_ptr(), self.w3f.data_ptr(), self._p("b3", 256).data_ptr(),
-                  cut.data_ptr(), code3.data_ptr(), B, s)
+        client_forward_kernels(x, self.sh, self._p("b1", 64), self._p("b2", 128), self._p("b3", 256),
+                               a1, p2, code2, cut, code3)
         self._x, self._a1, self._p2, self._code2, self._code3 = x, a1, p2, code2, code3
         self._saved[tag] = (x, a1, p2, code2, code3)
         return cut
 
     def backward_slabs(self, dcut: torch.Tensor, tag=""):
-        """Client backward into three slab sets (conv3, conv2, conv1); returns them."""
+        """Client backward into three slab sets (conv1, conv2, conv3); returns them."""
         B = dcut.shape[0]
-        _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
         self._x, self._a1, self._p2, self._code2, self._code3 = self._saved[tag]
-        s = _stream(dcut)
-        dc3 = self._b("dc3", (B, 32, 16, 16, 8), _BF)
-        dc2 = self._b("dc2", (B, 16, 32, 32, 8), _BF)
-        da1m = self._b("da1m", (B, 8, 32, 32, 8), _BF)
-        s3 = self._b("s3", (_q("slk_wide_conv3_wgrad_nslab", B), 294912 + 256), _F32)
-        s2 = self._b("s2", (_q("slk_wide_conv2_wgrad_nslab", B), 73728 + 128), _F32)
-        s1 = self._b("s1", (_q("slk_wide_conv1_wgrad_nslab", B), 1728 + 64), _F32)
-        _k("wide_unpool", dcut.data_ptr(), self._code3.data_ptr(), dc3.data_ptr(), B, s)
-        _k("wide_conv3_wgrad", dc3.data_ptr(), self._p2.data_ptr(), s3.data_ptr(), B, s)
-        _k("wide_conv3_dgrad", dc3.data_ptr(), self.w3d.data_ptr(), self._code2.data_ptr(),
-                  dc2.data_ptr(), B, s)
-        _k("wide_conv2_wgrad", dc2.data_ptr(), self._a1.data_ptr(), s2.data_ptr(), B, s)
-        _k("wide_conv2_dgrad", dc2.data_ptr(), self.w2d.data_ptr(), self._a1.data_ptr(),
-                  da1m.data_ptr(), B, s)
-        _k("wide_conv1_wgrad", self._x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
-        self._dc3, self._dc2, self._da1m = dc3, dc2, da1m
+        scratch = client_backward_scratch(B, self._b)
+        s1, s2, s3 = (self._b(n, shp, _F32) for n, shp in zip(("s1", "s2", "s3"), client_backward_slab_shapes(B)))
+        client_backward_kernels(dcut, self._saved[tag], self.sh["w2d"], self.sh["w3d"], scratch, s1, s2, s3)
+        self._dc3, self._dc2, self._da1m = scratch
         return s1, s2, s3
 
     def _adam(self, lo, n, slabs):

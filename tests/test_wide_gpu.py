@@ -309,3 +309,84 @@ def test_wide_graph_alternating_batch_sizes_equal_eager(gpu):
     assert torch.equal(results[0][0], results[1][0])
     assert torch.equal(results[0][1], results[1][1])
     assert results[0][2] == results[1][2]
+
+
+def test_wide_modules_run_the_reference_step_code(gpu):
+    """Module contract for the widened model: the reference's own step code (client_part.py:112-133,
+    server_part.py:45-57) run verbatim on WideModelPartA / WideModelPartB with torch.optim.Adam and the
+    drop-in CrossEntropyLoss. Same kernels as the stages, so the cut, the loss, the cut gradient and
+    every weight gradient equal the fused WideTrainer step's; Adam (torch's own here) matches the
+    torch formula on those gradients; WideFullModel's forward/backward equals the split modules'."""
+    from splitcnn.model_def import CrossEntropyLoss
+    from splitcnn.wide import (CUT_SHAPE, SyntheticCIFAR, WideFullModel, WideTrainer, c8_to_nchw,
+                               init_wide_models)
+    B = 8
+    x, y = SyntheticCIFAR(4).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    ref = WideTrainer(*init_wide_models(seed=0), device=gpu, graph=False)
+    ref.step(x, y)
+    torch.cuda.synchronize()
+    ref_cut = c8_to_nchw(ref.client._buf.get("cut", (B,) + CUT_SHAPE, torch.bfloat16, ref.device))
+    ref_dcut = c8_to_nchw(ref.server._buf.get("dcut", (B,) + CUT_SHAPE, torch.bfloat16, ref.device))
+    (_, ref_loss), = ref.loss_log.flush()
+
+    client_m, server_m = init_wide_models(seed=0)
+    client_m, server_m = client_m.to(gpu), server_m.to(gpu)
+    P0 = {k: _np(v) for k, v in list(client_m.state_dict().items()) + list(server_m.state_dict().items())}
+    optimizer_c = torch.optim.Adam(client_m.parameters(), lr=1e-3)
+    optimizer_s = torch.optim.Adam(server_m.parameters(), lr=1e-3)
+    criterion = CrossEntropyLoss()
+    # --- client_part.py:112-122
+    optimizer_c.zero_grad()
+    activations = client_m(x)
+    client_activations = activations.clone().detach()
+    # --- server_part.py:45-57
+    client_activations.requires_grad_(True)
+    optimizer_s.zero_grad()
+    outputs = server_m(client_activations)
+    loss = criterion(outputs, y)
+    loss.backward()
+    optimizer_s.step()
+    server_grads = client_activations.grad.clone().detach()
+    # --- client_part.py:131-133
+    activations.backward(server_grads)
+    optimizer_c.step()
+    torch.cuda.synchronize()
+
+    assert activations.dtype == torch.bfloat16 and tuple(activations.shape) == (B, 256, 8, 8)
+    assert torch.equal(activations, ref_cut)
+    assert abs(loss.item() - ref_loss) <= 1e-6 * abs(ref_loss)
+    assert torch.equal(server_grads, ref_dcut)
+    cg, sg = _np(ref.client.grads), _np(ref.server.grads)
+    offs = {"conv1.weight": (0, 1728), "conv1.bias": (1728, 1792), "conv2.weight": (1792, 75520),
+            "conv2.bias": (75520, 75648), "conv3.weight": (75648, 370560), "conv3.bias": (370560, 370816)}
+    for name, p in client_m.named_parameters():
+        lo, hi = offs[name]
+        grad_close(_np(p.grad).ravel(), cg[lo:hi], rtol=1e-6)
+    grad_close(_np(server_m.fc.weight.grad).ravel(), sg[:163840], rtol=1e-6)
+    grad_close(_np(server_m.fc.bias.grad), sg[163840:], rtol=1e-6)
+    # torch's Adam on these gradients = the torch formula (oracle/wide_step.adam) to f32 rounding
+    for m in (client_m, server_m):
+        for name, p in m.named_parameters():
+            g = _np(p.grad).ravel()
+            want, _, _ = W.adam(P0[name].ravel(), g, np.zeros_like(g), np.zeros_like(g), 1)
+            tol = 1e-6 * np.abs(want - P0[name].ravel()).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
+            assert (np.abs(_np(p).ravel() - want) <= tol).all(), name
+
+    # WideFullModel (seeded like the halves): same logits and gradients as the split modules
+    torch.manual_seed(0)
+    full = WideFullModel().to(gpu)
+    out_full = full(x)
+    assert torch.equal(out_full, outputs)
+    criterion(out_full, y).backward()
+    for name in ("conv1.weight", "conv3.weight", "fc.weight"):
+        mod, attr = name.split(".")
+        a = getattr(getattr(full, mod), attr).grad
+        b = getattr(getattr(client_m if mod != "fc" else server_m, mod), attr).grad
+        assert torch.equal(a, b), name
+    # eval mode: no dropout, no counter advance
+    server_m.eval()
+    with torch.no_grad():
+        e1 = server_m(client_activations)
+        e2 = server_m(client_activations)
+    assert torch.equal(e1, e2)
