@@ -836,26 +836,67 @@ constexpr int WW_THREADS = WW_WAVES * 64;
 constexpr int WW_DSTR = 52;                           // dpooled band row stride (48 used; 2-way banks)
 constexpr int WW_DP_OFF = WF_BSTR;                    // float offset of the dpooled band in a buffer
 constexpr int WW_DP_CH = 64 * 13 / 64;                // 13 chunks (13 sixteen-byte pieces per row)
-constexpr int WW_CSTR = 64;                           // code band row stride in bytes (48 used)
+// Code band rows are 48 bytes (the band's 48 windows, 3 DMA pieces): lanes li = 0..15 (one co each)
+// then read bytes 12 dwords apart, 2-way at worst on ds_read_u8's 32 banks (a 64-byte stride put 8
+// lanes on each of 2 banks: 8-way). The ZT table rows are 20 floats apart so that the five codes'
+// float4 reads sit on five distinct 16-byte slots of the 256-byte bank row (at 16 floats, code 4 —
+// ReLU-blocked, the commonest — shared a slot with code 0). A/B knobs: SLK_WW_CSTR, SLK_WW_LUTS.
+#ifndef SLK_WW_CSTR
+#define SLK_WW_CSTR 48
+#endif
+#ifndef SLK_WW_LUTS
+#define SLK_WW_LUTS 20
+#endif
+constexpr int WW_CSTR = SLK_WW_CSTR;                  // code band row stride in bytes (48 used)
+constexpr int WW_LUTS = SLK_WW_LUTS;                  // ZT row stride in floats (16 used)
+// Profiling-only ablation bits (tools/build_variant.sh -DSLK_WW_ABL=...; outputs wrong): 1 = no code
+// reads (code 0), 2 = no dpooled reads, 4 = no ZT reads, 8 = code as a dword read + byte extract,
+// 16 = no DMA / wait / barrier in the unit loop, 32 = no act patch transform (raw patch as operand),
+// 64 = no MFMA (operands kept alive), 128 = no barrier per unit, 256 = no DMA issue per unit,
+// 512 = clock diagnostic: slab[0] of each workgroup = its mean shader clock in GHz.
+#ifndef SLK_WW_ABL
+#define SLK_WW_ABL 0
+#endif
 constexpr int WW_CD_OFF = WW_DP_OFF + 64 * WW_DSTR;   // float offset of the code band
-constexpr int WW_CD_CH = 64 * 4 / 64;                 // 4 chunks (4 pieces per row)
+constexpr int WW_CD_PC = WW_CSTR / 16;                // DMA pieces per code row (3 used)
+constexpr int WW_CD_CH = 64 * WW_CD_PC / 64;          // chunks of the code band
 constexpr int WW_NCH = WF_CHUNKS + WW_DP_CH + WW_CD_CH;
 constexpr int WW_BSTR = WW_CD_OFF + 64 * WW_CSTR / 4; // 12800 floats = 51,200 B per buffer
 constexpr int WW_GRID = 256;
 constexpr int WW_SLAB = W2_N + C2;
+// Staging buffers (2: a unit's DMA is issued one unit ahead). Removing DMA + wait + barrier saves
+// 0.085 of 0.413 ms (tools/ablate.py, -DSLK_WW_ABL=16), but 3 buffers (DMA two units ahead) gain
+// nothing (0.422 vs 0.417 ms): not DMA latency. Knob kept for A/B.
+#ifndef SLK_WW_NBUF
+#define SLK_WW_NBUF 2
+#endif
+constexpr int WW_NBUF = SLK_WW_NBUF;
+// SLK_WW_SPREAD = 1 issues the next unit's DMA two or three pieces per K step instead of all at the
+// unit start: no gain (0.4175 vs 0.4153 ms), and neither with 3 buffers (0.4286). The DMA's cost
+// (dropping its issue entirely: 0.414 -> 0.346 ms at an unchanged 2.31 GHz in-kernel clock) is not
+// its latency nor its issue burst.
+#ifndef SLK_WW_SPREAD
+#define SLK_WW_SPREAD 0
+#endif
+constexpr bool WW_SPREAD = SLK_WW_SPREAD;
+// glds16 instructions of wave w per unit (chunks w, w+4, ...): the counted wait leaves the newer
+// unit's batch in flight
+template <int W>
+__device__ __forceinline__ void ww_wait_newest_batch() { wg_wait_vmcnt<(WW_NCH - W + WW_WAVES - 1) / WW_WAVES>(); }
 static_assert(WW_DP_OFF * 4 == WF_CHUNKS * 1024 && WW_CD_OFF * 4 == (WF_CHUNKS + WW_DP_CH) * 1024,
               "the three staging regions are consecutive KiB chunks");
 
+// chunks i0 .. i1-1 of this wave's share (chunk c = wave + 4i) of unit u's staging DMA
 __device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const float* __restrict__ dpool,
                                             const uint8_t* __restrict__ code, int u, const float* dst, int wave,
-                                            int lane) {
+                                            int lane, int i0 = 0, int i1 = 1 << 20) {
     const int b = u / 3, band = u - 3 * (u / 3);
     const uint32_t base = (uint32_t)(uintptr_t)dst;
     const float* asrc = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
     const float* dsrc = dpool + (size_t)b * P_SAMPLE + band * 48;
     const uint8_t* csrc = code + (size_t)b * P_SAMPLE + band * 48;
 #pragma unroll 1
-    for (int c = wave; c < WW_NCH; c += WW_WAVES) {
+    for (int c = wave + WW_WAVES * i0; c < WW_NCH && c < wave + WW_WAVES * i1; c += WW_WAVES) {
         const void* src;
         if (c < WF_CHUNKS) {
             const int p = min(c * 64 + lane, WF_PIECES - 1);
@@ -867,7 +908,7 @@ __device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const
             src = dsrc + co * P_WIN + 4 * k;
         } else {
             const int p = (c - WF_CHUNKS - WW_DP_CH) * 64 + lane;
-            const int co = p >> 2, k = min(p & 3, 2);
+            const int co = p / WW_CD_PC, k = min(p - WW_CD_PC * (p / WW_CD_PC), 2);
             src = csrc + co * P_WIN + 16 * k;
         }
         glds16(src, __builtin_amdgcn_readfirstlane(base + c * 1024));
@@ -896,14 +937,17 @@ __device__ __forceinline__ void wino_filter_grad(const float (&du)[16], float (&
 __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
     const float* __restrict__ act, const float* __restrict__ dpool, const uint8_t* __restrict__ code,
     float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * WW_BSTR + 5 * 16];
-    float* lutz = smem + 2 * WW_BSTR;  // ZT[c][16]
+    __shared__ __attribute__((aligned(16))) float smem[WW_NBUF * WW_BSTR + 5 * WW_LUTS];
+    float* lutz = smem + WW_NBUF * WW_BSTR;  // ZT[c][16], rows WW_LUTS floats apart
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar branches on tp
     const int mh = wu & 1, tp = wu >> 1;
     const int nunit = 3 * B;
+#if SLK_WW_ABL & 512
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     int u = blockIdx.x;
     if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wu, lane);
@@ -911,7 +955,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         const int c = tid >> 4, i = (tid >> 2) & 3, j = tid & 3;
         const float ai = (c & 2) ? (i == 0 ? 0.f : (i == 1 ? 1.f : -1.f)) : (i == 3 ? 0.f : 1.f);
         const float aj = (c & 1) ? (j == 0 ? 0.f : (j == 1 ? 1.f : -1.f)) : (j == 3 ? 0.f : 1.f);
-        lutz[tid] = c < 4 ? ai * aj : 0.f;
+        lutz[c * WW_LUTS + (tid & 15)] = c < 4 ? ai * aj : 0.f;
     }
     f32x4 acc[2][2][16];
 #pragma unroll
@@ -921,17 +965,32 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
 #pragma unroll
             for (int ij = 0; ij < 16; ++ij) acc[m][n][ij] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dbp[2] = {0.f, 0.f};
-    wg_wait_vmcnt<0>();
+    if (WW_NBUF > 2 && u + (int)gridDim.x < nunit)
+        ww_dma_unit(act, dpool, code, u + gridDim.x, smem + WW_BSTR, wu, lane);
 
     int buf = 0;
 #pragma unroll 1
     for (; u < nunit; u += gridDim.x) {
-        // this unit's band landed (no stores in this loop: vmcnt(0) is that DMA alone) and every wave
-        // is done with the other buffer
-        wg_wait_vmcnt<0>();
-        lds_barrier();
-        const int nu = u + gridDim.x;
-        if (nu < nunit) ww_dma_unit(act, dpool, code, nu, smem + (buf ^ 1) * WW_BSTR, wu, lane);
+        // this unit's DMA landed (no other vector memory ops in this loop: only the next unit's batch
+        // may stay in flight) and every wave is done with the buffer refilled next
+        const int nu = u + (WW_NBUF - 1) * (int)gridDim.x;
+        if (!(SLK_WW_ABL & 16)) {
+            if (WW_NBUF > 2 && u + (int)gridDim.x < nunit) {
+                switch (wu) {
+                    case 0: ww_wait_newest_batch<0>(); break;
+                    case 1: ww_wait_newest_batch<1>(); break;
+                    case 2: ww_wait_newest_batch<2>(); break;
+                    default: ww_wait_newest_batch<3>(); break;
+                }
+            } else {
+                wg_wait_vmcnt<0>();
+            }
+            if (!(SLK_WW_ABL & 128)) lds_barrier();
+            if (nu < nunit && !(SLK_WW_ABL & 256) && !WW_SPREAD) {
+                const int nb = buf + WW_NBUF - 1 >= WW_NBUF ? buf - 1 : buf + WW_NBUF - 1;
+                ww_dma_unit(act, dpool, code, nu, smem + nb * WW_BSTR, wu, lane);
+            }
+        }
         const float* img = smem + buf * WW_BSTR;
         const float* dpb = img + WW_DP_OFF + (32 * mh + li) * WW_DSTR;
         const uint8_t* cdb = reinterpret_cast<const uint8_t*>(img + WW_CD_OFF) + (32 * mh + li) * WW_CSTR;
@@ -952,8 +1011,14 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             lds_patch_pk(pa + 16 * WF_CSTR, lo[1], hi[1]);
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                v[m] = dpb[m * 16 * WW_DSTR + tl];
-                c[m] = cdb[m * 16 * WW_CSTR + tl];
+                v[m] = (SLK_WW_ABL & 2) ? 1.f : dpb[m * 16 * WW_DSTR + tl];
+                if (SLK_WW_ABL & 1)
+                    c[m] = 0;
+                else if (SLK_WW_ABL & 8)
+                    c[m] = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(cdb + m * 16 * WW_CSTR + (tl & ~3)),
+                                                 8 * (tl & 3), 8);
+                else
+                    c[m] = cdb[m * 16 * WW_CSTR + tl];
             }
         };
         f2 v01[2][4], v23[2][4], z01[2][4], z23[2][4];
@@ -962,14 +1027,21 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         auto zload = [&](const int (&c)[2], float4 (&E)[2][4]) {
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                const float4* zt = reinterpret_cast<const float4*>(lutz) + 4 * c[m];
+                const float4* zt = reinterpret_cast<const float4*>(lutz + WW_LUTS * c[m]);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) E[m][i] = zt[i];
+                for (int i = 0; i < 4; ++i) E[m][i] = (SLK_WW_ABL & 4) ? make_float4(1.f, 0.f, 1.f, 0.f) : zt[i];
             }
         };
         auto xform = [&](const f2 (&lo)[2][4], const f2 (&hi)[2][4], const float (&v)[2], const float4 (&E)[2][4]) {
-            pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
-            pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
+            if (SLK_WW_ABL & 32) {
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { v01[n][r] = lo[n][r]; v23[n][r] = hi[n][r]; }
+            } else {
+                pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
+                pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
+            }
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 const f2 vv = {v[m], v[m]};
@@ -987,8 +1059,12 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         load(1, Rlo[1], Rhi[1], dv[1], cd[1]);
         zload(cd[0], E);
         xform(Rlo[0], Rhi[0], dv[0], E);
+        const float* dma_dst = smem + (buf + WW_NBUF - 1 >= WW_NBUF ? buf - 1 : buf + WW_NBUF - 1) * WW_BSTR;
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
+            // (SLK_WW_SPREAD) the next unit's staging DMA, two or three pieces per K step
+            if (WW_SPREAD && !(SLK_WW_ABL & (16 | 256)) && nu < nunit)
+                ww_dma_unit(act, dpool, code, nu, dma_dst, wu, lane, 2 * j, j == 5 ? 1 << 20 : 2 * j + 2);
             if (j < 5) zload(cd[(j + 1) & 1], E);                                  // under these MFMAs
             if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // likewise
             __builtin_amdgcn_sched_barrier(0);
@@ -1006,7 +1082,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             __builtin_amdgcn_sched_barrier(0);
             if (j < 5) xform(Rlo[(j + 1) & 1], Rhi[(j + 1) & 1], dv[(j + 1) & 1], E);
         }
-        buf ^= 1;
+        buf = buf + 1 == WW_NBUF ? 0 : buf + 1;
     }
 
     mfma_drain();
@@ -1056,6 +1132,13 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
 #pragma unroll
         for (int m = 0; m < 2; ++m) slab[W2_N + 32 * mh + 16 * m + li] = dbp[m] + park[(mh * 2 + m) * 16 + li];
     }
+#if SLK_WW_ABL & 512
+    lds_barrier();
+    if (tid == 0) {
+        const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime();
+        slab[0] = (float)((double)(clk_t1 - clk_t0) / (double)(clk_r1 - clk_r0) * 0.1);
+    }
+#endif
 }
 
 extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (3 * B < WW_GRID ? 3 * B : WW_GRID) : 0; }

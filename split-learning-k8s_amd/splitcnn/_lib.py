@@ -90,6 +90,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # profiling only: run the same Python path over a variant build (tools/build_variant.sh output,
+    # compiled from these very sources, so the provenance check below still applies)
+    path = os.environ.get("SLK_LIB_VARIANT", path)
     if not os.path.exists(path):
         raise ImportError(
             f"splitcnn: {path} is missing. Build the HIP kernels first "
