@@ -230,6 +230,9 @@ constexpr int WF_CHUNKS = (WF_PIECES + 63) / 64;
 constexpr int WF_BSTR = WF_CHUNKS * 256;       // buffer stride: the last chunk writes a full KiB
 constexpr int WF_GRID = 256;                   // one workgroup per CU
 
+// The one-M-block-per-wave forward (round 1's v1, superseded by conv2_fwd_pool_wino2_kernel below)
+// is kept only as a profiling variant: tools/build_variant.sh NAME -DSLK_WINO_V1=1 (tools/ab_wino.py).
+#if SLK_WINO_V1
 __device__ __forceinline__ void wf_dma_band(const float* __restrict__ act, int u, const float* dst, int wave, int lane) {
     const int b = u / 3, band = u - 3 * (u / 3);
     const float* src = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
@@ -382,6 +385,7 @@ extern "C" int slk_conv2_fwd_pool_v1(const float* act, const float* W2, const fl
     return slk_launch_status();
 }
 
+#endif  // SLK_WINO_V1
 // ============================================================================ shared helpers
 // 4x4 patch of a row-major LDS image (row stride A_HW floats) as 8 ds_read_b64, as row pairs
 __device__ __forceinline__ void lds_patch_pk(const float* ps, f2 (&lo)[4], f2 (&hi)[4]) {
@@ -853,7 +857,8 @@ constexpr int WW_LUTS = SLK_WW_LUTS;                  // ZT row stride in floats
 // reads (code 0), 2 = no dpooled reads, 4 = no ZT reads, 8 = code as a dword read + byte extract,
 // 16 = no DMA / wait / barrier in the unit loop, 32 = no act patch transform (raw patch as operand),
 // 64 = no MFMA (operands kept alive), 128 = no barrier per unit, 256 = no DMA issue per unit,
-// 512 = clock diagnostic: slab[0] of each workgroup = its mean shader clock in GHz.
+// 512 = clock diagnostic: slab[0] of each workgroup = its mean shader clock in GHz, 1024 = every DMA
+// re-fetches the workgroup's first unit (L2-resident source: DMA mechanism vs memory traffic).
 #ifndef SLK_WW_ABL
 #define SLK_WW_ABL 0
 #endif
@@ -890,6 +895,7 @@ static_assert(WW_DP_OFF * 4 == WF_CHUNKS * 1024 && WW_CD_OFF * 4 == (WF_CHUNKS +
 __device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const float* __restrict__ dpool,
                                             const uint8_t* __restrict__ code, int u, const float* dst, int wave,
                                             int lane, int i0 = 0, int i1 = 1 << 20) {
+    if (SLK_WW_ABL & 1024) u = blockIdx.x;
     const int b = u / 3, band = u - 3 * (u / 3);
     const uint32_t base = (uint32_t)(uintptr_t)dst;
     const float* asrc = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
