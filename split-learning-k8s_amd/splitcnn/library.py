@@ -1,0 +1,212 @@
+"""torch.library registration of the split-CNN kernels (namespace ``splitcnn``).
+
+Every op here is a functional wrapper over one libslk.so entry point (ops.py), registered with
+``torch.library.custom_op`` so that the drop-in modules (model_def.py) are visible to the PyTorch
+stack as opaque, differentiable operators rather than as Python autograd.Functions: each op has a
+fake (meta) kernel, so ``torch.export`` / ``make_fx`` / ``torch.compile`` can trace a module without
+running it, and the forward ops register their backward through other ``splitcnn`` ops, so the
+traced backward graph is made of them too. The real kernels run only on a ROCm device (ops.py raises
+otherwise); there is no CPU implementation.
+
+The ops and the reference calls they replace (src/model_def.py, src/server_part.py):
+  conv1_relu(x, W1, b1) -> act                              ModelPartA.forward (model_def.py:11-12)
+  conv2_relu_pool(act, W2, b2) -> (pooled, code)            model_def.py:25-26
+  linear(flat, W3, b3) -> logits                            fc1 (model_def.py:22,28)
+  cross_entropy(logits, labels) -> loss                     nn.CrossEntropyLoss() (server_part.py:16,49)
+and their backward helpers conv1_wgrad, conv2_dgrad, conv2_wgrad, linear_dgrad, linear_wgrad,
+cross_entropy_grad.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from . import ops
+
+_NS = "splitcnn"
+
+
+# ----------------------------------------------------------------------------------- conv1 + ReLU
+@torch.library.custom_op(f"{_NS}::conv1_relu", mutates_args=())
+def conv1_relu(x: Tensor, W1: Tensor, b1: Tensor) -> Tensor:
+    return ops.conv1_fwd(x.contiguous(), W1.contiguous(), b1.contiguous())
+
+
+@conv1_relu.register_fake
+def _(x, W1, b1):
+    return x.new_empty((x.shape[0], 32, 26, 26))
+
+
+@torch.library.custom_op(f"{_NS}::conv1_wgrad", mutates_args=())
+def conv1_wgrad(x: Tensor, act: Tensor, g: Tensor) -> Tensor:
+    """[dW1 (288) | db1 (32)] of relu(conv1(x)) for the output gradient g (mask act > 0)."""
+    return ops.reduce_slabs(ops.conv1_wgrad_slabs(x.contiguous(), act.contiguous(), g.contiguous()))
+
+
+@conv1_wgrad.register_fake
+def _(x, act, g):
+    return x.new_empty((ops.CLIENT_NPARAM,))
+
+
+def _conv1_setup(ctx, inputs, output):
+    x, _W1, _b1 = inputs
+    ctx.save_for_backward(x, output)
+
+
+def _conv1_backward(ctx, g):
+    x, act = ctx.saved_tensors
+    if ctx.needs_input_grad[0]:
+        raise NotImplementedError(
+            "splitcnn: gradient w.r.t. the client INPUT images is not part of the split step "
+            "(the reference's data never requires grad, src/client_part.py:110-114)")
+    flat = torch.ops.splitcnn.conv1_wgrad(x, act, g)
+    return None, flat[:288].view(32, 1, 3, 3), flat[288:].view(32)
+
+
+conv1_relu.register_autograd(_conv1_backward, setup_context=_conv1_setup)
+
+
+# ----------------------------------------------------------------------------------- conv2 + ReLU + pool
+@torch.library.custom_op(f"{_NS}::conv2_relu_pool", mutates_args=())
+def conv2_relu_pool(act: Tensor, W2: Tensor, b2: Tensor) -> Tuple[Tensor, Tensor]:
+    return ops.conv2_fwd_pool(act.contiguous(), W2.contiguous(), b2.contiguous())
+
+
+@conv2_relu_pool.register_fake
+def _(act, W2, b2):
+    B = act.shape[0]
+    return act.new_empty((B, 64, 12, 12)), act.new_empty((B, 64, 12, 12), dtype=torch.uint8)
+
+
+@torch.library.custom_op(f"{_NS}::conv2_dgrad", mutates_args=())
+def conv2_dgrad(dpooled: Tensor, code: Tensor, W2: Tensor) -> Tensor:
+    """Cut gradient: conv2 input gradient of the pool/ReLU-routed dpooled."""
+    return ops.conv2_dgrad(dpooled.contiguous(), code.contiguous(), W2.contiguous())
+
+
+@conv2_dgrad.register_fake
+def _(dpooled, code, W2):
+    return dpooled.new_empty((dpooled.shape[0], 32, 26, 26))
+
+
+@torch.library.custom_op(f"{_NS}::conv2_wgrad", mutates_args=())
+def conv2_wgrad(act: Tensor, dpooled: Tensor, code: Tensor) -> Tensor:
+    """[dW2 (18432) | db2 (64)]."""
+    return ops.reduce_slabs(ops.conv2_wgrad_slabs(act.contiguous(), dpooled.contiguous(), code.contiguous()))
+
+
+@conv2_wgrad.register_fake
+def _(act, dpooled, code):
+    return act.new_empty((ops.CONV2_SLAB,))
+
+
+def _conv2_setup(ctx, inputs, output):
+    act, W2, _b2 = inputs
+    _pooled, code = output
+    ctx.save_for_backward(act, code, W2)
+    ctx.mark_non_differentiable(code)
+
+
+def _conv2_backward(ctx, dpooled, _dcode):
+    act, code, W2 = ctx.saved_tensors
+    gact = torch.ops.splitcnn.conv2_dgrad(dpooled, code, W2) if ctx.needs_input_grad[0] else None
+    dW2 = db2 = None
+    if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        flat = torch.ops.splitcnn.conv2_wgrad(act, dpooled, code)
+        dW2, db2 = flat[:18432].view(64, 32, 3, 3), flat[18432:].view(64)
+    return gact, dW2, db2
+
+
+conv2_relu_pool.register_autograd(_conv2_backward, setup_context=_conv2_setup)
+
+
+# ----------------------------------------------------------------------------------- fc1
+@torch.library.custom_op(f"{_NS}::linear", mutates_args=())
+def linear(flat: Tensor, W3: Tensor, b3: Tensor) -> Tensor:
+    return ops.fc_fwd(flat.contiguous(), W3.contiguous(), b3.contiguous())
+
+
+@linear.register_fake
+def _(flat, W3, b3):
+    return flat.new_empty((flat.shape[0], 10))
+
+
+@torch.library.custom_op(f"{_NS}::linear_dgrad", mutates_args=())
+def linear_dgrad(dlogits: Tensor, W3: Tensor) -> Tensor:
+    return ops.fc_dgrad(dlogits.contiguous(), W3.contiguous())
+
+
+@linear_dgrad.register_fake
+def _(dlogits, W3):
+    return dlogits.new_empty((dlogits.shape[0], 9216))
+
+
+@torch.library.custom_op(f"{_NS}::linear_wgrad", mutates_args=())
+def linear_wgrad(dlogits: Tensor, flat: Tensor) -> Tensor:
+    """[dW3 (92160) | db3 (10)]."""
+    return ops.reduce_slabs(ops.fc_wgrad_slabs(dlogits.contiguous(), flat.contiguous()))
+
+
+@linear_wgrad.register_fake
+def _(dlogits, flat):
+    return dlogits.new_empty((ops.FC_SLAB,))
+
+
+def _linear_setup(ctx, inputs, output):
+    flat, W3, _b3 = inputs
+    ctx.save_for_backward(flat, W3)
+
+
+def _linear_backward(ctx, dlogits):
+    flat, W3 = ctx.saved_tensors
+    dflat = torch.ops.splitcnn.linear_dgrad(dlogits, W3) if ctx.needs_input_grad[0] else None
+    dW3 = db3 = None
+    if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        g = torch.ops.splitcnn.linear_wgrad(dlogits, flat)
+        dW3, db3 = g[:92160].view(10, 9216), g[92160:].view(10)
+    return dflat, dW3, db3
+
+
+linear.register_autograd(_linear_backward, setup_context=_linear_setup)
+
+
+# ----------------------------------------------------------------------------------- cross-entropy
+@torch.library.custom_op(f"{_NS}::cross_entropy", mutates_args=())
+def cross_entropy(logits: Tensor, labels: Tensor) -> Tensor:
+    """Mean cross-entropy (nn.CrossEntropyLoss(), integer labels) as a 0-d tensor."""
+    logits = logits.contiguous()
+    loss_i, _ = ops.xent_fwd_bwd(logits, labels.contiguous(), 1.0 / logits.shape[0])
+    return ops.loss_mean(loss_i).view(())
+
+
+@cross_entropy.register_fake
+def _(logits, labels):
+    return logits.new_empty(())
+
+
+@torch.library.custom_op(f"{_NS}::cross_entropy_grad", mutates_args=())
+def cross_entropy_grad(logits: Tensor, labels: Tensor, gloss: Tensor) -> Tensor:
+    """d loss / d logits = (softmax - onehot) / B * gloss (the fused kernel, then the upstream scale)."""
+    logits = logits.contiguous()
+    _, dlogits = ops.xent_fwd_bwd(logits, labels.contiguous(), 1.0 / logits.shape[0])
+    return dlogits * gloss
+
+
+@cross_entropy_grad.register_fake
+def _(logits, labels, gloss):
+    return torch.empty_like(logits)
+
+
+def _xent_setup(ctx, inputs, output):
+    logits, labels = inputs
+    ctx.save_for_backward(logits, labels)
+
+
+def _xent_backward(ctx, gloss):
+    logits, labels = ctx.saved_tensors
+    return torch.ops.splitcnn.cross_entropy_grad(logits, labels, gloss), None
+
+
+cross_entropy.register_autograd(_xent_backward, setup_context=_xent_setup)

@@ -120,3 +120,56 @@ def test_library_build_id_matches_tree():
     lib = _lib.load()
     assert lib.slk_build_id().decode() == build.source_hash() == build.library_build_id()
     assert not build.needs_build()
+
+
+def test_modules_export_as_splitcnn_custom_ops():
+    """torch.library registration (splitcnn/library.py): the drop-in modules trace under
+    torch.export with fake CUDA inputs (no GPU needed, fake kernels give the shapes); the exported
+    graph holds only splitcnn:: ops plus views — no aten conv / linear / loss."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from splitcnn.model_def import CrossEntropyLoss, FullModel
+
+    class Step(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.m, self.ce = FullModel(), CrossEntropyLoss()
+
+        def forward(self, x, y):
+            return self.ce(self.m(x), y)
+
+    with FakeTensorMode():
+        x = torch.empty(4, 1, 28, 28, device="cuda")
+        y = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ep = torch.export.export(Step().to("meta"), (x, y), strict=False)
+    targets = [str(n.target) for n in ep.graph.nodes if n.op == "call_function"]
+    assert [t for t in targets if t.startswith("splitcnn.")] == [
+        "splitcnn.conv1_relu.default", "splitcnn.conv2_relu_pool.default", "splitcnn.linear.default",
+        "splitcnn.cross_entropy.default"]
+    assert all(t.startswith("splitcnn.") or t in ("aten.view.default", "<built-in function getitem>") for t in targets)
+    loss = [n for n in ep.graph.nodes if n.op == "output"][0].args[0][0]
+    assert tuple(loss.meta["val"].shape) == ()
+
+
+def test_custom_op_fake_kernels_shapes():
+    """Every splitcnn op's fake kernel returns the shapes/dtypes the real kernel writes."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from splitcnn import library  # noqa: F401
+    O = torch.ops.splitcnn
+    with FakeTensorMode():
+        x = torch.empty(3, 1, 28, 28, device="cuda")
+        act = O.conv1_relu(x, torch.empty(32, 1, 3, 3, device="cuda"), torch.empty(32, device="cuda"))
+        pooled, code = O.conv2_relu_pool(act, torch.empty(64, 32, 3, 3, device="cuda"), torch.empty(64, device="cuda"))
+        flat = pooled.view(3, 9216)
+        logits = O.linear(flat, torch.empty(10, 9216, device="cuda"), torch.empty(10, device="cuda"))
+        y = torch.zeros(3, dtype=torch.int64, device="cuda")
+        got = {"act": act, "pooled": pooled, "code": code, "logits": logits,
+               "loss": O.cross_entropy(logits, y), "dlogits": O.cross_entropy_grad(logits, y, logits.new_ones(())),
+               "dflat": O.linear_dgrad(logits, torch.empty(10, 9216, device="cuda")),
+               "g3": O.linear_wgrad(logits, flat), "cut": O.conv2_dgrad(pooled, code, torch.empty(64, 32, 3, 3, device="cuda")),
+               "g2": O.conv2_wgrad(act, pooled, code), "g1": O.conv1_wgrad(x, act, act)}
+    want = {"act": (3, 32, 26, 26), "pooled": (3, 64, 12, 12), "code": (3, 64, 12, 12), "logits": (3, 10),
+            "loss": (), "dlogits": (3, 10), "dflat": (3, 9216), "g3": (92170,), "cut": (3, 32, 26, 26),
+            "g2": (18496,), "g1": (320,)}
+    for k, shp in want.items():
+        assert tuple(got[k].shape) == shp, k
+        assert got[k].dtype == (torch.uint8 if k == "code" else torch.float32), k

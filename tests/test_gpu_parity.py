@@ -354,3 +354,34 @@ def test_slab_reduction_both_orders_vs_float64(gpu, nslab):
     grad = torch.empty(n, device=gpu)
     ops.sgd_from_slabs(param, grad, slabs, 0.5)
     assert torch.equal(grad, got) and torch.equal(param, -0.5 * got)
+
+
+def test_traced_step_runs_the_custom_ops(gpu):
+    """make_fx of a full split step (forward, CE, autograd backward) over the drop-in modules: the
+    traced graph's forward AND backward are splitcnn:: ops (library.py), and running the traced graph
+    gives the eager step's loss and gradients bit for bit."""
+    from torch.fx.experimental.proxy_tensor import make_fx
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.model_def import CrossEntropyLoss
+    full = init_models(seed=4, full=True).to(gpu)
+    names = [n for n, _ in full.named_parameters()]
+    ce = CrossEntropyLoss()
+
+    def step(x, y, *params):
+        out = torch.func.functional_call(full, dict(zip(names, params)), (x,))
+        loss = ce(out, y)
+        return (loss, *torch.autograd.grad(loss, params))
+
+    x, y = SyntheticMNIST(3).batch(6)
+    x, y = x.to(gpu), y.to(gpu)
+    params = [p.detach().clone().requires_grad_(True) for p in full.parameters()]
+    gm = make_fx(step, tracing_mode="fake")(x, y, *params)
+    targets = {str(n.target) for n in gm.graph.nodes if n.op == "call_function"}
+    for op in ("conv1_relu", "conv2_relu_pool", "linear", "cross_entropy", "cross_entropy_grad", "linear_dgrad",
+               "linear_wgrad", "conv2_dgrad", "conv2_wgrad", "conv1_wgrad"):
+        assert f"splitcnn.{op}.default" in targets, op
+    assert not any("convolution" in t or "addmm" in t or "nll_loss" in t for t in targets)
+    got = gm(x, y, *params)
+    want = step(x, y, *params)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
