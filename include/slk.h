@@ -229,6 +229,14 @@ int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, co
 int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogits, const int* step, unsigned seed,
                       unsigned keep_threshold, float keep_scale, uint16_t* dcut, float* slabs, int b0, int B,
                       void* stream);
+/* slk_wide_head for the fused 1-GPU step: identical, except that the cut gradient is not written as
+ * dcut but directly as the client's conv3 output gradient dc3 = max-pool backward by code3 (bit for bit
+ * slk_wide_unpool(dcut, code3)): the unpool pass and the dcut round trip disappear when server and
+ * client share the device. b0 = 0. */
+int slk_wide_head_dc3(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
+                      unsigned seed, unsigned keep_threshold, float keep_scale, float grad_scale, float* logits,
+                      float* loss_i, float* dlogits, const uint8_t* code3, uint16_t* dc3, float* slabs, float* work,
+                      int* err_flag, int B, void* stream);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
  * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
  * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs

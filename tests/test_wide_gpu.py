@@ -318,16 +318,16 @@ def test_wide_modules_run_the_reference_step_code(gpu):
     every weight gradient equal the fused WideTrainer step's; Adam (torch's own here) matches the
     torch formula on those gradients; WideFullModel's forward/backward equals the split modules'."""
     from splitcnn.model_def import CrossEntropyLoss
-    from splitcnn.wide import (CUT_SHAPE, SyntheticCIFAR, WideFullModel, WideTrainer, c8_to_nchw,
-                               init_wide_models)
+    from splitcnn.wide import SyntheticCIFAR, WideFullModel, WideTrainer, c8_to_nchw, init_wide_models
     B = 8
     x, y = SyntheticCIFAR(4).batch(B)
     x, y = x.to(gpu), y.to(gpu)
     ref = WideTrainer(*init_wide_models(seed=0), device=gpu, graph=False)
-    ref.step(x, y)
+    cut_r = ref.client.forward(x)           # the stage path (dcut returned to the client)
+    dcut_r, _ = ref.server.step_request(cut_r, y)
+    ref.client.backward_step(dcut_r)
     torch.cuda.synchronize()
-    ref_cut = c8_to_nchw(ref.client._buf.get("cut", (B,) + CUT_SHAPE, torch.bfloat16, ref.device))
-    ref_dcut = c8_to_nchw(ref.server._buf.get("dcut", (B,) + CUT_SHAPE, torch.bfloat16, ref.device))
+    ref_cut, ref_dcut = c8_to_nchw(cut_r), c8_to_nchw(dcut_r)
     (_, ref_loss), = ref.loss_log.flush()
 
     client_m, server_m = init_wide_models(seed=0)
@@ -390,3 +390,26 @@ def test_wide_modules_run_the_reference_step_code(gpu):
         e1 = server_m(client_activations)
         e2 = server_m(client_activations)
     assert torch.equal(e1, e2)
+
+
+def test_fused_head_to_dc3_equals_stage_path(gpu):
+    """WideTrainer's fused step (slk_wide_head_dc3: the head writes the client's unpooled conv3
+    gradient, no dcut, no unpool pass) equals the stage path (step_request -> dcut -> unpool ->
+    client backward) bit for bit over 3 Adam steps at a ragged batch."""
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    data = SyntheticCIFAR(13)
+    batches = [data.batch(19) for _ in range(3)]
+    fused = WideTrainer(*init_wide_models(seed=2), device=gpu, graph=False)
+    staged = WideTrainer(*init_wide_models(seed=2), device=gpu, graph=False)
+    for x, y in batches:
+        x, y = x.to(gpu), y.to(gpu)
+        fused.step(x, y)
+        cut = staged.client.forward(x)
+        dcut, _ = staged.server.step_request(cut, y)
+        staged.client.backward_step(dcut)
+    torch.cuda.synchronize()
+    for a, b in ((fused.client.params, staged.client.params), (fused.client.m, staged.client.m),
+                 (fused.client.v, staged.client.v), (fused.server.params, staged.server.params),
+                 (fused.client.grads, staged.client.grads), (fused.server.grads, staged.server.grads)):
+        assert torch.equal(a, b)
+    assert [l for _, l in fused.loss_log.flush()] == [l for _, l in staged.loss_log.flush()]
