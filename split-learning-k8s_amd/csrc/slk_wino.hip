@@ -610,6 +610,11 @@ constexpr int WD_CD_CH = P_SAMPLE / 1024;      // 9 KiB chunks of code
 constexpr int WD_BSTR = WD_CD_OFF + P_SAMPLE / 4 + 64;   // 11648 floats = 46,592 B per buffer
 constexpr int WD_XCH = 2 * 2 * 4 * 64 * 4;     // per parity: [group slot][writer kh][r][lane] float4
 constexpr int WD_GRID = 256;
+// Profiling-only ablation bits (tools/build_variant.sh -DSLK_WD_ABL=...; outputs wrong): 1 = no sample
+// DMA after the first two, 2 = no exchange barrier, 4 = no cut-gradient stores, 8 = no LUT reads.
+#ifndef SLK_WD_ABL
+#define SLK_WD_ABL 0
+#endif
 
 __device__ __forceinline__ void wd_dma_sample(const float* __restrict__ dpool, const uint8_t* __restrict__ code, int b,
                                               const float* dst, int wave, int lane) {
@@ -682,7 +687,8 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
         // every tile before this iteration was read before the previous iteration's exchange
         // barrier: sample next_dma - 2 is free once its last tile is behind us
         if (next_dma < nloc && WD_NT * (next_dma - 1) <= 32 * it) {
-            wd_dma_sample(dpool, code, b + next_dma * (int)gridDim.x, smem + (next_dma & 1) * WD_BSTR, wu, lane);
+            if (!(SLK_WD_ABL & 1))
+                wd_dma_sample(dpool, code, b + next_dma * (int)gridDim.x, smem + (next_dma & 1) * WD_BSTR, wu, lane);
             ++next_dma;
         }
         const int p = it;
@@ -723,7 +729,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             // earlier), so the dependent LDS read is not exposed in front of the expansion
             auto lutload = [&](const int (&c)[4], float4 (&E)[4]) {
 #pragma unroll
-                for (int w = 0; w < 4; ++w) E[w] = lutw[w][c[w]];
+                for (int w = 0; w < 4; ++w) E[w] = (SLK_WD_ABL & 8) ? make_float4((float)c[w], 0.f, 1.f, 0.f) : lutw[w][c[w]];
             };
             auto expand = [&](const float (&v)[4], const float4 (&E)[4], f2 (&v01)[4], f2 (&v23)[4]) {
                 f2 Rlo[4], Rhi[4];
@@ -791,7 +797,10 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             // kh = 1 ci 16..31 — slot 0 is always the wave's own block: no selects on kh)
 #pragma unroll
             for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
-            lds_barrier();
+            if (SLK_WD_ABL & 2)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            else
+                lds_barrier();
             auto finish = [&](const f2 (&ym)[2][4], int mb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -799,7 +808,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                     const float4 tot = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
                     const int ci = 16 * mb + 4 * lk + r;
                     float* op = gsm + ci * A_PIX + 2 * ty * A_HW + 2 * tx;
-                    if (valid) {
+                    if (valid && !((SLK_WD_ABL & 4) && tot.x != 12345.f)) {
                         *reinterpret_cast<f2*>(op) = f2{tot.x, tot.y};
                         *reinterpret_cast<f2*>(op + A_HW) = f2{tot.z, tot.w};
                     }
