@@ -86,13 +86,17 @@ def cpu_baseline(seconds: float):
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         model = "?"
+    aff = d.get("affinity_cpus") or d.get("nproc")
     return {"value": round(d["value"], 1), "unit": "samples/s",
-            "cores": max(d.get("server_threads") or 1, d.get("client_threads") or 1),
+            # cores = the CPUs this job may run on (its affinity mask: what torch's threads share);
+            # the machine's nproc is larger and not available to it
+            "cores": aff,
             "kind": "port",
             "sample": f"{d['steps']} steps x B=64 in {d['seconds']:.1f}s: torch-CPU client+server processes "
                       f"over FastAPI/uvicorn + requests + pickle on localhost (src/client_part.py:103-138 <-> "
-                      f"src/server_part.py:25-58, MLflow omitted); torch threads server={d.get('server_threads')} "
-                      f"client={d.get('client_threads')}; host nproc={d.get('nproc')} ({model})"}
+                      f"src/server_part.py:25-58, MLflow omitted), both processes on the job's {aff} CPUs "
+                      f"(affinity mask) with torch threads server={d.get('server_threads')} "
+                      f"client={d.get('client_threads')}; machine nproc={d.get('nproc')} ({model})"}
 
 
 def make_pool(B, n, device, seed=42):

@@ -195,7 +195,7 @@ def main(argv=None):
             srv.kill()
     out = {"value": steps * args.batch / dt, "unit": "samples/s", "steps": steps, "seconds": dt,
            "batch": args.batch, "server_threads": h.get("threads"), "client_threads": torch.get_num_threads(),
-           "nproc": os.cpu_count()}
+           "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
     if args.compute_seconds > 0:
         out["compute_only"] = compute_only(args.batch, args.compute_seconds)
     print(json.dumps(out))

@@ -283,6 +283,25 @@ def _worker(rank, world, port, topo, fixture, micro, outdir):
             res["sparams_1"] = t.server.params.cpu().numpy()
             res["bucket_1"] = t.bucket.cpu().numpy()
             res["losses"] = np.array([l for _, l in t.server.loss_log.flush()])
+        elif topo == "widehub":
+            from splitcnn.wide import SyntheticCIFAR, WideClientStage, WideServerStage, init_wide_models
+            grp = sd.client_group_for(world)
+            nc, WB = world - 1, 4
+            x, y = SyntheticCIFAR(17).batch(nc * WB)
+            x, y = x.to(dev), y.to(dev)
+            wa, wb = init_wide_models(seed=0)
+            if rank < nc:
+                t = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=grp, micro=micro)
+                sl = slice(rank * WB, (rank + 1) * WB)
+                t.client_step(x[sl].contiguous(), y[sl].contiguous())
+            else:
+                t = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=grp, micro=micro)
+                t.server_step(WB, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)
+                torch.cuda.synchronize()
+                res["losses"] = np.array([l for _, l in t.stage.loss_log.flush()])
+            torch.cuda.synchronize()
+            res["params_1"] = t.stage.params.cpu().numpy()
+            res["grads_1"] = t.stage.grads.cpu().numpy()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
     finally:
         dist.destroy_process_group()
@@ -339,3 +358,32 @@ def test_replicated_vs_fixture(gpu, tmp_path, world):
         grads = {**_split(bk[:CLIENT_N], C_OFF), **_split(bk[CLIENT_N:CLIENT_N + SERVER_N], S_OFF)}
         _check_step(fx, 1, got, prev, grads, None, None, float(o["losses"][0]))
         assert np.array_equal(o["cparams_1"], out[0]["cparams_1"]) and np.array_equal(o["sparams_1"], out[0]["sparams_1"])
+
+
+def test_widened_splitfed_hub_vs_fused_step(gpu, tmp_path):
+    """K5 SplitFed protocol (dist.WideHub: 2 client ranks -> 1 server rank, 2 micro-batches each,
+    client all-reduce) on the HIP stages vs the fused single-process widened step at the concatenated
+    batch of 8: loss 1e-6, server and (all-reduced) client gradients 1e-6 of their max (summation
+    order differs), clients identical, and every rank's Adam step = the torch formula on its gradient."""
+    from oracle import wide_step as W
+    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
+    out = _spawn(3, "widehub", "split_step_b4.npz", 2, tmp_path)
+    x, y = SyntheticCIFAR(17).batch(8)
+    ref = WideTrainer(*init_wide_models(seed=0), device=gpu, graph=False)
+    ref.step(x.to(gpu), y.to(gpu))
+    torch.cuda.synchronize()
+    (_, ref_loss), = ref.loss_log.flush()
+    assert abs(float(out[2]["losses"][0]) - ref_loss) <= 1e-6 * abs(ref_loss)
+
+    def close(g, w):
+        assert np.abs(g - w).max() <= 1e-6 * np.abs(w).max()
+    close(out[0]["grads_1"].astype(np.float64), ref.client.grads.double().cpu().numpy())
+    close(out[2]["grads_1"].astype(np.float64), ref.server.grads.double().cpu().numpy())
+    assert np.array_equal(out[0]["params_1"], out[1]["params_1"]) and np.array_equal(out[0]["grads_1"], out[1]["grads_1"])
+    wa, wb = init_wide_models(seed=0)
+    for r, model in ((0, wa), (2, wb)):
+        flat0 = np.concatenate([v.detach().double().numpy().ravel() for v in model.state_dict().values()])
+        g = out[r]["grads_1"].astype(np.float64)
+        want, _, _ = W.adam(flat0, g, np.zeros_like(g), np.zeros_like(g), 1)
+        tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
+        assert (np.abs(out[r]["params_1"].astype(np.float64) - want) <= tol).all(), r
