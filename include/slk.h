@@ -238,18 +238,20 @@ int slk_wide_head_dc3(const uint16_t* cut, const float* wf8, const float* bf, co
                       float* loss_i, float* dlogits, const uint8_t* code3, uint16_t* dc3, float* slabs, float* work,
                       int* err_flag, int B, void* stream);
 /* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
- * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dc2 = conv3 dgrad routed by code2;
- * conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs
- * [nslab][1728 + 64] (bf16(x) operand). Slabs are [dW (torch layout) | db], reduced in fixed order. */
+ * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dp2 = conv3 dgrad = the gradient of
+ * p2 at its own 16 x 16 resolution (bf16, C8); conv2's dgrad and wgrad apply conv2's max-pool backward
+ * (code2) to dp2 while staging it, so the unpooled 32 x 32 gradient is never stored; conv2 wgrad slabs
+ * [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs [nslab][1728 + 64]
+ * (bf16(x) operand). Slabs are [dW (torch layout) | db], reduced in fixed order. */
 int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream);
 int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream);
 int slk_wide_conv3_wgrad_nslab(int B);
-int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, const uint8_t* code2, uint16_t* dc2, int B,
+int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, uint16_t* dp2, int B, void* stream);
+int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
                          void* stream);
-int slk_wide_conv2_wgrad(const uint16_t* dc2, const uint16_t* a1, float* slabs, int B, void* stream);
 int slk_wide_conv2_wgrad_nslab(int B);
-int slk_wide_conv2_dgrad(const uint16_t* dc2, const uint16_t* w2d, const uint16_t* a1, uint16_t* da1m, int B,
-                         void* stream);
+int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint16_t* a1,
+                         uint16_t* da1m, int B, void* stream);
 int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream);
 int slk_wide_conv1_wgrad_nslab(int B);
 

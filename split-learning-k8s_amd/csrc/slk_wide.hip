@@ -43,6 +43,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // Profiling-only ablation bits of the non-prefetch conv loop (tools/ablate_wide.py): 1 = no DMA in
 // the loop, 2 = no MFMA, 4 = no LDS fragment reads, 8 = no waits / barriers, 16 = no weight DMA,
 // 32 = no input DMA, 64 = no epilogue. Production = 0.
+// Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
+// sample 0 (L2-resident): the HBM-read share of a kernel's time.
+#ifndef SLK_WIDE_FIXSRC
+#define SLK_WIDE_FIXSRC 0
+#endif
 #ifndef SLK_WABL
 #define SLK_WABL 0
 #endif
@@ -67,7 +72,7 @@ constexpr int IMG = 32;                 // input 3 x 32 x 32
 constexpr int C1 = 64, C2 = 128, C3 = 256;
 constexpr int CUT = C3 * 8 * 8;         // 16384 features per sample
 constexpr int NCLS = 10;
-constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_UNPOOL = 1, MODE_DGRAD_MASK = 2;
+constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_UNPOOL = 1, MODE_DGRAD_MASK = 2, MODE_DGRAD_PLAIN = 3;
 }  // namespace wide
 
 __device__ __attribute__((aligned(64))) uint32_t slk_wide_zero[64];  // zero source for halo lanes
@@ -99,7 +104,7 @@ __device__ __forceinline__ void wait_vmcnt_sat() { wait_vmcnt<(N > 63 ? 63 : N)>
 #endif
 
 // ----------------------------------------------------------------------------- conv geometry
-template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_>
+template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_, int EXP_ = 0>
 struct ConvCfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = MT_, MODE = MODE_;
     static constexpr bool K32 = false;                      // 16x16x32 kernel (wide_conv_kernel)
@@ -129,7 +134,18 @@ struct ConvCfg {
     // VMEM instructions per lane in the epilogue: stores (pooled value + code, 4 unpooled positions,
     // masked value) and the code2 / a1 words loaded at tile start. Must never over-count.
     static constexpr int EPI_ST = MODE == 1 ? 16 * FW : 4 * FW;
-    static constexpr int EPI_LD = MODE == 0 ? 0 : 4 * FW;
+    static constexpr int EPI_LD = (MODE == 0 || MODE == 3) ? 0 : 4 * FW;
+    // EXP: the input is the max-pool backward of a POOLED gradient (HW/2 x HW/2, bf16 C8) and its
+    // routing code, expanded into the LDS tile in registers (exp_load / exp_store) instead of an
+    // unpooled tensor moved by LDS-DMA: the unpooled tensor is never written nor read.
+    static constexpr bool EXP = EXP_;
+    static constexpr int XPR = TR / 2 + 2;                  // pooled rows feeding a tile (with halo)
+    static constexpr int XITEMS = 4 * XPR * (HW / 2);       // pooled chunks per 32-channel group
+    static constexpr int XR = (XITEMS + THREADS - 1) / THREADS;
+    // input VMEM instructions per wave per group issued at tap 0 (EXP: round 0's two loads; round 1,
+    // if any, is issued at tap 2 and stored at tap 4, so only 6 VGPRs of staging are live at a time)
+    static constexpr int NIN = EXP ? 2 : NDW;
+    static_assert(!EXP || XR <= 2, "EXP: at most two staging rounds");
     static_assert(MT == 128 || MT == 64, "MT");
     static_assert(HW % TR == 0 && TR % 2 == 0 && (16 * FW) % (2 * HW) == 0, "tile rows / pool pairs per wave");
     static_assert(NW >= 1 && W_SLOT % (1024 * NWV) == 0, "weight slot must split over the waves");
@@ -190,7 +206,7 @@ __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, con
                                             const int (&poff)[C::NDW], int g, char* slot, int wave, int lane) {
     const int c = wave & 3;
     const char* plane = reinterpret_cast<const char*>(in) +
-                        ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * (C::HW * C::HW)) * 16;
+                        ((size_t)((SLK_WIDE_FIXSRC ? 0 : s.n) * (C::CI / 8) + g * 4 + c) * (C::HW * C::HW)) * 16;
     const char* zero = reinterpret_cast<const char*>(slk_wide_zero);
     char* dst = slot + c * C::NPP * 16;
 #pragma unroll
@@ -198,6 +214,60 @@ __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, con
         const int d = (wave >> 2) + k * C::DSPLIT;
         const char* src = poff[k] >= 0 ? plane + (size_t)poff[k] * 16 : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + d * 1024), 16, 0, 0);
+    }
+}
+
+// EXP staging. Pooled chunk i = (plane c, pooled row pr, pooled col px) of group g: its 8 channels'
+// values and routing codes (code 0..3 = window position, 4 = ReLU-blocked). Every lane issues exactly
+// 2 XR loads (out-of-range items read the zero block), so the counted waits stay exact.
+template <class C>
+__device__ __forceinline__ void exp_load(const uint16_t* __restrict__ dp, const uint8_t* __restrict__ code,
+                                         const TileState& s, int g, int i, uint4& v, uint2& cw) {
+    constexpr int PH = C::HW / 2;
+    const int c = i / (C::XPR * PH), rem = i - c * (C::XPR * PH), pr = rem / PH, px = rem - pr * PH;
+    const int py = s.rb * (C::TR / 2) - 1 + pr;
+    const bool ok = i < C::XITEMS && py >= 0 && py < PH;
+    const size_t idx = ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * PH + (ok ? py : 0)) * PH + px;
+    v = *(ok ? reinterpret_cast<const uint4*>(dp) + idx : reinterpret_cast<const uint4*>(slk_wide_zero));
+    cw = *(ok ? reinterpret_cast<const uint2*>(code) + idx : reinterpret_cast<const uint2*>(slk_wide_zero));
+}
+
+// 16-bit lane masks of one window position: v_perm_b32 with the codes as byte selectors into the table
+// {0 (bytes 4-7), 0xFF << 8 pos (bytes 0-3)} gives 0xFF exactly where code == pos.
+__device__ __forceinline__ uint4 route_chunk(uint4 v, uint32_t cA, uint32_t cB, uint32_t cC, uint32_t cD, int pos) {
+    const uint32_t T = 0xFFu << (8 * pos);
+    return make_uint4(v.x & __builtin_amdgcn_perm(0u, T, cA), v.y & __builtin_amdgcn_perm(0u, T, cB),
+                      v.z & __builtin_amdgcn_perm(0u, T, cC), v.w & __builtin_amdgcn_perm(0u, T, cD));
+}
+
+// max-pool backward of the loaded pooled chunk i into the tile's LDS image [4][NPP][16 B]: pooled
+// (pr, px) feeds unpooled rows 2 pr - 1 + dy (tile-local, halo row 0 included) and columns 2 px + dx.
+template <class C>
+__device__ __forceinline__ void exp_store(char* slot, int i, uint4 v, uint2 cw) {
+    constexpr int PH = C::HW / 2;
+    if (i >= C::XITEMS) return;
+    const int c = i / (C::XPR * PH), rem = i - c * (C::XPR * PH), pr = rem / PH, px = rem - pr * PH;
+    const uint32_t cA = __builtin_amdgcn_perm(0u, cw.x, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw.x, 0x03030202u);
+    const uint32_t cC = __builtin_amdgcn_perm(0u, cw.y, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw.y, 0x03030202u);
+    char* base = slot + (c * C::NPP + 2 * px + 1) * 16;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+        const int ry = 2 * pr + dy - 1;
+        if (ry < 0 || ry > C::TR + 1) continue;
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx)
+            *reinterpret_cast<uint4*>(base + (ry * C::PW + dx) * 16) = route_chunk(v, cA, cB, cC, cD, 2 * dy + dx);
+    }
+}
+
+// the halo columns (x = -1, HW) of both input slots, zero for the kernel's lifetime (EXP never writes them)
+template <class C>
+__device__ __forceinline__ void exp_zero_halo(char* slots, int tid) {
+    constexpr int N = 2 * 4 * (C::TR + 2) * 2;
+    for (int k = tid; k < N; k += C::THREADS) {
+        const int side = k & 1, ry = (k >> 1) % (C::TR + 2), c = ((k >> 1) / (C::TR + 2)) & 3, sl = (k >> 1) / (4 * (C::TR + 2));
+        *reinterpret_cast<uint4*>(slots + sl * C::IN_SLOT + (c * C::NPP + ry * C::PW + side * (C::PW - 1)) * 16) =
+            make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
@@ -220,7 +290,7 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
 template <class C>
 __device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const TileState& s, int wm, int wn,
                                              int lane, uint32_t (&ecw)[4][C::FW], uint2 (&em)[4][C::FW]) {
-    if constexpr (C::MODE != wide::MODE_FWD_POOL) {
+    if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL || C::MODE == wide::MODE_DGRAD_MASK) {
         const int ch_base = s.cob * C::MT + wm * 64 + 4 * (lane >> 4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -293,11 +363,23 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     // therefore covers weight step s+1 (issued 2 steps earlier; lookahead L = 3, 4 ring slots) and,
     // at tap 8, the next group's input tile.
     static_assert(C::L == 3, "prefetch schedule assumes a weight lookahead of 3");
-    issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
+    uint4 xv;
+    uint2 xc;
+    if constexpr (C::EXP) {
+        exp_zero_halo<C>(islot0, tid);
+#pragma unroll
+        for (int r = 0; r < C::XR; ++r) {
+            exp_load<C>(in, out2, cur, 0, tid + r * C::THREADS, xv, xc);
+            exp_store<C>(islot0, tid + r * C::THREADS, xv, xc);
+        }
+    } else {
+        issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
+    }
 #pragma unroll
     for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
     if (!nxt.valid && C::S == 1) wait_vmcnt<0>();
     else wait_vmcnt<2 * C::NW>();
+    if constexpr (C::EXP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     bf16x8 av_n[4], bv_n[C::FW];
@@ -336,12 +418,16 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                         if (post) wait_vmcnt_sat<C::NW + C::EPI_ST + C::EPI_LD>();
                         else wait_vmcnt_sat<C::NW + C::EPI_LD>();
                     } else {
-                        if (post) wait_vmcnt_sat<C::NW + C::NDW + C::EPI_ST + C::EPI_LD>();
-                        else wait_vmcnt_sat<C::NW + C::NDW + C::EPI_LD>();
+                        if (post) wait_vmcnt_sat<C::NW + C::NIN + C::EPI_ST + C::EPI_LD>();
+                        else wait_vmcnt_sat<C::NW + C::NIN + C::EPI_LD>();
                     }
                 }
-                else if (tap == 1 || tap == 2) wait_vmcnt<C::NW + C::NDW>();
+                else if (tap == 1 || tap == 2) wait_vmcnt<C::NW + C::NIN>();
+                else if (C::EXP && C::XR == 2 && tap == 3) wait_vmcnt<C::NW + 2>();  // round 1's loads may fly
                 else wait_vmcnt<C::NW>();
+                // EXP: the next group's tile was written to LDS by tap 4 (each round after its loads
+                // landed); this wave's writes complete before the barrier that precedes its readers
+                if (C::EXP && tap == 5) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
@@ -351,7 +437,21 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
                     else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
                 }
-                if (tap == 0) {
+                if constexpr (C::EXP) {
+                    // next group's pooled input into the free slot: round 0 loads at tap 0 and is
+                    // expanded at tap 2, round 1 loads at tap 2 (after that) and is expanded at tap 4
+                    if (g + 1 < C::G || !tail) {
+                        const TileState& xs = g + 1 < C::G ? cur : nxt;
+                        const int xg = g + 1 < C::G ? g + 1 : 0;
+                        char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
+                        if (tap == 0) exp_load<C>(in, out2, xs, xg, tid, xv, xc);
+                        if (tap == 2) {
+                            exp_store<C>(nslot, tid, xv, xc);
+                            if (C::XR == 2) exp_load<C>(in, out2, xs, xg, tid + C::THREADS, xv, xc);
+                        }
+                        if (tap == 4 && C::XR == 2) exp_store<C>(nslot, tid + C::THREADS, xv, xc);
+                    }
+                } else if (tap == 0) {
                     char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
                     if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
                     else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
@@ -383,6 +483,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
         }
 #else
     // prologue: input group 0 of the first tile, then weight steps 0 .. L-1
+    static_assert(!C::EXP, "EXP staging needs the prefetch loop (SLK_WIDE_PF)");
     issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
 #pragma unroll
     for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
@@ -514,7 +615,12 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 }
             }
         } else if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL) {
-            const uint8_t* code = reinterpret_cast<const uint8_t*>(aux);
+            // Max-pool backward of conv2: the 4 channels' values go to the window position their
+            // code names. Round once to bf16 pairs, then mask per position with byte lookups:
+            // v_perm_b32 with the codes as selectors into the table {0, 0xFF << 8 pos} gives 0xFF
+            // exactly where code == pos (code 4, ReLU-blocked, hits the zero half). 20 VALU per
+            // (i, f) instead of ~65 compare/select/or (bit-identical: a masked-out bf16 is 0x0000,
+            // the value 0.f rounds to). The 4 stores share one address (constant offsets).
             constexpr int FH = 2 * C::HW;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -525,14 +631,32 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
                     const uint32_t cw = ecw[i][f];
+                    const uint32_t p01 = pack_bf16x2(acc[i][f][0], acc[i][f][1]);
+                    const uint32_t p23 = pack_bf16x2(acc[i][f][2], acc[i][f][3]);
+                    const uint32_t cA = __builtin_amdgcn_perm(0u, cw, 0x01010000u);  // codes (0, 0, 1, 1)
+                    const uint32_t cB = __builtin_amdgcn_perm(0u, cw, 0x03030202u);  // codes (2, 2, 3, 3)
+                    uint16_t* o = out + ((plane * FH + 2 * y) * FH + 2 * x) * 8 + (ch0 & 7);
 #pragma unroll
                     for (int pos = 0; pos < 4; ++pos) {
-                        float v[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = ((cw >> (8 * r)) & 0xFF) == (uint32_t)pos ? acc[i][f][r] : 0.f;
-                        const size_t o = ((plane * FH + 2 * y + (pos >> 1)) * FH + 2 * x + (pos & 1)) * 8 + (ch0 & 7);
-                        *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                        const uint32_t T = 0xFFu << (8 * pos);
+                        const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
+                        *reinterpret_cast<uint2*>(o + ((pos >> 1) * FH + (pos & 1)) * 8) = make_uint2(p01 & mA, p23 & mB);
                     }
+                }
+            }
+        } else if constexpr (C::MODE == wide::MODE_DGRAD_PLAIN) {
+            // the input gradient as is (bf16): conv3's dgrad writes the gradient of p2 at pooled
+            // resolution; conv2's consumers route it by code2 while staging (EXP)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ch0 = ch_base + i * 16;
+#pragma unroll
+                for (int f = 0; f < C::FW; ++f) {
+                    const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
+                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
+                    const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
+                    *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(acc[i][f][0], acc[i][f][1]),
+                                                                    pack_bf16x2(acc[i][f][2], acc[i][f][3]));
                 }
             }
         } else {
@@ -823,22 +947,24 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
 #if SLK_WIDE_K32 == 2
 using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
 using CfgConv3Fwd = Conv32Cfg<128, 256, 16, wide::MODE_FWD_POOL>;
-using CfgConv3Dgrad = Conv32Cfg<256, 128, 16, wide::MODE_DGRAD_UNPOOL>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #elif SLK_WIDE_K32 == 1
 using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
 using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #else
 using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
 using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_UNPOOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #endif
-using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4>;
+// conv3's dgrad writes dp2 (the gradient of p2, 16 x 16); conv2's dgrad and wgrad route it by code2
+// while staging (EXP), so the unpooled 32 x 32 gradient (256 KB per sample) is never materialised
+using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4, 1>;
 
 template <class C>
 static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux, uint16_t* out, uint8_t* out2,
                        int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && in && wsh && aux && out);
+    SLK_CHECK_ARG(B >= 0 && in && wsh && out && (aux || C::MODE == wide::MODE_DGRAD_PLAIN));
     if (C::MODE == wide::MODE_FWD_POOL) SLK_CHECK_ARG(out2 != nullptr);
     if (B == 0) return 0;
     const long ntiles = (long)B * C::RB * C::NCB;
@@ -866,13 +992,13 @@ extern "C" int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const
                                   uint8_t* code3, int B, void* stream) {
     return launch_conv<CfgConv3Fwd>(p2, w3f, b3, cut, code3, B, stream);
 }
-extern "C" int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, const uint8_t* code2, uint16_t* dc2,
-                                    int B, void* stream) {
-    return launch_conv<CfgConv3Dgrad>(dc3, w3d, code2, dc2, nullptr, B, stream);
+extern "C" int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, uint16_t* dp2, int B, void* stream) {
+    return launch_conv<CfgConv3Dgrad>(dc3, w3d, nullptr, dp2, nullptr, B, stream);
 }
-extern "C" int slk_wide_conv2_dgrad(const uint16_t* dc2, const uint16_t* w2d, const uint16_t* a1, uint16_t* da1m,
-                                    int B, void* stream) {
-    return launch_conv<CfgConv2Dgrad>(dc2, w2d, a1, da1m, nullptr, B, stream);
+extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint16_t* a1,
+                                    uint16_t* da1m, int B, void* stream) {
+    SLK_CHECK_ARG(code2 != nullptr);
+    return launch_conv<CfgConv2Dgrad>(dp2, w2d, a1, da1m, const_cast<uint8_t*>(code2), B, stream);
 }
 
 // ============================================================================ conv3x3 weight gradient
@@ -890,9 +1016,13 @@ extern "C" int slk_wide_conv2_dgrad(const uint16_t* dc2, const uint16_t* w2d, co
 // fixed order by slk_reduce_slabs / slk_adam_from_slabs.
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int CI_, int CO_, int HW_, int TR_>
+template <int CI_, int CO_, int HW_, int TR_, int EXP_ = 0>
 struct WgCfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, TR = TR_;
+    // EXP: dC is the max-pool backward of a pooled gradient + routing code (as ConvCfg::EXP), expanded
+    // into the dC tile in registers; the input halo tile still moves by LDS-DMA
+    static constexpr bool EXP = EXP_;
+    static constexpr int XITEMS = 16 * (TR / 2) * (HW / 2);   // pooled dC chunks per tile (16 planes)
     static constexpr int COB = 128, CIB = 64;
     static constexpr int NCOB = CO / COB, NCIB = CI / CIB, NBLK = NCOB * NCIB;
     static constexpr int NPX = TR * HW;                  // pixels per tile (K per tile)
@@ -911,12 +1041,14 @@ struct WgCfg {
     static constexpr int KSPLIT = 256 / NBLK;            // one workgroup per CU
     static_assert(NPX % 32 == 0 && (HW == 32 || HW == 16), "tile");
     static_assert(DC_BYTES % 16 == 0 && ((NPX * 16) % 1024) == 0, "dC rows move in whole KiB");
+    static_assert(!EXP || (XITEMS == 512 && NCOB == 1), "EXP: one pooled chunk per thread, one co block");
 };
 
 template <class C>
 __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __restrict__ dc,
                                                             const uint16_t* __restrict__ in,
-                                                            float* __restrict__ slabs, int B) {
+                                                            float* __restrict__ slabs, int B,
+                                                            const uint8_t* __restrict__ dcode = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -962,17 +1094,37 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         tile_of(t, n, rb);
         return n < B;
     };
+    // EXP: pooled dC chunk tid = (plane c, pooled row pr, pooled col px) of tile t
+    auto exp_load_dc = [&](int t, uint4& v, uint2& cw) {
+        int n, rb;
+        tile_of(t, n, rb);
+        constexpr int PH = C::HW / 2, PR = C::TR / 2;
+        const int c = tid / (PR * PH), rem = tid - c * (PR * PH), pr = rem / PH, px = rem - pr * PH;
+        const size_t idx = ((size_t)(n * (C::CO / 8) + c) * PH + rb * PR + pr) * PH + px;
+        v = reinterpret_cast<const uint4*>(dc)[idx];
+        cw = reinterpret_cast<const uint2*>(dcode)[idx];
+    };
+    auto exp_store_dc = [&](char* buf, uint4 v, uint2 cw) {
+        constexpr int PH = C::HW / 2, PR = C::TR / 2;
+        const int c = tid / (PR * PH), rem = tid - c * (PR * PH), pr = rem / PH, px = rem - pr * PH;
+        const uint32_t cA = __builtin_amdgcn_perm(0u, cw.x, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw.x, 0x03030202u);
+        const uint32_t cC = __builtin_amdgcn_perm(0u, cw.y, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw.y, 0x03030202u);
+        char* base = buf + (c * C::NPXP + 2 * pr * C::HW + 2 * px) * 16;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos)
+            *reinterpret_cast<uint4*>(base + ((pos >> 1) * C::HW + (pos & 1)) * 16) = route_chunk(v, cA, cB, cC, cD, pos);
+    };
     auto issue_tile = [&](int t, char* buf) {
         int n, rb;
         tile_of(t, n, rb);
         // dC rows: 16 chunk planes x (NPX*16/1024) KiB, 4 pieces per wave
         constexpr int PPC = C::NPX * 16 / 1024;
 #pragma unroll
-        for (int k = 0; k < (16 * PPC) / 8; ++k) {
+        for (int k = 0; k < (C::EXP ? 0 : (16 * PPC) / 8); ++k) {
             const int piece = wave * ((16 * PPC) / 8) + k;
             const int c = piece / PPC, part = piece - (piece / PPC) * PPC;
             const char* src = reinterpret_cast<const char*>(dc) +
-                              (((size_t)(n * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
+                              (((size_t)((SLK_WIDE_FIXSRC ? 0 : n) * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
                               part * 1024 + lane * 16;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + c * C::NPXP * 16 + part * 1024), 16, 0, 0);
         }
@@ -992,13 +1144,26 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     };
 
     int t = ks, b = 0;
-    if (valid(t)) issue_tile(t, smem);
+    uint4 xv;
+    uint2 xc;
+    if (valid(t)) {
+        issue_tile(t, smem);
+        if constexpr (C::EXP) {
+            exp_load_dc(t, xv, xc);
+            exp_store_dc(smem, xv, xc);
+        }
+    }
 #pragma unroll 1
     for (; valid(t); t += C::KSPLIT) {
         wait_vmcnt<0>();
+        if constexpr (C::EXP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // dC tile written
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (valid(t + C::KSPLIT)) issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
+        const bool more = valid(t + C::KSPLIT);
+        if (more) {
+            issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
+            if constexpr (C::EXP) exp_load_dc(t + C::KSPLIT, xv, xc);
+        }
         const char* buf = smem + b * C::BUF;
 #pragma unroll
         for (int j = 0; j < C::KS; ++j) {
@@ -1028,6 +1193,10 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
                 for (int i = 0; i < 4; ++i) acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][u], 0, 0, 0);
             }
         }
+        // EXP: the next tile's dC, routed into the other buffer (free since this tile's barrier)
+        if constexpr (C::EXP) {
+            if (more) exp_store_dc(smem + (b ^ 1) * C::BUF, xv, xc);
+        }
         b ^= 1;
     }
 
@@ -1052,20 +1221,22 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     }
 }
 
-using CfgWg2 = WgCfg<64, 128, 32, 4>;
+using CfgWg2 = WgCfg<64, 128, 32, 4, 1>;   // dC = routed dp2 (EXP)
 using CfgWg3 = WgCfg<128, 256, 16, 8>;
 
 template <class C>
-static int launch_wgrad(const uint16_t* dc, const uint16_t* in, float* slabs, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && dc && in && slabs);
-    hipLaunchKernelGGL(wide_wgrad_kernel<C>, dim3(256), dim3(512), 0, slk_stream(stream), dc, in, slabs, B);
+static int launch_wgrad(const uint16_t* dc, const uint16_t* in, float* slabs, int B, void* stream,
+                        const uint8_t* dcode = nullptr) {
+    SLK_CHECK_ARG(B >= 0 && dc && in && slabs && (!C::EXP || dcode));
+    hipLaunchKernelGGL(wide_wgrad_kernel<C>, dim3(256), dim3(512), 0, slk_stream(stream), dc, in, slabs, B, dcode);
     return slk_launch_status();
 }
 
 extern "C" int slk_wide_conv2_wgrad_nslab(int B) { return B >= 0 ? CfgWg2::KSPLIT : 0; }
 extern "C" int slk_wide_conv3_wgrad_nslab(int B) { return B >= 0 ? CfgWg3::KSPLIT : 0; }
-extern "C" int slk_wide_conv2_wgrad(const uint16_t* dc2, const uint16_t* a1, float* slabs, int B, void* stream) {
-    return launch_wgrad<CfgWg2>(dc2, a1, slabs, B, stream);
+extern "C" int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
+                                    void* stream) {
+    return launch_wgrad<CfgWg2>(dp2, a1, slabs, B, stream, code2);
 }
 extern "C" int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream) {
     return launch_wgrad<CfgWg3>(dc3, p2, slabs, B, stream);

@@ -63,10 +63,10 @@ _SIGS = {
     "slk_wide_unpool": [_P, _P, _P, _I, _P],
     "slk_wide_conv3_wgrad": [_P, _P, _P, _I, _P],
     "slk_wide_conv3_wgrad_nslab": [_I],
-    "slk_wide_conv3_dgrad": [_P, _P, _P, _P, _I, _P],
-    "slk_wide_conv2_wgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv3_dgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv2_wgrad_nslab": [_I],
-    "slk_wide_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
+    "slk_wide_conv2_dgrad": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_conv1_wgrad": [_P, _P, _P, _I, _P],
     "slk_wide_conv1_wgrad_nslab": [_I],
     "slk_adam_from_slabs": [_P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _P, _P],

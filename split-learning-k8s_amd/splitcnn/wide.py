@@ -229,25 +229,26 @@ def client_backward_slab_shapes(B):
 
 def client_backward_kernels(dcut, saved, w2d, w3d, scratch, s1, s2, s3):
     """activations.backward(dcut) of the client stack into three slab sets [dW | db] (conv1, conv2,
-    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dc3, dc2, da1m). dcut=None:
+    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dc3, dp2, da1m) — dp2 is the
+    gradient of p2 (16 x 16; conv2's kernels route it by code2 themselves). dcut=None:
     scratch's dc3 already holds the unpooled cut gradient (slk_wide_head_dc3, the fused step)."""
     x, a1, p2, code2, code3 = saved
-    dc3, dc2, da1m = scratch
+    dc3, dp2, da1m = scratch
     B = x.shape[0]
     s = _stream(dc3)
     if dcut is not None:
         _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
         _k("wide_unpool", dcut.data_ptr(), code3.data_ptr(), dc3.data_ptr(), B, s)
     _k("wide_conv3_wgrad", dc3.data_ptr(), p2.data_ptr(), s3.data_ptr(), B, s)
-    _k("wide_conv3_dgrad", dc3.data_ptr(), w3d.data_ptr(), code2.data_ptr(), dc2.data_ptr(), B, s)
-    _k("wide_conv2_wgrad", dc2.data_ptr(), a1.data_ptr(), s2.data_ptr(), B, s)
-    _k("wide_conv2_dgrad", dc2.data_ptr(), w2d.data_ptr(), a1.data_ptr(), da1m.data_ptr(), B, s)
+    _k("wide_conv3_dgrad", dc3.data_ptr(), w3d.data_ptr(), dp2.data_ptr(), B, s)
+    _k("wide_conv2_wgrad", dp2.data_ptr(), code2.data_ptr(), a1.data_ptr(), s2.data_ptr(), B, s)
+    _k("wide_conv2_dgrad", dp2.data_ptr(), code2.data_ptr(), w2d.data_ptr(), a1.data_ptr(), da1m.data_ptr(), B, s)
     _k("wide_conv1_wgrad", x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
 
 
 def client_backward_scratch(B, get):
-    """(dc3, dc2, da1m) via get(name, shape, dtype)."""
-    return (get("dc3", (B, 32, 16, 16, 8), _BF), get("dc2", (B, 16, 32, 32, 8), _BF),
+    """(dc3, dp2, da1m) via get(name, shape, dtype)."""
+    return (get("dc3", (B, 32, 16, 16, 8), _BF), get("dp2", (B, 16, 16, 16, 8), _BF),
             get("da1m", (B, 8, 32, 32, 8), _BF))
 
 
@@ -392,7 +393,7 @@ class WideClientStage:
         scratch = client_backward_scratch(B, self._b)
         s1, s2, s3 = (self._b(n, shp, _F32) for n, shp in zip(("s1", "s2", "s3"), client_backward_slab_shapes(B)))
         client_backward_kernels(dcut, self._saved[tag], self.sh["w2d"], self.sh["w3d"], scratch, s1, s2, s3)
-        self._dc3, self._dc2, self._da1m = scratch
+        self._dc3, self._dp2, self._da1m = scratch
         return s1, s2, s3
 
     def _adam(self, lo, n, slabs):

@@ -129,9 +129,9 @@ def test_wide_step_layer_by_layer_vs_oracle(gpu):
     dcut_g = _nchw(dcut)
     dc3 = W.unpool(dcut_g, code3_gpu)
     assert np.array_equal(_nchw(c._dc3), dc3)                        # bit-exact routing
-    dc2 = W.unpool(W.conv3x3p1_dgrad(dc3, W3b), code2_gpu)
-    bf16_close(_nchw(c._dc2), bf(dc2))
-    dc2_g = _nchw(c._dc2)
+    # conv3's dgrad stores dp2, the gradient of p2 (16 x 16); conv2's kernels route it by code2
+    bf16_close(_nchw(c._dp2), bf(W.conv3x3p1_dgrad(dc3, W3b)))
+    dc2_g = W.unpool(_nchw(c._dp2), code2_gpu)
     da1 = W.conv3x3p1_dgrad(dc2_g, W2b)
     bf16_close(_nchw(c._da1m), bf(np.where(a1 > 0, da1, 0.0)))
     g = _np(c.grads)
@@ -168,13 +168,13 @@ def test_wide_large_batch_per_sample_rows_and_linearity(gpu):
     dcut = (torch.randn(B, 32, 8, 8, 8, generator=gen) * 1e-3).to(torch.bfloat16).to(gpu)
     cut = c.forward(x).clone()
     s1, s2, s3 = (t.sum(0) for t in c.backward_slabs(dcut))
-    dc2, da1m = c._dc2.clone(), c._da1m.clone()
+    dp2, da1m = c._dp2.clone(), c._da1m.clone()
     parts = []
     for lo, hi in ((0, 4), (4, 260), (260, 516), (516, 520)):
         cut_p = c.forward(x[lo:hi].contiguous()).clone()
         assert torch.equal(cut_p, cut[lo:hi]), (lo, hi)
         t1, t2, t3 = (t.sum(0) for t in c.backward_slabs(dcut[lo:hi].contiguous()))
-        assert torch.equal(c._dc2, dc2[lo:hi]) and torch.equal(c._da1m, da1m[lo:hi]), (lo, hi)
+        assert torch.equal(c._dp2, dp2[lo:hi]) and torch.equal(c._da1m, da1m[lo:hi]), (lo, hi)
         parts.append((t1, t2, t3))
     for k, tot in enumerate((s1, s2, s3)):
         acc = sum(p[k].double() for p in parts)
