@@ -229,24 +229,18 @@ int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, co
 int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogits, const int* step, unsigned seed,
                       unsigned keep_threshold, float keep_scale, uint16_t* dcut, float* slabs, int b0, int B,
                       void* stream);
-/* slk_wide_head for the fused 1-GPU step: identical, except that the cut gradient is not written as
- * dcut but directly as the client's conv3 output gradient dc3 = max-pool backward by code3 (bit for bit
- * slk_wide_unpool(dcut, code3)): the unpool pass and the dcut round trip disappear when server and
- * client share the device. b0 = 0. */
-int slk_wide_head_dc3(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
-                      unsigned seed, unsigned keep_threshold, float keep_scale, float grad_scale, float* logits,
-                      float* loss_i, float* dlogits, const uint8_t* code3, uint16_t* dc3, float* slabs, float* work,
-                      int* err_flag, int B, void* stream);
-/* Client backward (activations.backward(grads), client_part.py:132): dc3 = max-pool backward of the
- * cut gradient (code3); conv3 wgrad slabs [nslab][294912 + 256]; dp2 = conv3 dgrad = the gradient of
+/* Client backward (activations.backward(grads), client_part.py:132), with no unpooled gradient ever
+ * stored: conv3's wgrad and dgrad apply conv3's max-pool backward (code3) to the POOLED cut gradient
+ * dcut while staging it; conv3 wgrad slabs [nslab][294912 + 256]; dp2 = conv3 dgrad = the gradient of
  * p2 at its own 16 x 16 resolution (bf16, C8); conv2's dgrad and wgrad apply conv2's max-pool backward
- * (code2) to dp2 while staging it, so the unpooled 32 x 32 gradient is never stored; conv2 wgrad slabs
- * [nslab][73728 + 128]; da1m = conv2 dgrad masked by a1 > 0; conv1 wgrad slabs [nslab][1728 + 64]
- * (bf16(x) operand). Slabs are [dW (torch layout) | db], reduced in fixed order. */
-int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream);
-int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream);
+ * (code2) to dp2 the same way; conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by
+ * a1 > 0; conv1 wgrad slabs [nslab][1728 + 64] (bf16(x) operand). Slabs are [dW (torch layout) | db],
+ * reduced in fixed order. */
+int slk_wide_conv3_wgrad(const uint16_t* dcut, const uint8_t* code3, const uint16_t* p2, float* slabs, int B,
+                         void* stream);
 int slk_wide_conv3_wgrad_nslab(int B);
-int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, uint16_t* dp2, int B, void* stream);
+int slk_wide_conv3_dgrad(const uint16_t* dcut, const uint8_t* code3, const uint16_t* w3d, uint16_t* dp2, int B,
+                         void* stream);
 int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
                          void* stream);
 int slk_wide_conv2_wgrad_nslab(int B);

@@ -947,18 +947,17 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
 #if SLK_WIDE_K32 == 2
 using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
 using CfgConv3Fwd = Conv32Cfg<128, 256, 16, wide::MODE_FWD_POOL>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #elif SLK_WIDE_K32 == 1
 using CfgConv2Fwd = Conv32Cfg<64, 128, 32, wide::MODE_FWD_POOL>;
 using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #else
 using CfgConv2Fwd = ConvCfg<64, 128, 32, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
 using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW, SLK_WIDE_NWV>;
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV>;
 #endif
-// conv3's dgrad writes dp2 (the gradient of p2, 16 x 16); conv2's dgrad and wgrad route it by code2
-// while staging (EXP), so the unpooled 32 x 32 gradient (256 KB per sample) is never materialised
+// Backward: no unpooled gradient is ever materialised. conv3's dgrad and wgrad read the pooled cut
+// gradient dcut + code3 and route it while staging (EXP); conv3's dgrad writes dp2 (the gradient of
+// p2, 16 x 16), which conv2's dgrad and wgrad route by code2 the same way.
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV, 1>;
 using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4, 1>;
 
 template <class C>
@@ -992,8 +991,10 @@ extern "C" int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const
                                   uint8_t* code3, int B, void* stream) {
     return launch_conv<CfgConv3Fwd>(p2, w3f, b3, cut, code3, B, stream);
 }
-extern "C" int slk_wide_conv3_dgrad(const uint16_t* dc3, const uint16_t* w3d, uint16_t* dp2, int B, void* stream) {
-    return launch_conv<CfgConv3Dgrad>(dc3, w3d, nullptr, dp2, nullptr, B, stream);
+extern "C" int slk_wide_conv3_dgrad(const uint16_t* dcut, const uint8_t* code3, const uint16_t* w3d, uint16_t* dp2,
+                                    int B, void* stream) {
+    SLK_CHECK_ARG(code3 != nullptr);
+    return launch_conv<CfgConv3Dgrad>(dcut, w3d, nullptr, dp2, const_cast<uint8_t*>(code3), B, stream);
 }
 extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint16_t* a1,
                                     uint16_t* da1m, int B, void* stream) {
@@ -1041,7 +1042,7 @@ struct WgCfg {
     static constexpr int KSPLIT = 256 / NBLK;            // one workgroup per CU
     static_assert(NPX % 32 == 0 && (HW == 32 || HW == 16), "tile");
     static_assert(DC_BYTES % 16 == 0 && ((NPX * 16) % 1024) == 0, "dC rows move in whole KiB");
-    static_assert(!EXP || (XITEMS == 512 && NCOB == 1), "EXP: one pooled chunk per thread, one co block");
+    static_assert(!EXP || XITEMS == 512, "EXP: one pooled chunk per thread");
 };
 
 template <class C>
@@ -1100,7 +1101,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         tile_of(t, n, rb);
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
         const int c = tid / (PR * PH), rem = tid - c * (PR * PH), pr = rem / PH, px = rem - pr * PH;
-        const size_t idx = ((size_t)(n * (C::CO / 8) + c) * PH + rb * PR + pr) * PH + px;
+        const size_t idx = ((size_t)(n * (C::CO / 8) + cob * 16 + c) * PH + rb * PR + pr) * PH + px;
         v = reinterpret_cast<const uint4*>(dc)[idx];
         cw = reinterpret_cast<const uint2*>(dcode)[idx];
     };
@@ -1222,7 +1223,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
 }
 
 using CfgWg2 = WgCfg<64, 128, 32, 4, 1>;   // dC = routed dp2 (EXP)
-using CfgWg3 = WgCfg<128, 256, 16, 8>;
+using CfgWg3 = WgCfg<128, 256, 16, 8, 1>;   // dC = routed dcut (EXP)
 
 template <class C>
 static int launch_wgrad(const uint16_t* dc, const uint16_t* in, float* slabs, int B, void* stream,
@@ -1238,8 +1239,9 @@ extern "C" int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, c
                                     void* stream) {
     return launch_wgrad<CfgWg2>(dp2, a1, slabs, B, stream, code2);
 }
-extern "C" int slk_wide_conv3_wgrad(const uint16_t* dc3, const uint16_t* p2, float* slabs, int B, void* stream) {
-    return launch_wgrad<CfgWg3>(dc3, p2, slabs, B, stream);
+extern "C" int slk_wide_conv3_wgrad(const uint16_t* dcut, const uint8_t* code3, const uint16_t* p2, float* slabs, int B,
+                                    void* stream) {
+    return launch_wgrad<CfgWg3>(dcut, p2, slabs, B, stream, code3);
 }
 
 // ============================================================================ conv1 (3 -> 64), bf16 MFMA
@@ -1451,38 +1453,5 @@ extern "C" int slk_wide_conv1_wgrad_nslab(int B) { return B >= 0 ? C1W_GRID : 0;
 extern "C" int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && x && da1m && slabs);
     hipLaunchKernelGGL(wide_conv1_wgrad_kernel, dim3(C1W_GRID), dim3(256), 0, slk_stream(stream), x, da1m, slabs, B);
-    return slk_launch_status();
-}
-
-// ============================================================================ unpool of the cut gradient
-// dc3[b][c][2y+dy][2x+dx] = dcut[b][c][y][x] if code3 == 2dy+dx else 0 (max-pool backward of conv3's
-// pool with the ReLU folded into code 4). One thread per 8-channel chunk of one pooled pixel.
-__global__ __launch_bounds__(256) void wide_unpool_kernel(const uint16_t* __restrict__ dcut, const uint8_t* __restrict__ code,
-                                                          uint16_t* __restrict__ dc3, int nchunk) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= nchunk) return;
-    const int plane = i >> 6, pix = i & 63, y = pix >> 3, xx = pix & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(dcut + (size_t)i * 8);
-    const uint2 c = *reinterpret_cast<const uint2*>(code + (size_t)i * 8);
-    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t cw[2] = {c.x, c.y};
-#pragma unroll
-    for (int pos = 0; pos < 4; ++pos) {
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t c0 = (cw[k >> 1] >> (16 * (k & 1))) & 0xFF, c1 = (cw[k >> 1] >> (16 * (k & 1) + 8)) & 0xFF;
-            o[k] = (c0 == (uint32_t)pos ? (vw[k] & 0xFFFFu) : 0u) | (c1 == (uint32_t)pos ? (vw[k] & 0xFFFF0000u) : 0u);
-        }
-        const size_t off = (((size_t)plane * 16 + 2 * y + (pos >> 1)) * 16 + 2 * xx + (pos & 1)) * 8;
-        *reinterpret_cast<uint4*>(dc3 + off) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-}
-
-extern "C" int slk_wide_unpool(const uint16_t* dcut, const uint8_t* code3, uint16_t* dc3, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && dcut && code3 && dc3);
-    if (B == 0) return 0;
-    const int nchunk = B * 32 * 64;
-    hipLaunchKernelGGL(wide_unpool_kernel, dim3((nchunk + 255) / 256), dim3(256), 0, slk_stream(stream), dcut, code3, dc3, nchunk);
     return slk_launch_status();
 }

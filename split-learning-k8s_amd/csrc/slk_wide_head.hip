@@ -190,33 +190,12 @@ __global__ __launch_bounds__(256) void wide_head_ce_kernel(const float* __restri
     loss_i[b] = ok ? lse - z[(int)y] : __builtin_nanf("");
 }
 
-// dc3 != NULL (the fused 1-GPU step, where the server knows the client's code3): the cut gradient
-// goes straight to the client's conv3 output gradient — max-pool backward by code3, four 16-byte
-// chunks per cut chunk (= slk_wide_unpool of dcut, bit for bit) — and dcut is not written.
-__device__ __forceinline__ void unpool_chunk(const uint32_t (&o)[4], uint2 c, uint16_t* __restrict__ dc3, int b,
-                                             int fc) {
-    const int plane = fc >> 6, pix = fc & 63, y = pix >> 3, xx = pix & 7;
-    const uint32_t cw[2] = {c.x, c.y};
-#pragma unroll
-    for (int pos = 0; pos < 4; ++pos) {
-        uint32_t r[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t c0 = (cw[k >> 1] >> (16 * (k & 1))) & 0xFF, c1 = (cw[k >> 1] >> (16 * (k & 1) + 8)) & 0xFF;
-            r[k] = (c0 == (uint32_t)pos ? (o[k] & 0xFFFFu) : 0u) | (c1 == (uint32_t)pos ? (o[k] & 0xFFFF0000u) : 0u);
-        }
-        const size_t off = ((((size_t)b * (NCH / 64) + plane) * 16 + 2 * y + (pos >> 1)) * 16 + 2 * xx + (pos & 1)) * 8;
-        *reinterpret_cast<uint4*>(dc3 + off) = make_uint4(r[0], r[1], r[2], r[3]);
-    }
-}
-
 __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
                                                              const float* __restrict__ dlogits,
                                                              const int* __restrict__ step_ptr, uint32_t seed,
                                                              uint32_t thresh, float keep_scale,
                                                              uint16_t* __restrict__ dcut, float* __restrict__ slabs, int b0,
-                                                             int B, const uint8_t* __restrict__ code3 = nullptr,
-                                                             uint16_t* __restrict__ dc3 = nullptr) {
+                                                             int B) {
     const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
     const int fc = slice * 256 + threadIdx.x;
     const uint32_t step = (uint32_t)*step_ptr;
@@ -257,10 +236,7 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
             for (int k = 0; k < 8; ++k) acc[j][k] = __builtin_fmaf(dlr[j], d[k], acc[j][k]);
         if (slice == 0 && threadIdx.x < NC) accb += dl[threadIdx.x];
         const uint32_t ow[4] = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
-        if (dc3)
-            unpool_chunk(ow, *reinterpret_cast<const uint2*>(code3 + ((size_t)b * NCH + fc) * 8), dc3, b, fc);
-        else
-            *reinterpret_cast<uint4*>(dcut + ((size_t)b * NCH + fc) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        *reinterpret_cast<uint4*>(dcut + ((size_t)b * NCH + fc) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     }
     float* slab = slabs + (size_t)grp * (NC * CUTF + NC);
     const int plane = fc >> 6, pix = fc & 63;
@@ -469,25 +445,6 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
                        keep_threshold, keep_scale, dcut, slabs, b0, B);
     return slk_launch_status();
 }
-extern "C" int slk_wide_head_dc3(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels,
-                                 const int* step, unsigned seed, unsigned keep_threshold, float keep_scale,
-                                 float grad_scale, float* logits, float* loss_i, float* dlogits, const uint8_t* code3,
-                                 uint16_t* dc3, float* slabs, float* work, int* err_flag, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && cut && wf8 && bf && labels && step && logits && loss_i && dlogits && code3 && dc3 &&
-                  slabs && work);
-    SLK_CHECK_ARG(((uintptr_t)work & 15) == 0);
-    if (B == 0) return 0;
-    const int ng = slk_wide_head_nslab(B);
-    hipStream_t st = slk_stream(stream);
-    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ((B + HSG_L - 1) / HSG_L)), dim3(256), 0, st, cut, wf8, step, seed,
-                       keep_threshold, keep_scale, work, 0, B);
-    hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + 255) / 256), dim3(256), 0, st, work, bf, labels, grad_scale,
-                       logits, loss_i, dlogits, err_flag, B);
-    hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, dlogits, step, seed,
-                       keep_threshold, keep_scale, nullptr, slabs, 0, B, code3, dc3);
-    return slk_launch_status();
-}
-
 extern "C" int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step,
                                  unsigned seed, unsigned keep_threshold, float keep_scale, float* logits, float* work,
                                  int b0, int B, void* stream) {

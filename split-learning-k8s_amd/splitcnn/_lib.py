@@ -56,14 +56,12 @@ _SIGS = {
     "slk_wide_conv3_fwd": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_head": [_P, _P, _P, _P, _P, _U, _U, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "slk_wide_head_nslab": [_I],
-    "slk_wide_head_dc3": [_P, _P, _P, _P, _P, _U, _U, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "slk_wide_head_fwd": [_P, _P, _P, _P, _U, _U, _F, _P, _P, _I, _I, _P],
     "slk_wide_head_bwd": [_P, _P, _P, _P, _U, _U, _F, _P, _P, _I, _I, _P],
     "slk_wide_head_work": [_I],
-    "slk_wide_unpool": [_P, _P, _P, _I, _P],
-    "slk_wide_conv3_wgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv3_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv3_wgrad_nslab": [_I],
-    "slk_wide_conv3_dgrad": [_P, _P, _P, _I, _P],
+    "slk_wide_conv3_dgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv2_wgrad_nslab": [_I],
     "slk_wide_conv2_dgrad": [_P, _P, _P, _P, _P, _I, _P],

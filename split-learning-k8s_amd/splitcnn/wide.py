@@ -229,27 +229,24 @@ def client_backward_slab_shapes(B):
 
 def client_backward_kernels(dcut, saved, w2d, w3d, scratch, s1, s2, s3):
     """activations.backward(dcut) of the client stack into three slab sets [dW | db] (conv1, conv2,
-    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dc3, dp2, da1m) — dp2 is the
-    gradient of p2 (16 x 16; conv2's kernels route it by code2 themselves). dcut=None:
-    scratch's dc3 already holds the unpooled cut gradient (slk_wide_head_dc3, the fused step)."""
+    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dp2, da1m). No unpooled
+    gradient is stored: conv3's kernels route the pooled dcut by code3 while staging it, conv3's dgrad
+    writes dp2 (the gradient of p2, 16 x 16) and conv2's kernels route dp2 by code2 the same way."""
     x, a1, p2, code2, code3 = saved
-    dc3, dp2, da1m = scratch
+    dp2, da1m = scratch
     B = x.shape[0]
-    s = _stream(dc3)
-    if dcut is not None:
-        _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
-        _k("wide_unpool", dcut.data_ptr(), code3.data_ptr(), dc3.data_ptr(), B, s)
-    _k("wide_conv3_wgrad", dc3.data_ptr(), p2.data_ptr(), s3.data_ptr(), B, s)
-    _k("wide_conv3_dgrad", dc3.data_ptr(), w3d.data_ptr(), dp2.data_ptr(), B, s)
+    s = _stream(dp2)
+    _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
+    _k("wide_conv3_wgrad", dcut.data_ptr(), code3.data_ptr(), p2.data_ptr(), s3.data_ptr(), B, s)
+    _k("wide_conv3_dgrad", dcut.data_ptr(), code3.data_ptr(), w3d.data_ptr(), dp2.data_ptr(), B, s)
     _k("wide_conv2_wgrad", dp2.data_ptr(), code2.data_ptr(), a1.data_ptr(), s2.data_ptr(), B, s)
     _k("wide_conv2_dgrad", dp2.data_ptr(), code2.data_ptr(), w2d.data_ptr(), a1.data_ptr(), da1m.data_ptr(), B, s)
     _k("wide_conv1_wgrad", x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
 
 
 def client_backward_scratch(B, get):
-    """(dc3, dp2, da1m) via get(name, shape, dtype)."""
-    return (get("dc3", (B, 32, 16, 16, 8), _BF), get("dp2", (B, 16, 16, 16, 8), _BF),
-            get("da1m", (B, 8, 32, 32, 8), _BF))
+    """(dp2, da1m) via get(name, shape, dtype)."""
+    return get("dp2", (B, 16, 16, 16, 8), _BF), get("da1m", (B, 8, 32, 32, 8), _BF)
 
 
 def _reduce(slabs):
@@ -381,19 +378,14 @@ class WideClientStage:
         self._saved[tag] = (x, a1, p2, code2, code3)
         return cut
 
-    def dc3_buffer(self, B: int) -> torch.Tensor:
-        """The conv3 output-gradient scratch the fused step's head writes (slk_wide_head_dc3)."""
-        return client_backward_scratch(B, self._b)[0]
-
-    def backward_slabs(self, dcut: Optional[torch.Tensor], tag=""):
-        """Client backward into three slab sets (conv1, conv2, conv3); returns them. dcut=None: the
-        unpooled gradient is already in dc3_buffer(B) (fused step)."""
+    def backward_slabs(self, dcut: torch.Tensor, tag=""):
+        """Client backward into three slab sets (conv1, conv2, conv3); returns them."""
         B = self._saved[tag][0].shape[0]
         self._x, self._a1, self._p2, self._code2, self._code3 = self._saved[tag]
         scratch = client_backward_scratch(B, self._b)
         s1, s2, s3 = (self._b(n, shp, _F32) for n, shp in zip(("s1", "s2", "s3"), client_backward_slab_shapes(B)))
         client_backward_kernels(dcut, self._saved[tag], self.sh["w2d"], self.sh["w3d"], scratch, s1, s2, s3)
-        self._dc3, self._dp2, self._da1m = scratch
+        self._dp2, self._da1m = scratch
         return s1, s2, s3
 
     def _adam(self, lo, n, slabs):
@@ -513,30 +505,6 @@ class WideServerStage:
         if step is not None:
             self.loss_log.note_step(step)
 
-    def step_request_dc3(self, cut, labels, code3, dc3, step=None):
-        """step_request for the fused 1-GPU step: the cut gradient lands directly as the client's
-        unpooled conv3 output gradient dc3 (routed by the client's code3), not as dcut."""
-        B = cut.shape[0]
-        _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
-        _dev(labels, "labels", (B,), torch.int64)
-        _dev(code3, "code3", (B,) + CUT_SHAPE, _U8)
-        _dev(dc3, "dc3", (B, 32, 16, 16, 8), _BF)
-        logits = self._b("logits", (B, 10), _F32)
-        loss_i = self._b("loss_i", (B,), _F32)
-        dlogits = self._b("dlogits", (B, 10), _F32)
-        sf = self._b("sf", (_q("slk_wide_head_nslab", B), SERVER_NPARAM), _F32)
-        work = self._b("work", (_q("slk_wide_head_work", B),), _F32)
-        _k("wide_head_dc3", cut.data_ptr(), self.wf8.data_ptr(), self.params[163840:].data_ptr(), labels.data_ptr(),
-           self.step_ctr.data_ptr(), self.seed, KEEP_THRESHOLD, KEEP_SCALE, 1.0 / B, logits.data_ptr(),
-           loss_i.data_ptr(), dlogits.data_ptr(), code3.data_ptr(), dc3.data_ptr(), sf.data_ptr(), work.data_ptr(),
-           self.err_flag.data_ptr(), B, _stream(cut))
-        self._logits, self._dlogits = logits, dlogits
-        self.log_loss(loss_i)
-        self.step_from_slabs(sf)
-        if step is not None:
-            self.loss_log.note_step(step)
-        return loss_i
-
     def step_request(self, cut, labels, step=None, dcut=None):
         """One /forward_pass for the widened model: returns (dcut, loss_i)."""
         B = cut.shape[0]
@@ -600,11 +568,8 @@ class WideTrainer:
 
     def _eager(self, x, y):
         c = self.client
-        cut = c.forward(x)
-        # one device: the head writes the client's unpooled conv3 gradient directly (no dcut round
-        # trip, no unpool pass) — bit-identical to step_request + backward_step (GPU test)
-        self.server.step_request_dc3(cut, y, c._code3, c.dc3_buffer(x.shape[0]))
-        c.step_from_slabs(*c.backward_slabs(None))
+        dcut, _ = self.server.step_request(c.forward(x), y)
+        c.backward_step(dcut)
 
     def _state(self):
         c, s = self.client, self.server

@@ -127,8 +127,7 @@ def test_wide_step_layer_by_layer_vs_oracle(gpu):
     grad_close(_np(grads_s[163840:]), sv["grads"]["fc.bias"])
     # client backward on the GPU's tensors
     dcut_g = _nchw(dcut)
-    dc3 = W.unpool(dcut_g, code3_gpu)
-    assert np.array_equal(_nchw(c._dc3), dc3)                        # bit-exact routing
+    dc3 = W.unpool(dcut_g, code3_gpu)     # conv3's kernels route dcut by code3 while staging it
     # conv3's dgrad stores dp2, the gradient of p2 (16 x 16); conv2's kernels route it by code2
     bf16_close(_nchw(c._dp2), bf(W.conv3x3p1_dgrad(dc3, W3b)))
     dc2_g = W.unpool(_nchw(c._dp2), code2_gpu)
@@ -392,24 +391,47 @@ def test_wide_modules_run_the_reference_step_code(gpu):
     assert torch.equal(e1, e2)
 
 
-def test_fused_head_to_dc3_equals_stage_path(gpu):
-    """WideTrainer's fused step (slk_wide_head_dc3: the head writes the client's unpooled conv3
-    gradient, no dcut, no unpool pass) equals the stage path (step_request -> dcut -> unpool ->
-    client backward) bit for bit over 3 Adam steps at a ragged batch."""
-    from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
-    data = SyntheticCIFAR(13)
-    batches = [data.batch(19) for _ in range(3)]
-    fused = WideTrainer(*init_wide_models(seed=2), device=gpu, graph=False)
-    staged = WideTrainer(*init_wide_models(seed=2), device=gpu, graph=False)
-    for x, y in batches:
-        x, y = x.to(gpu), y.to(gpu)
-        fused.step(x, y)
-        cut = staged.client.forward(x)
-        dcut, _ = staged.server.step_request(cut, y)
-        staged.client.backward_step(dcut)
-    torch.cuda.synchronize()
-    for a, b in ((fused.client.params, staged.client.params), (fused.client.m, staged.client.m),
-                 (fused.client.v, staged.client.v), (fused.server.params, staged.server.params),
-                 (fused.client.grads, staged.client.grads), (fused.server.grads, staged.server.grads)):
-        assert torch.equal(a, b)
-    assert [l for _, l in fused.loss_log.flush()] == [l for _, l in staged.loss_log.flush()]
+def test_pooled_gradient_routing_random_codes(gpu):
+    """The client backward never stores an unpooled gradient: conv3's dgrad/wgrad route the pooled
+    dcut by code3 while staging it, and conv2's route dp2 by code2. Drive client_backward_kernels
+    with arbitrary codes (every window position and the ReLU-blocked code 4, uniformly) and random
+    operands at a ragged batch (9: one image past the 8-XCD grouping), against the oracle applied to
+    the explicitly unpooled gradients."""
+    from splitcnn import wide
+    B = 9
+    g = torch.Generator().manual_seed(5)
+    rnd = lambda *shape, scale=1.0: torch.randn(*shape, generator=g) * scale  # noqa: E731
+    code = lambda *shape: torch.randint(0, 5, shape, generator=g, dtype=torch.uint8)  # noqa: E731
+    W1, W2, W3 = rnd(64, 3, 3, 3, scale=0.2), rnd(128, 64, 3, 3, scale=0.05), rnd(256, 128, 3, 3, scale=0.03)
+    x = rnd(B, 3, 32, 32)
+    a1 = rnd(B, 64, 32, 32).bfloat16()                  # signed: the a1 > 0 mask matters
+    p2 = rnd(B, 128, 16, 16).abs().bfloat16()
+    code2, code3 = code(B, 128, 16, 16), code(B, 256, 8, 8)
+    dcut = rnd(B, 256, 8, 8, scale=1e-2).bfloat16()
+    dev = torch.device(gpu)
+    sh = wide.new_shadows(dev)
+    W1d, W2d, W3d = (w.to(dev) for w in (W1, W2, W3))
+    wide.build_shadows(W1d, W2d, W3d, sh, wide._stream(W1d))
+    c8 = lambda t: wide.nchw_to_c8(t.to(dev))  # noqa: E731
+    saved = (x.to(dev), c8(a1), c8(p2), c8(code2), c8(code3))
+    scratch = wide.client_backward_scratch(B, lambda n, shp, dt: torch.empty(shp, dtype=dt, device=dev))
+    slabs = [torch.empty(shp, dtype=torch.float32, device=dev) for shp in wide.client_backward_slab_shapes(B)]
+    wide.client_backward_kernels(c8(dcut), saved, sh["w2d"], sh["w3d"], scratch, *slabs)
+    g1, g2, g3 = (_np(wide._reduce(sl)) for sl in slabs)
+    dp2, da1m = (_nchw(t) for t in scratch)
+
+    f = lambda t: t.double().numpy()  # noqa: E731
+    bf = lambda a: W.bf16(a).astype(np.float64)  # noqa: E731
+    dc3 = W.unpool(f(dcut), f(code3).astype(np.int64))
+    bf16_close(dp2, bf(W.conv3x3p1_dgrad(dc3, bf(f(W3)))))
+    dW3, db3 = W.conv3x3p1_wgrad(f(p2), dc3)
+    grad_close(g3[:294912].reshape(256, 128, 3, 3), dW3)
+    grad_close(g3[294912:], db3)
+    dc2 = W.unpool(dp2, f(code2).astype(np.int64))      # on the GPU's dp2 (layer-isolated)
+    bf16_close(da1m, bf(np.where(f(a1) > 0, W.conv3x3p1_dgrad(dc2, bf(f(W2))), 0.0)))
+    dW2, db2 = W.conv3x3p1_wgrad(f(a1), dc2)
+    grad_close(g2[:73728].reshape(128, 64, 3, 3), dW2)
+    grad_close(g2[73728:], db2)
+    dW1, db1 = W.conv3x3p1_wgrad(bf(f(x)), da1m)
+    grad_close(g1[:1728].reshape(64, 3, 3, 3), dW1)
+    grad_close(g1[1728:], db1)

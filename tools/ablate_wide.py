@@ -34,15 +34,13 @@ code2 = codes(B, 16, 16, 16, 8)
 cut = bf(B, 32, 8, 8, 8)
 code3 = codes(B, 32, 8, 8, 8)
 dcut = bf(B, 32, 8, 8, 8, scale=1e-3)
-dc3 = bf(B, 32, 16, 16, 8, scale=1e-3)
-dc2 = bf(B, 16, 32, 32, 8, scale=1e-3)
 da1m = bf(B, 8, 32, 32, 8, scale=1e-3)
 w1b, w2f, w2d, w3f, w3d = bf(64 * 32, scale=0.1), bf(73728, scale=0.05), bf(73728, scale=0.05), bf(294912, scale=0.03), bf(294912, scale=0.03)
 b1, b2, b3 = (torch.randn(n, device=dev, generator=g) * 0.01 for n in (64, 128, 256))
 out_a1 = torch.empty_like(a1)
 out_p2, out_c2 = torch.empty_like(p2), torch.empty_like(code2)
 out_cut, out_c3 = torch.empty_like(cut), torch.empty_like(code3)
-out_dc2, out_dc3, out_da1m = torch.empty_like(dc2), torch.empty_like(dc3), torch.empty_like(da1m)
+out_da1m = torch.empty_like(da1m)
 dp2 = bf(B, 16, 16, 16, 8, scale=1e-3)
 out_dp2 = torch.empty_like(dp2)
 slabs = torch.empty(256 * (73728 + 128) + 64 * (294912 + 256), device=dev)
@@ -61,10 +59,9 @@ def calls(L):
         "conv1_fwd": lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), B, P(s)),
         "conv2_fwd": lambda: L.slk_wide_conv2_fwd(p(a1), p(w2f), p(b2), p(out_p2), p(out_c2), B, P(s)),
         "conv3_fwd": lambda: L.slk_wide_conv3_fwd(p(p2), p(w3f), p(b3), p(out_cut), p(out_c3), B, P(s)),
-        "unpool": lambda: L.slk_wide_unpool(p(dcut), p(code3), p(out_dc3), B, P(s)),
-        "conv3_wgrad": lambda: L.slk_wide_conv3_wgrad(p(dc3), p(p2), p(slabs), B, P(s)),
-        # dp2 (16 x 16) + code2: conv3 dgrad writes the pooled-resolution gradient, conv2's kernels route it
-        "conv3_dgrad": lambda: L.slk_wide_conv3_dgrad(p(dc3), p(w3d), p(out_dp2), B, P(s)),
+        # pooled gradients + codes: conv3's kernels route dcut by code3, conv2's route dp2 by code2
+        "conv3_wgrad": lambda: L.slk_wide_conv3_wgrad(p(dcut), p(code3), p(p2), p(slabs), B, P(s)),
+        "conv3_dgrad": lambda: L.slk_wide_conv3_dgrad(p(dcut), p(code3), p(w3d), p(out_dp2), B, P(s)),
         "conv2_wgrad": lambda: L.slk_wide_conv2_wgrad(p(dp2), p(code2), p(a1), p(slabs), B, P(s)),
         "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1), p(out_da1m), B, P(s)),
         "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
