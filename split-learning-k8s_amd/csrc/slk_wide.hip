@@ -13,7 +13,7 @@
 // conv3x3 (pad 1) forward and input-gradient ("dgrad") are one implicit-GEMM kernel:
 //   out[m][px] = sum_{tap, c} A[tap][c][m] * In[c][px + off(tap)]
 // with A = the bf16 weight shadow (forward: W[co][ci][tap]; dgrad: W[co][ci][8 - tap], m = ci) and In
-// the activation (forward) or the unpooled output gradient (dgrad). A workgroup (4 waves, 2 per CU)
+// the activation (forward) or the layer's output gradient (dgrad). A workgroup (4 waves, 2 per CU)
 // owns MT output channels x NPX pixels (TR whole image rows); each wave a 64 x 64 sub-tile as
 // 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators. The input tile of one 32-channel group is staged in
 // LDS with its 1-pixel halo as [4 chunks][(TR+2)*(W+2) pixels][16 B] by LDS-DMA (halo lanes read a
@@ -24,8 +24,9 @@
 // One counted `s_waitcnt vmcnt` + one barrier per step; the stream continues across tiles.
 // Epilogues: forward = bias + ReLU + 2x2 max-pool in registers (vertical pairs are sibling
 // accumulators, horizontal pairs neighbouring lanes) -> pooled bf16 + routing code; dgrad of conv3 =
-// max-pool backward of conv2 (route to the code's position, bf16) -> conv2's unpooled output gradient;
-// dgrad of conv2 = ReLU mask of a1 -> the gradient conv1's wgrad consumes.
+// the gradient of p2 as is (16 x 16, bf16); dgrad of conv2 = ReLU mask of a1 -> the gradient conv1's
+// wgrad consumes. The dgrads' own input is a max-pool backward (conv3: dcut by code3, conv2: dp2 by
+// code2) that is never stored: the kernel expands the pooled gradient while staging it into LDS (EXP).
 #include "slk_common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -37,12 +38,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef SLK_WIDE_XCD
 #define SLK_WIDE_XCD 1
 #endif
-#ifndef SLK_WIDE_PF
-#define SLK_WIDE_PF 1
-#endif
-// Profiling-only ablation bits of the non-prefetch conv loop (tools/ablate_wide.py): 1 = no DMA in
-// the loop, 2 = no MFMA, 4 = no LDS fragment reads, 8 = no waits / barriers, 16 = no weight DMA,
-// 32 = no input DMA, 64 = no epilogue. Production = 0.
+// Profiling only (tools/ablate_wide.py): SLK_WABL = 64 drops the conv epilogues. Production = 0.
 // Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
 // sample 0 (L2-resident): the HBM-read share of a kernel's time.
 #ifndef SLK_WIDE_FIXSRC
@@ -63,16 +59,13 @@ __device__ __forceinline__ void wide_stagger() {
         for (int i = 0; i < SLK_WIDE_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
 }
-#ifndef SLK_WIDE_L
-#define SLK_WIDE_L (SLK_WIDE_PF ? 3 : 2)
-#endif
 
 namespace wide {
 constexpr int IMG = 32;                 // input 3 x 32 x 32
 constexpr int C1 = 64, C2 = 128, C3 = 256;
 constexpr int CUT = C3 * 8 * 8;         // 16384 features per sample
 constexpr int NCLS = 10;
-constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_UNPOOL = 1, MODE_DGRAD_MASK = 2, MODE_DGRAD_PLAIN = 3;
+constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_MASK = 2, MODE_DGRAD_PLAIN = 3;
 }  // namespace wide
 
 __device__ __attribute__((aligned(64))) uint32_t slk_wide_zero[64];  // zero source for halo lanes
@@ -125,16 +118,16 @@ struct ConvCfg {
     static constexpr int NW = W_SLOT / 1024 / NWV;          // weight DMA instructions per wave per step
     static constexpr int DSPLIT = NWV / 4;                  // waves sharing one input chunk plane
     static constexpr int NDW = ND / DSPLIT;                 // input DMA instructions per wave per group
-    static constexpr int L = SLK_WIDE_L;                    // weight lookahead (steps)
+    static constexpr int L = 3;                             // weight lookahead (steps)
     static constexpr int RW = L + 1;                        // weight ring slots
     static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
     static constexpr int RB = HW / TR;                      // row blocks per image
     static constexpr int NCB = CO / MT;                     // output-channel blocks
     static constexpr int FPR = HW / 16;                     // 16-pixel fragments per image row
-    // VMEM instructions per lane in the epilogue: stores (pooled value + code, 4 unpooled positions,
-    // masked value) and the code2 / a1 words loaded at tile start. Must never over-count.
-    static constexpr int EPI_ST = MODE == 1 ? 16 * FW : 4 * FW;
-    static constexpr int EPI_LD = (MODE == 0 || MODE == 3) ? 0 : 4 * FW;
+    // VMEM instructions per lane in the epilogue: stores (pooled value + code, plain or masked value)
+    // and the a1 words loaded at tile start. Must never over-count.
+    static constexpr int EPI_ST = 4 * FW;
+    static constexpr int EPI_LD = MODE == 2 ? 4 * FW : 0;
     // EXP: the input is the max-pool backward of a POOLED gradient (HW/2 x HW/2, bf16 C8) and its
     // routing code, expanded into the LDS tile in registers (exp_load / exp_store) instead of an
     // unpooled tensor moved by LDS-DMA: the unpooled tensor is never written nor read.
@@ -285,12 +278,12 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
     }
 }
 
-// Epilogue operands of a tile (dgrad-unpool: code2 words, dgrad-mask: a1 words), loaded when the tile
+// Epilogue operands of a tile (dgrad-mask: a1 words), loaded when the tile
 // starts so their latency hides under its main loop instead of draining the DMA queue at the epilogue.
 template <class C>
 __device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const TileState& s, int wm, int wn,
-                                             int lane, uint32_t (&ecw)[4][C::FW], uint2 (&em)[4][C::FW]) {
-    if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL || C::MODE == wide::MODE_DGRAD_MASK) {
+                                             int lane, uint2 (&em)[4][C::FW]) {
+    if constexpr (C::MODE == wide::MODE_DGRAD_MASK) {
         const int ch_base = s.cob * C::MT + wm * 64 + 4 * (lane >> 4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -300,19 +293,17 @@ __device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const
                 const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                 const int y = s.rb * C::TR + q / C::HW, x = q % C::HW;
                 const size_t o = (((size_t)(s.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
-                if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL)
-                    ecw[i][f] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(aux) + o);
-                else
-                    em[i][f] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + o);
+                em[i][f] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + o);
             }
         }
     }
 }
 
-// aux: forward = bias (f32 [CO]); dgrad-unpool = code2 (u8, C8 [B][CO/8][HW][HW][8]);
+// in: forward = activation, dgrad = the POOLED output gradient (EXP; out2 = its routing code, u8 C8);
+// aux: forward = bias (f32 [CO]); dgrad-plain = unused;
 //      dgrad-mask = a1 (bf16, C8 [B][CO/8][HW][HW][8]).
 // out: forward = pooled bf16 C8 [B][CO/8][HW/2][HW/2][8] (+ code u8 same layout in out2);
-//      dgrad-unpool = bf16 C8 [B][CO/8][2HW][2HW][8]; dgrad-mask = bf16 C8 [B][CO/8][HW][HW][8].
+//      dgrad-plain / dgrad-mask = bf16 C8 [B][CO/8][HW][HW][8].
 template <class C>
 __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t* __restrict__ in,
                                                            const uint16_t* __restrict__ wsh,
@@ -357,7 +348,6 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
             for (int r = 0; r < 4; ++r) bias[i][r] = b[cur.cob * C::MT + wm * 64 + i * 16 + 4 * (lane >> 4) + r];
     }
 
-#if SLK_WIDE_PF
     // Fragment prefetch: during step s the MFMAs consume fragments read in step s-1 while the reads
     // for step s+1 are in flight, so no step opens with an LDS-latency bubble. The wait of step s
     // therefore covers weight step s+1 (issued 2 steps earlier; lookahead L = 3, 4 ring slots) and,
@@ -393,12 +383,11 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     int wslot = 0;   // ring slot of the current step
     int islot = 0;   // input slot of the current group
     bool post = false;   // a previous tile's epilogue stores may be in flight
-    uint32_t ecw[4][C::FW];
     uint2 em[4][C::FW];
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
-        epi_prefetch<C>(aux, cur, wm, wn, lane, ecw, em);
+        epi_prefetch<C>(aux, cur, wm, wn, lane, em);
         f32x4 acc[4][C::FW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -481,97 +470,6 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
             }
             islot ^= 1;
         }
-#else
-    // prologue: input group 0 of the first tile, then weight steps 0 .. L-1
-    static_assert(!C::EXP, "EXP staging needs the prefetch loop (SLK_WIDE_PF)");
-    issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
-#pragma unroll
-    for (int k = 0; k < C::L; ++k) issue_weight<C>(wsh, cur.cob, k, wslot0 + k * C::W_SLOT, wave, lane);
-
-    int wslot = 0;   // ring slot of the current step
-    int islot = 0;   // input slot of the current group
-    bool post = false;   // a previous tile's epilogue stores may be in flight
-    uint32_t ecw[4][C::FW];
-    uint2 em[4][C::FW];
-#pragma unroll 1
-    while (true) {
-        const bool tail = !nxt.valid;
-        epi_prefetch<C>(aux, cur, wm, wn, lane, ecw, em);
-        f32x4 acc[4][C::FW];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int f = 0; f < C::FW; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll 1
-        for (int g = 0; g < C::G; ++g) {
-            const char* ib = islot0 + islot * C::IN_SLOT;
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                // this step's weight slice (and, at tap 0, this group's input tile) has landed
-                if (!(SLK_WABL & 8)) {
-                    if (tail || (SLK_WABL & 49)) wait_vmcnt<0>();
-                    else if (SLK_WIDE_EPI && tap < C::L && g == 0) {
-                        // this step's weights predate the previous epilogue and this tile's loads
-                        if (tap == 0) {
-                            if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_ST + C::EPI_LD>();
-                            else wait_vmcnt_sat<(C::L - 1) * C::NW + C::EPI_LD>();
-                        } else {
-                            if (post) wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_ST + C::EPI_LD>();
-                            else wait_vmcnt_sat<(C::L - 1) * C::NW + C::NDW + C::EPI_LD>();
-                        }
-                    }
-                    else if (tap >= 1 && tap <= C::L) wait_vmcnt<(C::L - 1) * C::NW + C::NDW>();
-                    else wait_vmcnt<(C::L - 1) * C::NW>();
-                    __builtin_amdgcn_s_barrier();
-                }
-                asm volatile("" ::: "memory");
-                // lookahead: weight step +L (ring slot of step -1, free since the barrier), then at
-                // tap 0 the next group's input tile (slot of group -1)
-                if (!(SLK_WABL & 17)) {
-                    const int sl = g * 9 + tap + C::L;
-                    int ws = wslot + C::L;
-                    ws = ws >= C::RW ? ws - C::RW : ws;
-                    if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
-                    else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
-                }
-                if (tap == 0 && !(SLK_WABL & 33)) {
-                    char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
-                    if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
-                    else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
-                }
-                const char* wb = wslot0 + wslot * C::W_SLOT;
-                const int toff = ((tap / 3 - 1) * C::PW + (tap % 3 - 1)) * 16;
-                bf16x8 av[4], bv[C::FW];
-#if SLK_WABL & 4
-#pragma unroll
-                for (int i = 0; i < 4; ++i) { av[i] = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) int){a_off + i, tap, 0, 0}); slk_keep(av[i]); }
-#pragma unroll
-                for (int f = 0; f < C::FW; ++f) { bv[f] = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) int){b_off[f], tap, 0, 0}); slk_keep(bv[f]); }
-#else
-#pragma unroll
-                for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const bf16x8*>(wb + a_off + i * 256);
-#pragma unroll
-                for (int f = 0; f < C::FW; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
-#endif
-#if SLK_WABL & 2
-#pragma unroll
-                for (int i = 0; i < 4; ++i) slk_keep(av[i]);
-#pragma unroll
-                for (int f = 0; f < C::FW; ++f) slk_keep(bv[f]);
-#else
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int f = 0; f < C::FW; ++f)
-                        acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
-#endif
-                wslot = wslot + 1 == C::RW ? 0 : wslot + 1;
-            }
-            islot ^= 1;
-        }
-
-#endif
         // ------------------------------------------------------------------ epilogue
         const int ch_base = cur.cob * C::MT + wm * 64 + 4 * (lane >> 4);
         if (SLK_WABL & 64) {
@@ -611,36 +509,6 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                         const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * PH + (y >> 1)) * PH + (x >> 1)) * 8 + (ch0 & 7);
                         *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
                         *reinterpret_cast<uint32_t*>(out2 + o) = cw;
-                    }
-                }
-            }
-        } else if constexpr (C::MODE == wide::MODE_DGRAD_UNPOOL) {
-            // Max-pool backward of conv2: the 4 channels' values go to the window position their
-            // code names. Round once to bf16 pairs, then mask per position with byte lookups:
-            // v_perm_b32 with the codes as selectors into the table {0, 0xFF << 8 pos} gives 0xFF
-            // exactly where code == pos (code 4, ReLU-blocked, hits the zero half). 20 VALU per
-            // (i, f) instead of ~65 compare/select/or (bit-identical: a masked-out bf16 is 0x0000,
-            // the value 0.f rounds to). The 4 stores share one address (constant offsets).
-            constexpr int FH = 2 * C::HW;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int ch0 = ch_base + i * 16;
-#pragma unroll
-                for (int f = 0; f < C::FW; ++f) {
-                    const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
-                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
-                    const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
-                    const uint32_t cw = ecw[i][f];
-                    const uint32_t p01 = pack_bf16x2(acc[i][f][0], acc[i][f][1]);
-                    const uint32_t p23 = pack_bf16x2(acc[i][f][2], acc[i][f][3]);
-                    const uint32_t cA = __builtin_amdgcn_perm(0u, cw, 0x01010000u);  // codes (0, 0, 1, 1)
-                    const uint32_t cB = __builtin_amdgcn_perm(0u, cw, 0x03030202u);  // codes (2, 2, 3, 3)
-                    uint16_t* o = out + ((plane * FH + 2 * y) * FH + 2 * x) * 8 + (ch0 & 7);
-#pragma unroll
-                    for (int pos = 0; pos < 4; ++pos) {
-                        const uint32_t T = 0xFFu << (8 * pos);
-                        const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
-                        *reinterpret_cast<uint2*>(o + ((pos >> 1) * FH + (pos & 1)) * 8) = make_uint2(p01 & mA, p23 & mB);
                     }
                 }
             }
@@ -724,8 +592,8 @@ struct Conv32Cfg {
     static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
     static constexpr int RB = HW / TR;
     static constexpr int NCB = CO / MT;
-    static constexpr int EPI_ST = MODE == 0 ? (HW == 32 ? 32 : 64) : 128;
-    static constexpr int EPI_LD = MODE == 0 ? 0 : 32;
+    static constexpr int EPI_ST = HW == 32 ? 32 : 64;
+    static constexpr int EPI_LD = 0;
     static_assert(HW % TR == 0 && TR % 2 == 0 && (HW == 32 || HW == 16), "tile rows");
     static_assert(NCB == 1 || NCB == 2, "NCB");
 };
@@ -840,7 +708,8 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
         }
 
         // ------------------------------------------------------------------ epilogue
-        if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+        static_assert(C::MODE == wide::MODE_FWD_POOL, "conv32: forward + pool only");
+        {
             constexpr int PH = C::HW / 2;
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
@@ -890,32 +759,6 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
                             const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * PH + (y >> 1)) * PH + (x >> 1)) * 8 + (ch0 & 7);
                             *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
                             *reinterpret_cast<uint32_t*>(out2 + o) = cw;
-                        }
-                    }
-                }
-            }
-        } else {
-            static_assert(C::MODE == wide::MODE_DGRAD_UNPOOL, "conv32: fwd-pool or dgrad-unpool");
-            const uint8_t* code = reinterpret_cast<const uint8_t*>(aux);
-            constexpr int FH = 2 * C::HW;
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-                for (int pt = 0; pt < 4; ++pt) {
-                    const int q = wn * 128 + pt * 32 + r;
-                    const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const int ch0 = wm * 64 + ct * 32 + 8 * g4 + 4 * h;
-                        const size_t plane = (size_t)(cur.n * (C::CO / 8) + (ch0 >> 3));
-                        const uint32_t cw = *reinterpret_cast<const uint32_t*>(code + ((plane * C::HW + y) * C::HW + x) * 8 + (ch0 & 7));
-#pragma unroll
-                        for (int pos = 0; pos < 4; ++pos) {
-                            float v[4];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = ((cw >> (8 * e)) & 0xFF) == (uint32_t)pos ? acc[ct][pt][4 * g4 + e] : 0.f;
-                            const size_t o = ((plane * FH + 2 * y + (pos >> 1)) * FH + 2 * x + (pos & 1)) * 8 + (ch0 & 7);
-                            *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
                         }
                     }
                 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a libslk variant with extra -D flags into build_abl/<name>.so (profiling only), with the same
 # per-source flags as the production build (splitcnn/build.py).
-# usage: tools/build_variant.sh NAME "-DSLK_WIDE_L=3 ..."
+# usage: tools/build_variant.sh NAME "-DSLK_WIDE_XCD=0 ..."
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/build_abl"

@@ -60,8 +60,7 @@ if args.traffic_out:
             ("wide_conv_kernel<ConvCfg<128, 64, 32", "wide_conv2_dgrad"),
             ("wide_wgrad_kernel<WgCfg<64, 128, 32", "wide_conv2_wgrad"),
             ("wide_wgrad_kernel<WgCfg<128, 256, 16", "wide_conv3_wgrad"),
-            ("wide_conv1_wgrad_kernel", "wide_conv1_wgrad"), ("wide_conv1_fwd_kernel", "wide_conv1_fwd"),
-            ("wide_unpool_kernel", "wide_unpool")]
+            ("wide_conv1_wgrad_kernel", "wide_conv1_wgrad"), ("wide_conv1_fwd_kernel", "wide_conv1_fwd")]
     for k, m in out.items():
         short = names.get(k) or next((v for pfx, v in wide if k.startswith(pfx)), None)
         if short and "hbm_bytes_corrected" in m:
