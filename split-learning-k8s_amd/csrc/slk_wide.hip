@@ -31,6 +31,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Build-time knobs (tools/ablate_wide.py builds variants): weight lookahead of the conv stream, and
 // XCD grouping of tiles (all row blocks / channel blocks of one image on one XCD at the same time,
@@ -46,6 +47,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #endif
 #ifndef SLK_WABL
 #define SLK_WABL 0
+#endif
+// Wave priority: raise it around each step's MFMA block (1: conv kernels, 2: also wgrad), so a wave
+// with MFMAs ready issues ahead of a co-resident wave's epilogue VALU / staging work.
+#ifndef SLK_WIDE_PRIO
+#define SLK_WIDE_PRIO 0
 #endif
 // Stagger: the second half of the grid (the second workgroup of each CU under round-robin dispatch)
 // sleeps SLK_WIDE_STAGGER x 127 x 64 cycles before its first tile, so the two co-resident workgroups
@@ -120,7 +126,6 @@ struct ConvCfg {
     static constexpr int NDW = ND / DSPLIT;                 // input DMA instructions per wave per group
     static constexpr int L = 3;                             // weight lookahead (steps)
     static constexpr int RW = L + 1;                        // weight ring slots
-    static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT;
     static constexpr int RB = HW / TR;                      // row blocks per image
     static constexpr int NCB = CO / MT;                     // output-channel blocks
     static constexpr int FPR = HW / 16;                     // 16-pixel fragments per image row
@@ -129,16 +134,19 @@ struct ConvCfg {
     static constexpr int EPI_ST = 4 * FW;
     static constexpr int EPI_LD = MODE == 2 ? 4 * FW : 0;
     // EXP: the input is the max-pool backward of a POOLED gradient (HW/2 x HW/2, bf16 C8) and its
-    // routing code, expanded into the LDS tile in registers (exp_load / exp_store) instead of an
-    // unpooled tensor moved by LDS-DMA: the unpooled tensor is never written nor read.
+    // routing code: both move by LDS-DMA into a raw staging area (values [XR*THREADS][16 B], code
+    // dwords 2 x [XR*THREADS][4 B]) and are expanded from there into the tile (exp_expand), so the
+    // unpooled tensor is never written nor read, and no VGPR-destination load enters the main loop
+    // (hipcc answers one beside LDS-DMA with vmcnt(0), draining the weight stream).
     static constexpr bool EXP = EXP_;
     static constexpr int XPR = TR / 2 + 2;                  // pooled rows feeding a tile (with halo)
     static constexpr int XITEMS = 4 * XPR * (HW / 2);       // pooled chunks per 32-channel group
     static constexpr int XR = (XITEMS + THREADS - 1) / THREADS;
-    // input VMEM instructions per wave per group issued at tap 0 (EXP: round 0's two loads; round 1,
-    // if any, is issued at tap 2 and stored at tap 4, so only 6 VGPRs of staging are live at a time)
-    static constexpr int NIN = EXP ? 2 : NDW;
-    static_assert(!EXP || XR <= 2, "EXP: at most two staging rounds");
+    static constexpr int XN = XR * THREADS;                 // staged items (the excess reads zeros)
+    static constexpr int RAW = EXP ? XN * 24 : 0;
+    // input VMEM instructions per wave per group, issued at tap 0
+    static constexpr int NIN = EXP ? 3 * XR : NDW;
+    static constexpr int LDS = 2 * IN_SLOT + RW * W_SLOT + RAW;
     static_assert(MT == 128 || MT == 64, "MT");
     static_assert(HW % TR == 0 && TR % 2 == 0 && (16 * FW) % (2 * HW) == 0, "tile rows / pool pairs per wave");
     static_assert(NW >= 1 && W_SLOT % (1024 * NWV) == 0, "weight slot must split over the waves");
@@ -211,18 +219,27 @@ __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, con
 }
 
 // EXP staging. Pooled chunk i = (plane c, pooled row pr, pooled col px) of group g: its 8 channels'
-// values and routing codes (code 0..3 = window position, 4 = ReLU-blocked). Every lane issues exactly
-// 2 XR loads (out-of-range items read the zero block), so the counted waits stay exact.
+// values and routing codes (code 0..3 = window position, 4 = ReLU-blocked). Wave w moves items
+// r * THREADS + 64 w + lane of every round r by LDS-DMA (value + two code dwords); items outside the
+// image or past XITEMS read the zero block, so each wave issues exactly NIN instructions.
 template <class C>
-__device__ __forceinline__ void exp_load(const uint16_t* __restrict__ dp, const uint8_t* __restrict__ code,
-                                         const TileState& s, int g, int i, uint4& v, uint2& cw) {
+__device__ __forceinline__ void exp_issue(const uint16_t* __restrict__ dp, const uint8_t* __restrict__ code,
+                                          const TileState& s, int g, char* raw, int wave, int lane) {
     constexpr int PH = C::HW / 2;
-    const int c = i / (C::XPR * PH), rem = i - c * (C::XPR * PH), pr = rem / PH, px = rem - pr * PH;
-    const int py = s.rb * (C::TR / 2) - 1 + pr;
-    const bool ok = i < C::XITEMS && py >= 0 && py < PH;
-    const size_t idx = ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * PH + (ok ? py : 0)) * PH + px;
-    v = *(ok ? reinterpret_cast<const uint4*>(dp) + idx : reinterpret_cast<const uint4*>(slk_wide_zero));
-    cw = *(ok ? reinterpret_cast<const uint2*>(code) + idx : reinterpret_cast<const uint2*>(slk_wide_zero));
+    const char* zero = reinterpret_cast<const char*>(slk_wide_zero);
+#pragma unroll
+    for (int r = 0; r < C::XR; ++r) {
+        const int i0 = r * C::THREADS + wave * 64, i = i0 + lane;
+        const int c = i / (C::XPR * PH), rem = i - c * (C::XPR * PH), pr = rem / PH, px = rem - pr * PH;
+        const int py = s.rb * (C::TR / 2) - 1 + pr;
+        const bool ok = i < C::XITEMS && py >= 0 && py < PH;
+        const size_t idx = ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * PH + (ok ? py : 0)) * PH + px;
+        const char* sv = ok ? reinterpret_cast<const char*>(dp) + idx * 16 : zero;
+        const char* sc = ok ? reinterpret_cast<const char*>(code) + idx * 8 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)sv, (lds_ptr_t)(raw + i0 * 16), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)sc, (lds_ptr_t)(raw + C::XN * 16 + i0 * 4), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(sc + 4), (lds_ptr_t)(raw + C::XN * 20 + i0 * 4), 4, 0, 0);
+    }
 }
 
 // 16-bit lane masks of one window position: v_perm_b32 with the codes as byte selectors into the table
@@ -231,6 +248,15 @@ __device__ __forceinline__ uint4 route_chunk(uint4 v, uint32_t cA, uint32_t cB, 
     const uint32_t T = 0xFFu << (8 * pos);
     return make_uint4(v.x & __builtin_amdgcn_perm(0u, T, cA), v.y & __builtin_amdgcn_perm(0u, T, cB),
                       v.z & __builtin_amdgcn_perm(0u, T, cC), v.w & __builtin_amdgcn_perm(0u, T, cD));
+}
+
+// A 16-byte LDS store hipcc does not see: it treats a plain store into LDS that LDS-DMA also writes
+// as aliasing every DMA in flight and drains them all (vmcnt(0)) first. The caller publishes it with
+// its own lgkmcnt wait + barrier.
+__device__ __forceinline__ void lds_store16(char* p, uint4 v) {
+    const uint32_t a = (uint32_t)(size_t)(lds_ptr_t)p;
+    const u32x4 d = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1\n\ts_nop 1" ::"v"(a), "v"(d) : "memory");
 }
 
 // max-pool backward of the loaded pooled chunk i into the tile's LDS image [4][NPP][16 B]: pooled
@@ -249,7 +275,29 @@ __device__ __forceinline__ void exp_store(char* slot, int i, uint4 v, uint2 cw) 
         if (ry < 0 || ry > C::TR + 1) continue;
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx)
-            *reinterpret_cast<uint4*>(base + (ry * C::PW + dx) * 16) = route_chunk(v, cA, cB, cC, cD, 2 * dy + dx);
+            lds_store16(base + (ry * C::PW + dx) * 16, route_chunk(v, cA, cB, cC, cD, 2 * dy + dx));
+    }
+}
+
+// the staged items of this thread (landed and barrier-published) -> the tile in `slot`
+template <class C>
+__device__ __forceinline__ void exp_expand(char* slot, const char* raw, int tid) {
+#pragma unroll
+    for (int r = 0; r < C::XR; ++r) {
+        const int i = tid + r * C::THREADS;
+        if (i >= C::XITEMS) break;
+        // read in one asm statement with its own lgkmcnt wait: hipcc treats a plain LDS read of a
+        // region that LDS-DMA writes as aliasing every DMA in flight and drains them all (vmcnt(0))
+        const uint32_t a = (uint32_t)(size_t)(lds_ptr_t)(raw + i * 16);
+        const uint32_t b = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 16 + i * 4);
+        const uint32_t c = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 20 + i * 4);
+        u32x4 v4;
+        uint32_t c0, c1;
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(v4), "=&v"(c0), "=&v"(c1)
+                     : "v"(a), "v"(b), "v"(c)
+                     : "memory");
+        exp_store<C>(slot, i, make_uint4(v4[0], v4[1], v4[2], v4[3]), make_uint2(c0, c1));
     }
 }
 
@@ -353,15 +401,14 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
     // therefore covers weight step s+1 (issued 2 steps earlier; lookahead L = 3, 4 ring slots) and,
     // at tap 8, the next group's input tile.
     static_assert(C::L == 3, "prefetch schedule assumes a weight lookahead of 3");
-    uint4 xv;
-    uint2 xc;
+    char* raw = smem + 2 * C::IN_SLOT + C::RW * C::W_SLOT;
     if constexpr (C::EXP) {
         exp_zero_halo<C>(islot0, tid);
-#pragma unroll
-        for (int r = 0; r < C::XR; ++r) {
-            exp_load<C>(in, out2, cur, 0, tid + r * C::THREADS, xv, xc);
-            exp_store<C>(islot0, tid + r * C::THREADS, xv, xc);
-        }
+        exp_issue<C>(in, out2, cur, 0, raw, wave, lane);
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        exp_expand<C>(islot0, raw, tid);
     } else {
         issue_input<C>(in, cur, pcur, 0, islot0, wave, lane);
     }
@@ -412,11 +459,10 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     }
                 }
                 else if (tap == 1 || tap == 2) wait_vmcnt<C::NW + C::NIN>();
-                else if (C::EXP && C::XR == 2 && tap == 3) wait_vmcnt<C::NW + 2>();  // round 1's loads may fly
                 else wait_vmcnt<C::NW>();
-                // EXP: the next group's tile was written to LDS by tap 4 (each round after its loads
-                // landed); this wave's writes complete before the barrier that precedes its readers
-                if (C::EXP && tap == 5) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // EXP: the next group's staged items landed by tap 3's wait and were expanded after its
+                // barrier; this wave's tile writes (and raw reads) complete before tap 4's barrier
+                if (C::EXP && tap == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
@@ -427,18 +473,14 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
                 }
                 if constexpr (C::EXP) {
-                    // next group's pooled input into the free slot: round 0 loads at tap 0 and is
-                    // expanded at tap 2, round 1 loads at tap 2 (after that) and is expanded at tap 4
+                    // next group's pooled input: staged by LDS-DMA at tap 0, expanded into the free
+                    // slot at tap 3 (read from tap 8 on)
                     if (g + 1 < C::G || !tail) {
-                        const TileState& xs = g + 1 < C::G ? cur : nxt;
-                        const int xg = g + 1 < C::G ? g + 1 : 0;
-                        char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
-                        if (tap == 0) exp_load<C>(in, out2, xs, xg, tid, xv, xc);
-                        if (tap == 2) {
-                            exp_store<C>(nslot, tid, xv, xc);
-                            if (C::XR == 2) exp_load<C>(in, out2, xs, xg, tid + C::THREADS, xv, xc);
+                        if (tap == 0) {
+                            if (g + 1 < C::G) exp_issue<C>(in, out2, cur, g + 1, raw, wave, lane);
+                            else exp_issue<C>(in, out2, nxt, 0, raw, wave, lane);
                         }
-                        if (tap == 4 && C::XR == 2) exp_store<C>(nslot, tid + C::THREADS, xv, xc);
+                        if (tap == 3) exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
                     }
                 } else if (tap == 0) {
                     char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
@@ -461,11 +503,13 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
 #pragma unroll
                     for (int f = 0; f < C::FW; ++f) bv_n[f] = *reinterpret_cast<const bf16x8*>(ib + b_off[f] + toff);
                 }
+                if (SLK_WIDE_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int f = 0; f < C::FW; ++f)
                         acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
+                if (SLK_WIDE_PRIO) __builtin_amdgcn_s_setprio(0);
                 wslot = wn1;
             }
             islot ^= 1;
@@ -1033,8 +1077,10 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
                 const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)pb);
                 const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(pb + 64));
                 const bf16x8 bv = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                if (SLK_WIDE_PRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][u], 0, 0, 0);
+                if (SLK_WIDE_PRIO & 2) __builtin_amdgcn_s_setprio(0);
             }
         }
         // EXP: the next tile's dC, routed into the other buffer (free since this tile's barrier)
