@@ -93,3 +93,23 @@ __device__ __forceinline__ float wave_sum(float v) {
     v += __shfl_xor(v, 32, 64);
     return v;
 }
+
+// ---------------------------------------------------------------------------- LDS-DMA as inline asm
+// global_load_lds issued through asm: hipcc then neither counts it nor inserts its own vmcnt(0) in
+// front of LDS reads and writes it cannot prove disjoint from a DMA in flight (it cannot tell a
+// prefetch buffer from the one being read, so the prefetch would drain before every use). The kernel
+// retires the DMA with its own counted `s_waitcnt vmcnt` + barrier. lds_dst is wave-uniform.
+typedef __attribute__((address_space(3))) void* slk_lds_ptr;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(slk_lds_ptr)(const_cast<void*>(p)));
+}
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}

@@ -107,6 +107,7 @@ template <int CI_, int CO_, int HW_, int MT_, int MODE_, int FW_, int NWV_, int 
 struct ConvCfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = MT_, MODE = MODE_;
     static constexpr bool K32 = false;                      // 16x16x32 kernel (wide_conv_kernel)
+    static constexpr bool ADMA = false;                     // builtin LDS-DMA (conv_dma16)
     static constexpr int FW = FW_;                          // 16-pixel fragments per wave (wave tile 64 x 16*FW)
     static constexpr int NWV = NWV_;                        // waves per workgroup (4: 2 WGs/CU; 8: 1 WG/CU)
     static constexpr int THREADS = NWV * 64;
@@ -136,8 +137,7 @@ struct ConvCfg {
     // EXP: the input is the max-pool backward of a POOLED gradient (HW/2 x HW/2, bf16 C8) and its
     // routing code: both move by LDS-DMA into a raw staging area (values [XR*THREADS][16 B], code
     // dwords 2 x [XR*THREADS][4 B]) and are expanded from there into the tile (exp_expand), so the
-    // unpooled tensor is never written nor read, and no VGPR-destination load enters the main loop
-    // (hipcc answers one beside LDS-DMA with vmcnt(0), draining the weight stream).
+    // unpooled tensor is never written nor read, and no VGPR-destination load enters the main loop.
     static constexpr bool EXP = EXP_;
     static constexpr int XPR = TR / 2 + 2;                  // pooled rows feeding a tile (with halo)
     static constexpr int XITEMS = 4 * XPR * (HW / 2);       // pooled chunks per 32-channel group
@@ -201,6 +201,21 @@ __device__ __forceinline__ void tile_poff(const TileState& s, int wave, int lane
     }
 }
 
+// LDS-DMA of the conv kernels: C::ADMA selects the asm form (glds16: invisible to hipcc's waitcnt
+// pass) or the builtin. Measured per kernel (tools/ablate_wide.py): the 32x32 forward is faster with
+// asm; wide_conv_kernel with the builtin (the asm statement pins the fragment reads around each DMA),
+// whose only hipcc-inserted drains were at the EXP staging reads/writes — those are asm instead.
+template <class C>
+__device__ __forceinline__ void conv_dma16(const void* src, char* dst) {
+    if constexpr (C::ADMA) glds16(src, lds_u32(dst));
+    else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)dst, 16, 0, 0);
+}
+template <class C>
+__device__ __forceinline__ void conv_dma4(const void* src, char* dst) {
+    if constexpr (C::ADMA) glds4(src, lds_u32(dst));
+    else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)dst, 4, 0, 0);
+}
+
 // input tile of group g (chunks 4g .. 4g+3) -> LDS slot; wave w moves chunk plane w
 template <class C>
 __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, const TileState& s,
@@ -214,7 +229,7 @@ __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, con
     for (int k = 0; k < C::NDW; ++k) {
         const int d = (wave >> 2) + k * C::DSPLIT;
         const char* src = poff[k] >= 0 ? plane + (size_t)poff[k] * 16 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + d * 1024), 16, 0, 0);
+        conv_dma16<C>((const void*)src, dst + d * 1024);
     }
 }
 
@@ -236,9 +251,9 @@ __device__ __forceinline__ void exp_issue(const uint16_t* __restrict__ dp, const
         const size_t idx = ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * PH + (ok ? py : 0)) * PH + px;
         const char* sv = ok ? reinterpret_cast<const char*>(dp) + idx * 16 : zero;
         const char* sc = ok ? reinterpret_cast<const char*>(code) + idx * 8 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)sv, (lds_ptr_t)(raw + i0 * 16), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)sc, (lds_ptr_t)(raw + C::XN * 16 + i0 * 4), 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(sc + 4), (lds_ptr_t)(raw + C::XN * 20 + i0 * 4), 4, 0, 0);
+        conv_dma16<C>((const void*)sv, raw + i0 * 16);
+        conv_dma4<C>((const void*)sc, raw + C::XN * 16 + i0 * 4);
+        conv_dma4<C>((const void*)(sc + 4), raw + C::XN * 20 + i0 * 4);
     }
 }
 
@@ -250,9 +265,8 @@ __device__ __forceinline__ uint4 route_chunk(uint4 v, uint32_t cA, uint32_t cB, 
                       v.z & __builtin_amdgcn_perm(0u, T, cC), v.w & __builtin_amdgcn_perm(0u, T, cD));
 }
 
-// A 16-byte LDS store hipcc does not see: it treats a plain store into LDS that LDS-DMA also writes
-// as aliasing every DMA in flight and drains them all (vmcnt(0)) first. The caller publishes it with
-// its own lgkmcnt wait + barrier.
+// A 16-byte LDS store hipcc does not see (see exp_expand); published by the caller's own lgkmcnt
+// wait + barrier.
 __device__ __forceinline__ void lds_store16(char* p, uint4 v) {
     const uint32_t a = (uint32_t)(size_t)(lds_ptr_t)p;
     const u32x4 d = {v.x, v.y, v.z, v.w};
@@ -286,8 +300,8 @@ __device__ __forceinline__ void exp_expand(char* slot, const char* raw, int tid)
     for (int r = 0; r < C::XR; ++r) {
         const int i = tid + r * C::THREADS;
         if (i >= C::XITEMS) break;
-        // read in one asm statement with its own lgkmcnt wait: hipcc treats a plain LDS read of a
-        // region that LDS-DMA writes as aliasing every DMA in flight and drains them all (vmcnt(0))
+        // one asm statement with its own lgkmcnt wait: beside the builtin LDS-DMA, hipcc drains every
+        // DMA in flight (vmcnt(0)) before a plain LDS access it cannot prove disjoint from them
         const uint32_t a = (uint32_t)(size_t)(lds_ptr_t)(raw + i * 16);
         const uint32_t b = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 16 + i * 4);
         const uint32_t c = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 20 + i * 4);
@@ -322,7 +336,7 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
 #pragma unroll
     for (int i = 0; i < C::NW; ++i) {
         const int j = wave * C::NW + i;
-        __builtin_amdgcn_global_load_lds((const void*)(src + j * 1024 + lane * 16), (lds_ptr_t)(slot + j * 1024), 16, 0, 0);
+        conv_dma16<C>((const void*)(src + j * 1024 + lane * 16), slot + j * 1024);
     }
 }
 
@@ -618,6 +632,7 @@ template <int CI_, int CO_, int HW_, int MODE_>
 struct Conv32Cfg {
     static constexpr int CI = CI_, CO = CO_, HW = HW_, MT = 128, MODE = MODE_;
     static constexpr bool K32 = true;
+    static constexpr bool ADMA = true;                      // asm LDS-DMA (conv_dma16)
     static constexpr int NWV = 4, THREADS = 256;
     static constexpr int WM = 2, WN = 2;                    // waves: 2 along channels x 2 along pixels
     static constexpr int NPX = WN * 128;                    // 256 pixels per tile
@@ -922,7 +937,8 @@ struct WgCfg {
     static constexpr int DC_BYTES = (COB / 8) * NPXP * 16;
     static constexpr int IN_BYTES = (CIB / 8) * NPI * 16;
     static constexpr int BUF = DC_BYTES + IN_BYTES;
-    static constexpr int LDS = 2 * BUF;
+    static constexpr int RAW = EXP ? XITEMS * 24 : 0;    // EXP staging: values [512][16 B], code dwords 2 x [512][4 B]
+    static constexpr int LDS = 2 * BUF + RAW;
     static constexpr int KS = NPX / 32;                  // MFMA k-steps per tile
     static constexpr int RB = HW / TR;
     static constexpr int SLAB = CO * CI * 9 + CO;
@@ -982,21 +998,28 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         tile_of(t, n, rb);
         return n < B;
     };
-    // EXP: pooled dC chunk tid = (plane c, pooled row pr, pooled col px) of tile t
-    auto exp_load_dc = [&](int t, uint4& v, uint2& cw) {
+    // EXP: pooled dC chunk tid = (plane c, pooled row pr, pooled col px) of tile t, staged by this
+    // thread's own wave (LDS-DMA into `raw`), so its expansion needs only that wave's vmcnt wait
+    char* raw = smem + 2 * C::BUF;
+    auto exp_issue_dc = [&](int t) {
         int n, rb;
         tile_of(t, n, rb);
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
         const int c = tid / (PR * PH), rem = tid - c * (PR * PH), pr = rem / PH, px = rem - pr * PH;
         const size_t idx = ((size_t)(n * (C::CO / 8) + cob * 16 + c) * PH + rb * PR + pr) * PH + px;
-        v = reinterpret_cast<const uint4*>(dc)[idx];
-        cw = reinterpret_cast<const uint2*>(dcode)[idx];
+        const int i0 = wave * 64;
+        glds16(reinterpret_cast<const char*>(dc) + idx * 16, lds_u32(raw + i0 * 16));
+        glds4(dcode + idx * 8, lds_u32(raw + C::XITEMS * 16 + i0 * 4));
+        glds4(dcode + idx * 8 + 4, lds_u32(raw + C::XITEMS * 20 + i0 * 4));
     };
-    auto exp_store_dc = [&](char* buf, uint4 v, uint2 cw) {
+    auto exp_expand_dc = [&](char* buf) {
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
         const int c = tid / (PR * PH), rem = tid - c * (PR * PH), pr = rem / PH, px = rem - pr * PH;
-        const uint32_t cA = __builtin_amdgcn_perm(0u, cw.x, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw.x, 0x03030202u);
-        const uint32_t cC = __builtin_amdgcn_perm(0u, cw.y, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw.y, 0x03030202u);
+        const uint4 v = *reinterpret_cast<const uint4*>(raw + tid * 16);
+        const uint32_t c0 = *reinterpret_cast<const uint32_t*>(raw + C::XITEMS * 16 + tid * 4);
+        const uint32_t c1 = *reinterpret_cast<const uint32_t*>(raw + C::XITEMS * 20 + tid * 4);
+        const uint32_t cA = __builtin_amdgcn_perm(0u, c0, 0x01010000u), cB = __builtin_amdgcn_perm(0u, c0, 0x03030202u);
+        const uint32_t cC = __builtin_amdgcn_perm(0u, c1, 0x01010000u), cD = __builtin_amdgcn_perm(0u, c1, 0x03030202u);
         char* base = buf + (c * C::NPXP + 2 * pr * C::HW + 2 * px) * 16;
 #pragma unroll
         for (int pos = 0; pos < 4; ++pos)
@@ -1014,7 +1037,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
             const char* src = reinterpret_cast<const char*>(dc) +
                               (((size_t)((SLK_WIDE_FIXSRC ? 0 : n) * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
                               part * 1024 + lane * 16;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + c * C::NPXP * 16 + part * 1024), 16, 0, 0);
+            glds16((const void*)src, lds_u32(buf + c * C::NPXP * 16 + part * 1024));
         }
         // input halo tile: wave w moves chunk plane w (ND pieces), halo lanes read zeros
         const char* plane = reinterpret_cast<const char*>(in) +
@@ -1026,19 +1049,17 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
             const int y = rb * C::TR - 1 + ry, x = rx - 1;
             const bool ok = P < C::NP && y >= 0 && y < C::HW && x >= 0 && x < C::HW;
             const char* src = ok ? plane + (size_t)(y * C::HW + x) * 16 : reinterpret_cast<const char*>(slk_wide_zero);
-            __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (lds_ptr_t)(buf + C::DC_BYTES + wave * C::NPI * 16 + d * 1024), 16, 0, 0);
+            glds16((const void*)src, lds_u32(buf + C::DC_BYTES + wave * C::NPI * 16 + d * 1024));
         }
     };
 
     int t = ks, b = 0;
-    uint4 xv;
-    uint2 xc;
     if (valid(t)) {
         issue_tile(t, smem);
         if constexpr (C::EXP) {
-            exp_load_dc(t, xv, xc);
-            exp_store_dc(smem, xv, xc);
+            exp_issue_dc(t);
+            wait_vmcnt<0>();
+            exp_expand_dc(smem);
         }
     }
 #pragma unroll 1
@@ -1050,7 +1071,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         const bool more = valid(t + C::KSPLIT);
         if (more) {
             issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
-            if constexpr (C::EXP) exp_load_dc(t + C::KSPLIT, xv, xc);
+            if constexpr (C::EXP) exp_issue_dc(t + C::KSPLIT);
         }
         const char* buf = smem + b * C::BUF;
 #pragma unroll
@@ -1083,9 +1104,13 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
                 if (SLK_WIDE_PRIO & 2) __builtin_amdgcn_s_setprio(0);
             }
         }
-        // EXP: the next tile's dC, routed into the other buffer (free since this tile's barrier)
+        // EXP: the next tile's dC, routed into the other buffer (free since this tile's barrier) once
+        // this wave's staging DMA has landed
         if constexpr (C::EXP) {
-            if (more) exp_store_dc(smem + (b ^ 1) * C::BUF, xv, xc);
+            if (more) {
+                wait_vmcnt<0>();
+                exp_expand_dc(smem + (b ^ 1) * C::BUF);
+            }
         }
         b ^= 1;
     }
@@ -1262,7 +1287,7 @@ __global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __re
             const int c = wave * 2 + (k >> 1), part = k & 1;
             const char* src = reinterpret_cast<const char*>(da1m) + ((size_t)(n * 8 + c) * 1024 + rb * 128) * 16 +
                               part * 1024 + lane * 16;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + c * C1W_NPXP * 16 + part * 1024), 16, 0, 0);
+            glds16((const void*)src, lds_u32(buf + c * C1W_NPXP * 16 + part * 1024));
         }
     };
     const int nimg = B > (int)blockIdx.x ? (B - 1 - (int)blockIdx.x) / C1W_GRID + 1 : 0;

@@ -143,15 +143,7 @@ __device__ __forceinline__ void wino_out(const float (&m)[16], float (&y)[4]) {
 
 }  // namespace
 
-// ============================================================================ LDS-DMA helpers
-// 16-byte LDS-DMA issued as inline asm: hipcc then neither counts it nor inserts its own vmcnt(0) in
-// front of every LDS read (it cannot tell a prefetch buffer from the one being read), so the next
-// band stays in flight under the current band's MFMAs and is retired by a counted wait.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
+// LDS-DMA helpers (glds16): slk_common.h
 
 template <int N>
 __device__ __forceinline__ void wg_wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
