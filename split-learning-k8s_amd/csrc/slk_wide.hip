@@ -39,7 +39,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef SLK_WIDE_XCD
 #define SLK_WIDE_XCD 1
 #endif
-// Profiling only (tools/ablate_wide.py): SLK_WABL = 64 drops the conv epilogues. Production = 0.
+// Profiling only (tools/ablate_wide.py): SLK_WABL bit 64 drops the conv epilogues, bit 128 the EXP
+// expansion in the main loop (results wrong). Production = 0.
 // Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
 // sample 0 (L2-resident): the HBM-read share of a kernel's time.
 #ifndef SLK_WIDE_FIXSRC
@@ -76,9 +77,12 @@ constexpr int MODE_FWD_POOL = 0, MODE_DGRAD_MASK = 2, MODE_DGRAD_PLAIN = 3;
 
 __device__ __attribute__((aligned(64))) uint32_t slk_wide_zero[64];  // zero source for halo lanes
 
+// bf16(a) | bf16(b) << 16, round to nearest even — the instruction the (__bf16) casts compile to, as
+// asm: from the casts hipcc pairs accumulator elements across calls and repacks with 4 extra VALU
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    const __bf16 x = (__bf16)a, y = (__bf16)b;
-    return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+    uint32_t r;
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
@@ -86,6 +90,38 @@ __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w 
 __device__ __forceinline__ float dpp_xor1(float v) {
     // quad_perm [1,0,3,2]: lane l reads lane l^1
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+// Epilogue forms (SLK_WIDE_EPI2 = 0: the first forms, for A/B): relu + 2x2 max-pool by v_max3 and
+// first-equal argmax, bias folded into the accumulator's initial value; the a1 > 0 mask of conv2's
+// dgrad on packed bf16 pairs.
+#ifndef SLK_WIDE_EPI2
+#define SLK_WIDE_EPI2 1
+#endif
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;   // asm: hipcc would canonicalize each operand of a plain fmaxf first
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// relu + max-pool of the window (v0, v1 | v2, v3) as torch's CPU kernel (strict > scan, first max
+// wins): m = max(v, 0); the code is the first i with v_i == m when m > 0 (then relu(v_i) == m iff
+// v_i == m), else CODE_NONE with value +0.
+__device__ __forceinline__ float pool4(float v0, float v1, float v2, float v3, uint32_t& code) {
+    const float m = max3f(max3f(v0, v1, v2), v3, 0.f);
+    uint32_t c = v2 == m ? 2u : 3u;
+    c = v1 == m ? 1u : c;
+    c = v0 == m ? 0u : c;
+    const bool pos = m > 0.f;
+    code = pos ? c : (uint32_t)slk::CODE_NONE;
+    return pos ? m : 0.f;
+}
+// keep the bf16 halves of w where the matching bf16 half of a1w is > 0 (as a signed int16: sign clear,
+// not +0), zero the others. asm: hipcc turns the packed min/max into per-half compares and selects.
+__device__ __forceinline__ uint32_t mask_pos_bf16x2(uint32_t w, uint32_t a1w) {
+    uint32_t k;
+    asm("v_pk_max_i16 %0, %1, 0\n\tv_pk_min_i16 %0, %0, %2\n\tv_pk_sub_u16 %0, 0, %0"
+        : "=&v"(k) : "v"(a1w), "v"(0x00010001u));
+    return w & k;
 }
 
 template <int N>
@@ -453,7 +489,12 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int f = 0; f < C::FW; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int f = 0; f < C::FW; ++f) {
+                if (C::MODE == wide::MODE_FWD_POOL && SLK_WIDE_EPI2)
+                    acc[i][f] = f32x4{bias[i][0], bias[i][1], bias[i][2], bias[i][3]};
+                else
+                    acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
 
 #pragma unroll 1
         for (int g = 0; g < C::G; ++g) {
@@ -494,7 +535,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                             if (g + 1 < C::G) exp_issue<C>(in, out2, cur, g + 1, raw, wave, lane);
                             else exp_issue<C>(in, out2, nxt, 0, raw, wave, lane);
                         }
-                        if (tap == 3) exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
+                        if (tap == 3 && !(SLK_WABL & 128)) exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
                     }
                 } else if (tap == 0) {
                     char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
@@ -548,6 +589,13 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     uint32_t cw = 0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
+                        if (SLK_WIDE_EPI2) {   // the bias is already in the accumulators
+                            const float v0 = acc[i][f][r], v2 = acc[i][fb][r];
+                            uint32_t code;
+                            pv[r] = pool4(v0, dpp_xor1(v0), v2, dpp_xor1(v2), code);
+                            cw |= code << (8 * r);
+                            continue;
+                        }
                         const float v0 = acc[i][f][r] + bias[i][r];
                         const float v2 = acc[i][fb][r] + bias[i][r];
                         const float v1 = dpp_xor1(v0), v3 = dpp_xor1(v2);
@@ -596,6 +644,12 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
                     const uint2 m = em[i][f];
+                    if (SLK_WIDE_EPI2) {
+                        *reinterpret_cast<uint2*>(out + o) =
+                            make_uint2(mask_pos_bf16x2(pack_bf16x2(acc[i][f][0], acc[i][f][1]), m.x),
+                                       mask_pos_bf16x2(pack_bf16x2(acc[i][f][2], acc[i][f][3]), m.y));
+                        continue;
+                    }
                     // a1 > 0 (bf16): sign bit clear and not +0
                     const float v0 = (int)(m.x << 16) > 0 ? acc[i][f][0] : 0.f;
                     const float v1 = (int)(m.x & 0xFFFF0000u) > 0 ? acc[i][f][1] : 0.f;
@@ -793,6 +847,12 @@ __global__ __launch_bounds__(256, 2) void wide_conv32_kernel(const uint16_t* __r
                                 v2 = __shfl_xor(v0, 16, 64);
                             }
                             const float v1 = dpp_xor1(v0), v3 = dpp_xor1(v2);
+                            if (SLK_WIDE_EPI2) {
+                                uint32_t code;
+                                pv[e] = pool4(v0, v1, v2, v3, code);
+                                cw |= code << (8 * e);
+                                continue;
+                            }
                             float best = v0 > 0.f ? v0 : 0.f;
                             int idx = 0;
                             const float r1 = v1 > 0.f ? v1 : 0.f, r2 = v2 > 0.f ? v2 : 0.f, r3 = v3 > 0.f ? v3 : 0.f;
