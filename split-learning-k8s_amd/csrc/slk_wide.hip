@@ -40,7 +40,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define SLK_WIDE_XCD 1
 #endif
 // Profiling only (tools/ablate_wide.py): SLK_WABL bit 64 drops the conv epilogues, bit 128 the EXP
-// expansion in the main loop (results wrong). Production = 0.
+// expansion in the main loop, bit 256 the barrier of odd taps, bit 512 the main loop's vmcnt waits
+// (results wrong). Production = 0.
 // Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
 // sample 0 (L2-resident): the HBM-read share of a kernel's time.
 #ifndef SLK_WIDE_FIXSRC
@@ -503,6 +504,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 const bool last = tail && g == C::G - 1 && tap == 8;
                 // step s+1's weight slice (and at tap 8 the next group's input tile) has landed
                 if (tail) wait_vmcnt<0>();
+                else if (SLK_WABL & 512) {}
                 else if (SLK_WIDE_EPI && tap < 2 && g == 0) {
                     // weight step +1 predates the previous epilogue and this tile's epilogue loads
                     if (tap == 0) {
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 // EXP: the next group's staged items landed by tap 3's wait and were expanded after its
                 // barrier; this wave's tile writes (and raw reads) complete before tap 4's barrier
                 if (C::EXP && tap == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
+                if (!((SLK_WABL & 256) && (tap & 1))) __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
                     const int sl = g * 9 + tap + C::L;
