@@ -40,8 +40,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define SLK_WIDE_XCD 1
 #endif
 // Profiling only (tools/ablate_wide.py): SLK_WABL bit 64 drops the conv epilogues, bit 128 the EXP
-// expansion in the main loop, bit 256 the barrier of odd taps, bit 512 the main loop's vmcnt waits
-// (results wrong). Production = 0.
+// expansion in the main loop, bit 256 the barrier of odd taps, bit 512 the main loop's vmcnt waits,
+// bit 1024 the fragment reads, bit 2048 the DMA issue (8192 weights only, 16384 input only), bit 4096
+// every barrier (results wrong; timing only). Production = 0.
 // Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
 // sample 0 (L2-resident): the HBM-read share of a kernel's time.
 #ifndef SLK_WIDE_FIXSRC
@@ -404,7 +405,7 @@ __device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const
 // out: forward = pooled bf16 C8 [B][CO/8][HW/2][HW/2][8] (+ code u8 same layout in out2);
 //      dgrad-plain / dgrad-mask = bf16 C8 [B][CO/8][HW][HW][8].
 template <class C>
-__global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t* __restrict__ in,
+__global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_kernel(const uint16_t* __restrict__ in,
                                                            const uint16_t* __restrict__ wsh,
                                                            const void* __restrict__ aux,
                                                            uint16_t* __restrict__ out,
@@ -520,16 +521,18 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
                 // EXP: the next group's staged items landed by tap 3's wait and were expanded after its
                 // barrier; this wave's tile writes (and raw reads) complete before tap 4's barrier
                 if (C::EXP && tap == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (!((SLK_WABL & 256) && (tap & 1))) __builtin_amdgcn_s_barrier();
+                if (!((SLK_WABL & 256) && (tap & 1)) && !(SLK_WABL & 4096)) __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
                     const int sl = g * 9 + tap + C::L;
                     int ws = wslot + C::L;
                     ws = ws >= C::RW ? ws - C::RW : ws;
-                    if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                    if (SLK_WABL & (2048 | 8192)) {}
+                    else if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
                     else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
                 }
-                if constexpr (C::EXP) {
+                if (SLK_WABL & (2048 | 16384)) {}
+                else if constexpr (C::EXP) {
                     // next group's pooled input: staged by LDS-DMA at tap 0, expanded into the free
                     // slot at tap 3 (read from tap 8 on)
                     if (g + 1 < C::G || !tail) {
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(C::THREADS, 2) void wide_conv_kernel(const uint16_t
 #pragma unroll
                 for (int f = 0; f < C::FW; ++f) bv[f] = bv_n[f];
                 const int wn1 = wslot + 1 == C::RW ? 0 : wslot + 1;
-                if (!last) {
+                if (!last && !(SLK_WABL & 1024)) {
                     const char* wb = wslot0 + wn1 * C::W_SLOT;
                     const char* ib = islot0 + (tap == 8 ? (islot ^ 1) : islot) * C::IN_SLOT;
                     const int tn = tap == 8 ? 0 : tap + 1;
