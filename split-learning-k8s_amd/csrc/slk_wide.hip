@@ -53,6 +53,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 // Wave priority: raise it around each step's MFMA block (1: conv kernels, 2: also wgrad), so a wave
 // with MFMAs ready issues ahead of a co-resident wave's epilogue VALU / staging work.
+#ifndef SLK_WIDE_DMA_LATE
+#define SLK_WIDE_DMA_LATE 0
+#endif
 #ifndef SLK_WIDE_PRIO
 #define SLK_WIDE_PRIO 0
 #endif
@@ -523,29 +526,36 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                 if (C::EXP && tap == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (!((SLK_WABL & 256) && (tap & 1)) && !(SLK_WABL & 4096)) __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
-                {   // weight step +3 into the slot of step -1; at tap 0 the next group's input tile
-                    const int sl = g * 9 + tap + C::L;
-                    int ws = wslot + C::L;
-                    ws = ws >= C::RW ? ws - C::RW : ws;
-                    if (SLK_WABL & (2048 | 8192)) {}
-                    else if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
-                    else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
-                }
-                if (SLK_WABL & (2048 | 16384)) {}
-                else if constexpr (C::EXP) {
-                    // next group's pooled input: staged by LDS-DMA at tap 0, expanded into the free
-                    // slot at tap 3 (read from tap 8 on)
-                    if (g + 1 < C::G || !tail) {
-                        if (tap == 0) {
+                // weight step +3 into the slot of step -1; at tap 0 the next group's input tile. Both
+                // after this step's MFMAs when SLK_WIDE_DMA_LATE (same order of VMEM operations, so
+                // the counted waits are unchanged; every target slot is free since the barrier).
+                auto issue_dma = [&]() {
+                    {
+                        const int sl = g * 9 + tap + C::L;
+                        int ws = wslot + C::L;
+                        ws = ws >= C::RW ? ws - C::RW : ws;
+                        if (SLK_WABL & (2048 | 8192)) {}
+                        else if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                        else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
+                    }
+                    if (SLK_WABL & (2048 | 16384)) {}
+                    else if constexpr (C::EXP) {
+                        if ((g + 1 < C::G || !tail) && tap == 0) {
                             if (g + 1 < C::G) exp_issue<C>(in, out2, cur, g + 1, raw, wave, lane);
                             else exp_issue<C>(in, out2, nxt, 0, raw, wave, lane);
                         }
-                        if (tap == 3 && !(SLK_WABL & 128)) exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
+                    } else if (tap == 0) {
+                        char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
+                        if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
+                        else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
                     }
-                } else if (tap == 0) {
-                    char* nslot = islot0 + (islot ^ 1) * C::IN_SLOT;
-                    if (g + 1 < C::G) issue_input<C>(in, cur, pcur, g + 1, nslot, wave, lane);
-                    else if (!tail) issue_input<C>(in, nxt, pnxt, 0, nslot, wave, lane);
+                };
+                if (!SLK_WIDE_DMA_LATE) issue_dma();
+                // EXP: the next group's pooled input, staged by LDS-DMA at tap 0, is expanded into the
+                // free slot at tap 3 (read from tap 8 on)
+                if constexpr (C::EXP) {
+                    if ((g + 1 < C::G || !tail) && tap == 3 && !(SLK_WABL & 128))
+                        exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
                 }
                 bf16x8 av[4], bv[C::FW];
 #pragma unroll
@@ -570,6 +580,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                     for (int f = 0; f < C::FW; ++f)
                         acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[f], acc[i][f], 0, 0, 0);
                 if (SLK_WIDE_PRIO) __builtin_amdgcn_s_setprio(0);
+                if (SLK_WIDE_DMA_LATE) issue_dma();
                 wslot = wn1;
             }
             islot ^= 1;
