@@ -182,6 +182,25 @@ int slk_mnist_batch(const uint8_t* images, const uint8_t* labels, int n_images, 
                     int B, float mean, float std, float* x, int64_t* y, int* err_flag, void* stream);
 
 
+/* ================================================================ lossless cut-exchange codec (K3 / K4)
+ * The multi-GPU topologies move the cut over RCCL instead of the reference's pickled HTTP body
+ * (src/client_part.py:117-125 activations out, src/server_part.py:57-58 gradient back). The cut is a
+ * ReLU output (about half zeros), so a micro-batch of n elements travels as mask (ceil(n/32) uint32
+ * words: bit set where the element's bit pattern is nonzero) + the set elements in order, and the cut
+ * gradient as its values at the same set positions only (the client applies its own ReLU mask, a subset
+ * of the set bits, before using the gradient; the left-out positions never reach a result). Blocks of
+ * 2048 elements: counts/offsets hold slk_cut_blocks(n) ints, total one int (the number of set bits).
+ *   encode : mask, per-block counts, exclusive offsets, total, and the packed values of x;
+ *   offsets: counts, offsets, total from a received mask;
+ *   pack   : the values of x at the mask's set positions (the gradient direction);
+ *   unpack : x = the values scattered to the set positions, zeros elsewhere. */
+int slk_cut_blocks(int64_t n);
+int slk_cut_encode(const float* x, int64_t n, uint32_t* mask, int* counts, int* offsets, int* total, float* vals,
+                   void* stream);
+int slk_cut_offsets(const uint32_t* mask, int64_t n, int* counts, int* offsets, int* total, void* stream);
+int slk_cut_pack(const float* x, int64_t n, const uint32_t* mask, const int* offsets, float* vals, void* stream);
+int slk_cut_unpack(const float* vals, int64_t n, const uint32_t* mask, const int* offsets, float* x, void* stream);
+
 /* ================================================================ widened split CNN (BASELINE config 5)
  * The reference has no such model: these entry points run the north star's
  * widened config — client conv1 3->64 (32x32) + ReLU, conv2 64->128 + ReLU + pool, conv3 128->256 +

@@ -19,10 +19,16 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _U = ctypes.c_uint
+_L = ctypes.c_int64
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 _SIGS = {
     "slk_abi_version": [],
+    "slk_cut_blocks": [_L],
+    "slk_cut_encode": [_P, _L, _P, _P, _P, _P, _P, _P],
+    "slk_cut_offsets": [_P, _L, _P, _P, _P, _P],
+    "slk_cut_pack": [_P, _L, _P, _P, _P, _P],
+    "slk_cut_unpack": [_P, _L, _P, _P, _P, _P],
     "slk_error_string": [_I],
     "slk_build_id": [],
     "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],

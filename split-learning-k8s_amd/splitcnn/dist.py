@@ -126,14 +126,31 @@ class Replicated:
 
 
 class Pipeline:
-    """2-rank client/server pipeline with m micro-batches. `role` is "client" or "server"."""
+    """2-rank client/server pipeline with m micro-batches. `role` is "client" or "server".
 
-    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None):
+    compress (default on for CUDA tensors): the cut and its gradient travel through the lossless
+    sparse codec (codec.py): per step one int32 header with the m micro-batches' nonzero counts, then
+    per micro-batch the bit mask + the nonzero activations out and the gradient at those positions back.
+    Results are bit-identical to the dense exchange; `exchange_bytes` counts what actually moved and
+    `dense_bytes` what the dense exchange would have moved."""
+
+    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None, compress: bool = True):
         assert role in ("client", "server")
         self.stage, self.role, self.peer, self.micro, self.group = stage, role, peer, micro, group
+        self.compress = compress
         self.global_step = 0
         self._bufs = {}
         self.exchange_bytes = 0
+        self.dense_bytes = 0
+        self._codec = None
+
+    def _use_codec(self, device):
+        if not (self.compress and torch.device(device).type == "cuda"):
+            return None
+        if self._codec is None:
+            from .codec import CutCodec
+            self._codec = CutCodec()
+        return self._codec
 
     def _buf(self, name, shape, dtype, device):
         t = self._bufs.get(name)
@@ -151,6 +168,9 @@ class Pipeline:
         dev = x.device
         acts = self._buf("acts", (B, 32, 26, 26), torch.float32, dev)
         cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, dev)
+        codec = self._use_codec(dev)
+        if codec is not None:
+            return self._client_step_codec(codec, x, y, acts, cuts, m, mb)
         sends, recvs = [], []
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
@@ -167,7 +187,43 @@ class Pipeline:
         for w in sends:
             w.wait()
         c.step()
-        self.exchange_bytes = 2 * acts.numel() * 4 + y.numel() * 8
+        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + y.numel() * 8
+        self.global_step += 1
+
+    def _client_step_codec(self, codec, x, y, acts, cuts, m, mb):
+        c = self.stage
+        n = mb * 32 * 26 * 26
+        bufs = []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            c.forward(x[sl], out=acts[sl])
+            b = codec.buffers(("c", k), n, x.device)
+            codec.encode(acts[sl], b)
+            bufs.append(b)
+        head = self._buf("head", (m,), torch.int32, x.device)
+        for k in range(m):
+            head[k:k + 1].copy_(bufs[k][3])
+        totals = head.tolist()            # the one host sync of the step: sizes of the sparse payloads
+        sends = [isend(head, self.peer, group=self.group)]
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            sends.append(isend(bufs[k][0], self.peer, group=self.group))
+            sends.append(isend(y[sl], self.peer, group=self.group))
+            if totals[k]:
+                sends.append(isend(bufs[k][4][:totals[k]], self.peer, group=self.group))
+        gv = [self._buf(("gvals", k), (n,), torch.float32, x.device) for k in range(m)]
+        recvs = [irecv(gv[k][:totals[k]], self.peer, group=self.group) if totals[k] else None for k in range(m)]
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            if recvs[k] is not None:
+                recvs[k].wait()
+            codec.unpack(cuts[sl], bufs[k], vals=gv[k])
+            c.backward(cuts[sl], x=x[sl], act=acts[sl], accumulate=k > 0)
+        for w in sends:
+            w.wait()
+        c.step()
+        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + y.numel() * 8
+        self.dense_bytes = 2 * acts.numel() * 4 + y.numel() * 8
         self.global_step += 1
 
     def server_step(self, B: int, device):
@@ -178,6 +234,9 @@ class Pipeline:
         labels = self._buf("labels", (B,), torch.int64, device)
         cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, device)
         parts = self._buf("loss_parts", (m,), torch.float32, device)
+        codec = self._use_codec(device)
+        if codec is not None:
+            return self._server_step_codec(codec, B, device, acts, labels, cuts, parts, m, mb)
         recvs = []
         for k in range(m):
             sl = slice(k * mb, (k + 1) * mb)
@@ -195,22 +254,64 @@ class Pipeline:
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:
             w.wait()
-        self.exchange_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.global_step += 1
+
+    def _server_step_codec(self, codec, B, device, acts, labels, cuts, parts, m, mb):
+        s = self.stage
+        n = mb * 32 * 26 * 26
+        head = self._buf("head", (m,), torch.int32, device)
+        irecv(head, self.peer, group=self.group).wait()
+        totals = head.tolist()            # the one host sync of the step: sizes of the sparse payloads
+        bufs, recvs = [], []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            b = codec.buffers(("s", k), n, device)
+            bufs.append(b)
+            rk = [irecv(b[0], self.peer, group=self.group), irecv(labels[sl], self.peer, group=self.group)]
+            if totals[k]:
+                rk.append(irecv(b[4][:totals[k]], self.peer, group=self.group))
+            recvs.append(rk)
+        sends = []
+        for k in range(m):
+            sl = slice(k * mb, (k + 1) * mb)
+            for r in recvs[k]:
+                r.wait()
+            codec.offsets(n, bufs[k])
+            codec.unpack(acts[sl], bufs[k])
+            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / B, accumulate=k > 0, cut_grad=cuts[sl])
+            _loss_sum(loss_i, 1.0 / B, parts[k:k + 1])
+            gv = self._buf(("gvals", k), (n,), torch.float32, device)
+            codec.pack(cuts[sl], bufs[k], vals=gv)
+            if totals[k]:
+                sends.append(isend(gv[:totals[k]], self.peer, group=self.group))
+        s.step()
+        s.log_loss(parts, scale=1.0, step=self.global_step)
+        for w in sends:
+            w.wait()
+        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + labels.numel() * 8
+        self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
         self.global_step += 1
 
 
 class Hub:
-    """N-1 client ranks (0..N-2) feed one server rank (N-1)."""
+    """N-1 client ranks (0..N-2) feed one server rank (N-1). `compress` as for Pipeline: per client
+    and step one int32 header of the micro-batch nonzero counts, then mask + values each way."""
 
-    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1):
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress: bool = True):
         self.stage, self.rank, self.world = stage, rank, world
         self.server_rank = world - 1
         self.nclients = world - 1
         self.client_group = client_group
         self.micro = micro
+        self.compress = compress
         self.global_step = 0
         self._bufs = {}
         self.exchange_bytes = 0
+        self.dense_bytes = 0
+        self._codec = None
+
+    _use_codec = Pipeline._use_codec
 
     @property
     def is_server(self):
@@ -232,6 +333,9 @@ class Hub:
         b = B // m
         act = self._buf("act", (B, 32, 26, 26), torch.float32, x.device)
         cut = self._buf("cut", (B, 32, 26, 26), torch.float32, x.device)
+        codec = self._use_codec(x.device)
+        if codec is not None:
+            return self._client_step_codec(codec, x, y, act, cut, m, b)
         sends, recvs = [], []
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
@@ -249,7 +353,45 @@ class Hub:
         if self.nclients > 1:
             dist.all_reduce(c.grads, group=self.client_group)
         c.step()
-        self.exchange_bytes = 2 * act.numel() * 4 + y.numel() * 8
+        self.exchange_bytes = self.dense_bytes = 2 * act.numel() * 4 + y.numel() * 8
+        self.global_step += 1
+
+    def _client_step_codec(self, codec, x, y, act, cut, m, b):
+        c = self.stage
+        n = b * 32 * 26 * 26
+        bufs = []
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            c.forward(x[sl], out=act[sl])
+            bk = codec.buffers(("c", k), n, x.device)
+            codec.encode(act[sl], bk)
+            bufs.append(bk)
+        head = self._buf("head", (m,), torch.int32, x.device)
+        for k in range(m):
+            head[k:k + 1].copy_(bufs[k][3])
+        totals = head.tolist()
+        sends = [isend(head, self.server_rank)]
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            sends.append(isend(bufs[k][0], self.server_rank))
+            sends.append(isend(y[sl], self.server_rank))
+            if totals[k]:
+                sends.append(isend(bufs[k][4][:totals[k]], self.server_rank))
+        gv = [self._buf(("gvals", k), (n,), torch.float32, x.device) for k in range(m)]
+        recvs = [irecv(gv[k][:totals[k]], self.server_rank) if totals[k] else None for k in range(m)]
+        for k in range(m):
+            sl = slice(k * b, (k + 1) * b)
+            if recvs[k] is not None:
+                recvs[k].wait()
+            codec.unpack(cut[sl], bufs[k], vals=gv[k])
+            c.backward(cut[sl], x=x[sl], act=act[sl], accumulate=k > 0)
+        for w in sends:
+            w.wait()
+        if self.nclients > 1:
+            dist.all_reduce(c.grads, group=self.client_group)
+        c.step()
+        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + y.numel() * 8
+        self.dense_bytes = 2 * act.numel() * 4 + y.numel() * 8
         self.global_step += 1
 
     def server_step(self, B: int, device):
@@ -262,6 +404,9 @@ class Hub:
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         parts = self._buf("loss_parts", (m * nc,), torch.float32, device)
+        codec = self._use_codec(device)
+        if codec is not None:
+            return self._server_step_codec(codec, B, device, acts, labels, cuts, parts)
         reqs = {}
         for c in range(nc):
             for k in range(m):
@@ -281,7 +426,53 @@ class Hub:
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:
             w.wait()
-        self.exchange_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        self.global_step += 1
+
+    def _server_step_codec(self, codec, B, device, acts, labels, cuts, parts):
+        s = self.stage
+        m, nc = self.micro, self.nclients
+        b, G = B // m, nc * B
+        n = b * 32 * 26 * 26
+        heads = [self._buf(("head", c), (m,), torch.int32, device) for c in range(nc)]
+        hreq = [irecv(heads[c], c) for c in range(nc)]
+        totals = {}
+        for c in range(nc):
+            hreq[c].wait()
+            for k, t in enumerate(heads[c].tolist()):
+                totals[c, k] = t
+        reqs, bufs = {}, {}
+        for c in range(nc):
+            for k in range(m):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                bk = codec.buffers(("s", c, k), n, device)
+                bufs[c, k] = bk
+                rk = [irecv(bk[0], c), irecv(labels[sl], c)]
+                if totals[c, k]:
+                    rk.append(irecv(bk[4][:totals[c, k]], c))
+                reqs[c, k] = rk
+        sends, part = [], 0
+        for k in range(m):
+            for c in range(nc):
+                sl = slice(c * B + k * b, c * B + (k + 1) * b)
+                for r in reqs[c, k]:
+                    r.wait()
+                codec.offsets(n, bufs[c, k])
+                codec.unpack(acts[sl], bufs[c, k])
+                _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=part > 0, cut_grad=cuts[sl])
+                _loss_sum(loss_i, 1.0 / G, parts[part:part + 1])
+                gv = self._buf(("gvals", c, k), (n,), torch.float32, device)
+                codec.pack(cuts[sl], bufs[c, k], vals=gv)
+                if totals[c, k]:
+                    sends.append(isend(gv[:totals[c, k]], c))
+                part += 1
+        s.step()
+        s.log_loss(parts, scale=1.0, step=self.global_step)
+        for w in sends:
+            w.wait()
+        self.exchange_bytes = (nc * m * 4 + sum(bufs[key][0].numel() * 4 + 2 * t * 4 for key, t in totals.items())
+                               + labels.numel() * 8)
+        self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
         self.global_step += 1
 
 

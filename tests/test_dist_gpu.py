@@ -216,7 +216,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, topo, fixture, micro, outdir):
+def _worker(rank, world, port, topo, fixture, micro, outdir, compress=True):
     import sys
     sys.path[:0] = [PKG, ROOT, os.path.join(ROOT, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -233,9 +233,9 @@ def _worker(rank, world, port, topo, fixture, micro, outdir):
     try:
         if topo == "pipeline":
             if rank == 0:
-                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro)
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=compress)
             else:
-                t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro)
+                t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=compress)
             for s in range(1, nsteps + 1):
                 x = torch.from_numpy(fx[f"x_{s}"]).to(dev)
                 y = torch.from_numpy(fx[f"y_{s}"]).to(dev)
@@ -244,6 +244,7 @@ def _worker(rank, world, port, topo, fixture, micro, outdir):
                     res[f"act_{s}"] = t._bufs["acts"].cpu().numpy()
                     res[f"params_{s}"] = t.stage.params.cpu().numpy()
                     res[f"grads_{s}"] = t.stage.grads.cpu().numpy()
+                    res[f"bytes_{s}"] = np.array([t.exchange_bytes, t.dense_bytes])
                 else:
                     t.server_step(x.shape[0], dev)
                     res[f"cut_{s}"] = t._bufs["cuts"].cpu().numpy()
@@ -259,18 +260,19 @@ def _worker(rank, world, port, topo, fixture, micro, outdir):
             y = torch.from_numpy(fx["y_1"]).to(dev)
             B = x.shape[0] // nc
             if rank < nc:
-                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro)
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=compress)
                 sl = slice(rank * B, (rank + 1) * B)
                 t.client_step(x[sl].contiguous(), y[sl].contiguous())
                 res["act_1"] = t._bufs["act"].cpu().numpy()
             else:
-                t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro)
+                t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=compress)
                 t.server_step(B, dev)
                 res["cut_1"] = t._bufs["cuts"].cpu().numpy()
                 torch.cuda.synchronize()
                 res["losses"] = np.array([l for _, l in t.stage.loss_log.flush()])
             res["params_1"] = t.stage.params.cpu().numpy()
             res["grads_1"] = t.stage.grads.cpu().numpy()
+            res["bytes_1"] = np.array([t.exchange_bytes, t.dense_bytes])
         elif topo == "replicated":
             x = torch.from_numpy(fx["x_1"]).to(dev)
             y = torch.from_numpy(fx["y_1"]).to(dev)
@@ -307,9 +309,10 @@ def _worker(rank, world, port, topo, fixture, micro, outdir):
         dist.destroy_process_group()
 
 
-def _spawn(world, topo, fixture, micro, outdir):
+def _spawn(world, topo, fixture, micro, outdir, compress=True):
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(world, _port(), topo, fixture, micro, str(outdir)), nprocs=world, join=True)
+    os.makedirs(outdir, exist_ok=True)
+    mp.spawn(_worker, args=(world, _port(), topo, fixture, micro, str(outdir), compress), nprocs=world, join=True)
     return [dict(np.load(os.path.join(outdir, f"r{r}.npz"))) for r in range(world)]
 
 
@@ -387,3 +390,22 @@ def test_widened_splitfed_hub_vs_fused_step(gpu, tmp_path):
         want, _, _ = W.adam(flat0, g, np.zeros_like(g), np.zeros_like(g), 1)
         tol = 1e-6 * np.abs(want - flat0).max() + 2 * np.finfo(np.float32).eps * np.abs(want)
         assert (np.abs(out[r]["params_1"].astype(np.float64) - want) <= tol).all(), r
+
+
+@pytest.mark.parametrize("topo,world,micro,fixture", [("pipeline", 2, 2, "split_step_b4.npz"),
+                                                      ("hub", 3, 2, "split_step_b12.npz")])
+def test_cut_codec_bit_identical_to_dense(gpu, tmp_path, topo, world, micro, fixture):
+    """The sparse cut codec (the default on CUDA tensors) vs the dense exchange (compress=False):
+    every rank's weights, gradients and losses are BIT-identical; the codec moved fewer bytes; the
+    cut activations the client kept are the same."""
+    dense = _spawn(world, topo, fixture, micro, tmp_path / "dense", compress=False)
+    sparse = _spawn(world, topo, fixture, micro, tmp_path / "sparse", compress=True)
+    for r in range(world):
+        for k in dense[r]:
+            if k.startswith("bytes_"):
+                continue
+            assert np.array_equal(dense[r][k], sparse[r][k]), (r, k)
+        for k in sparse[r]:
+            if k.startswith("bytes_"):
+                moved, full = sparse[r][k]
+                assert dense[r][k][0] == dense[r][k][1] == full and 0 < moved < full, (r, k, moved, full)
