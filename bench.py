@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU (per-client) batch")
     ap.add_argument("--topology", default="auto", choices=["auto", "replicated", "pipeline", "hub"])
     ap.add_argument("--micro", type=int, default=4, help="micro-batches of the pipeline / hub topologies")
+    ap.add_argument("--dense-exchange", action="store_true",
+                    help="pipeline / hub: ship the dense cut + gradient instead of the lossless sparse codec")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -253,6 +255,8 @@ def run_distributed(args, out, rank, world, local):
     X, Y = make_pool(B, 4, dev, seed=42 + rank)
     grp = sd.client_group_for(world)   # every rank creates it (collective), used by hub topologies
 
+    codec = not args.dense_exchange
+
     def build(topology, micro):
         a, b = init_models(seed=0)
         if topology == "replicated":
@@ -261,15 +265,15 @@ def run_distributed(args, out, rank, world, local):
         if topology == "pipeline":
             assert world == 2
             if rank == 0:
-                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro)
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=codec)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
-            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro)
+            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec)
             return (lambda i: t.server_step(B, dev)), t, B
         if topology == "hub":
             if rank < world - 1:
-                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro)
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=codec)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
-            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro)
+            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec)
             return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
         raise ValueError(topology)
 
@@ -281,6 +285,16 @@ def run_distributed(args, out, rank, world, local):
                     "activations and cut gradients",
         "hub": "K4: SplitFed, N-1 client GPUs feeding 1 server GPU (reference cut), micro-batched RCCL "
                "send/recv, client-gradient all-reduce"}
+    cut_codec = ("lossless sparse codec: ReLU-cut bit mask + nonzero values out, gradient at those positions back "
+                 "(bit-identical results)" if codec else "dense fp32")
+
+    def wire(t):
+        """rank 0 is a client in both exchange topologies: its link's bytes (both directions, labels and
+        codec headers included) actually moved vs what the dense exchange moves."""
+        v = torch.tensor([float(getattr(t, "exchange_bytes", 0)), float(getattr(t, "dense_bytes", 0))],
+                         dtype=torch.float64, device=dev)
+        dist.broadcast(v, 0)
+        return int(v[0].item()), int(v[1].item())
     fn, t, global_batch = build(topo, args.micro)
     progress(f"{topo} x{world}: timing {args.steps} steps")
     dt = timed(fn, args.steps, args.warmup, dev)
@@ -290,8 +304,10 @@ def run_distributed(args, out, rank, world, local):
     out["scaling"] = "weak"
     if topo != "replicated":
         out["config"]["micro_batches"] = args.micro
-        out["exchange"] = {"bytes_per_step_each_direction": B * CUT_BYTES * (1 if topo == "pipeline" else world - 1),
-                           "GBps_per_direction": round(t.exchange_bytes / 2 / (dt / args.steps) / 1e9, 2)}
+        moved, dense = wire(t)
+        out["exchange"] = {"cut_codec": cut_codec, "link_bytes_per_step_moved": moved, "link_bytes_per_step_dense": dense,
+                           "dense_equivalent_GBps_per_link_per_direction": round(dense / 2 / (dt / args.steps) / 1e9, 2),
+                           "wire_GBps_per_link_per_direction": round(moved / 2 / (dt / args.steps) / 1e9, 2)}
 
     peak = None
     if not args.no_exchange_phase:
@@ -313,14 +329,18 @@ def run_distributed(args, out, rank, world, local):
             K2 = args.exchange_steps
             progress(f"{key} x{world}: timing {K2} steps")
             dt2 = timed(fn2, K2, 2, dev)
-            per_dir = B * CUT_BYTES          # one client link, one direction, per step
-            gbps = per_dir / (dt2 / K2) / 1e9
+            per_dir = B * CUT_BYTES          # one client link, one direction, per step, dense
+            moved, dense = wire(t2)
+            gbps = per_dir / (dt2 / K2) / 1e9                    # dense-equivalent cut rate
+            wgbps = moved / 2 / (dt2 / K2) / 1e9                 # what actually crossed the link
             r = {"workload": labels[ex], "samples_per_s": round(K2 * gb2 / dt2, 1), "ms_per_step": round(dt2 / K2 * 1e3, 3),
-                 "global_batch": gb2, "per_client_batch": B, "micro_batches": args.micro,
+                 "global_batch": gb2, "per_client_batch": B, "micro_batches": args.micro, "cut_codec": cut_codec,
                  "cut_bytes_per_link_per_direction_per_step": per_dir,
+                 "link_bytes_per_step_moved": moved, "link_bytes_per_step_dense": dense,
                  "exchange_GBps_per_link_per_direction": round(gbps, 2),
-                 "exchange_frac_of_measured_p2p_peak": round(gbps / peak, 3) if peak else None,
-                 "exchange_frac_of_vendor_link": round(gbps / XGMI_LINK_GBPS, 3)}
+                 "wire_GBps_per_link_per_direction": round(wgbps, 2),
+                 "wire_frac_of_measured_p2p_peak": round(wgbps / peak, 3) if peak else None,
+                 "wire_frac_of_vendor_link": round(wgbps / XGMI_LINK_GBPS, 3)}
             if ex == "hub":
                 r["server_inbound_GBps_all_links"] = round(gbps * (world - 1), 2)
             out[key] = r
