@@ -408,15 +408,29 @@ __device__ __forceinline__ void mfma_ac(f32x4& acc, float a, float b, const f32x
 #endif
 }
 
-__device__ __forceinline__ void wf2_dma_band(const float* __restrict__ act, int band, const float* dst, int half, int lane) {
+// A band's staging DMA: wave pair half h moves chunks c = h, h+2, ... (< WF_CHUNKS) of 64 sixteen-byte
+// pieces; piece (c, lane) = channel p / 65, 16-byte column p % 65 of the band (p = 64 c + lane). The
+// per-lane byte offsets from the band's first float are the same for every band, so they are computed
+// once per launch and each piece is one saddr-form DMA (no VALU address arithmetic, no loop branch:
+// the per-piece division, address and branch code had cost ~150 cycles per piece beside the MFMAs).
+constexpr int WF_PPW = (WF_CHUNKS + 1) / 2;   // pieces per wave and band (17 for half 0, 16 for half 1)
+__device__ __forceinline__ void wf2_dma_offsets(int half, int lane, uint32_t (&off)[WF_PPW]) {
+#pragma unroll
+    for (int i = 0; i < WF_PPW; ++i) {
+        const int p = min((half + 2 * i) * 64 + lane, WF_PIECES - 1);
+        const int ci = p / 65, k = p - 65 * (p / 65);
+        off[i] = (uint32_t)(ci * A_PIX + 4 * k) * 4u;
+    }
+}
+__device__ __forceinline__ void wf2_dma_band(const float* __restrict__ act, int band, const float* dst, int half,
+                                             const uint32_t (&off)[WF_PPW]) {
     const int b = band / 3, bs = band - 3 * (band / 3);
     const float* src = act + (size_t)b * A_SAMPLE + bs * 8 * A_HW;
-    const uint32_t base = (uint32_t)(uintptr_t)dst;
-#pragma unroll 1
-    for (int c = half; c < WF_CHUNKS; c += 2) {
-        const int p = min(c * 64 + lane, WF_PIECES - 1);
-        const int ci = p / 65, k = p - 65 * (p / 65);
-        glds16(src + ci * A_PIX + 4 * k, __builtin_amdgcn_readfirstlane(base + c * 1024));
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+#pragma unroll
+    for (int i = 0; i < WF_PPW; ++i) {
+        const int c = half + 2 * i;
+        if (c < WF_CHUNKS) glds16_so(src, off[i], base + c * 1024);
     }
 }
 
@@ -432,8 +446,10 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino2_kernel(
     const int nband = 3 * B, nsu = (nband + 1) >> 1;
     float* bufs = smem + 2 * pr * WF_BSTR;
 
+    uint32_t doff[WF_PPW];
+    wf2_dma_offsets(mh, lane, doff);
     int su = blockIdx.x;
-    if (2 * su + pr < nband) wf2_dma_band(act, 2 * su + pr, bufs, mh, lane);
+    if (2 * su + pr < nband) wf2_dma_band(act, 2 * su + pr, bufs, mh, doff);
 
     // transformed filters (co = 32mh + 16m + li, ci = 4s + lk) and the bias of this lane's rows
     float uw[2][8][16];
@@ -465,7 +481,7 @@ __global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino2_kernel(
         wg_wait_vmcnt<48>();
         lds_barrier();
         const int nb = 2 * (su + gridDim.x) + pr;
-        if (nb < nband) wf2_dma_band(act, nb, bufs + (buf ^ 1) * WF_BSTR, mh, lane);
+        if (nb < nband) wf2_dma_band(act, nb, bufs + (buf ^ 1) * WF_BSTR, mh, doff);
         const int band = 2 * su + pr;
         if (band < nband) {
             const float* img = bufs + buf * WF_BSTR;
@@ -892,33 +908,61 @@ __device__ __forceinline__ void ww_wait_newest_batch() { wg_wait_vmcnt<(WW_NCH -
 static_assert(WW_DP_OFF * 4 == WF_CHUNKS * 1024 && WW_CD_OFF * 4 == (WF_CHUNKS + WW_DP_CH) * 1024,
               "the three staging regions are consecutive KiB chunks");
 
-// chunks i0 .. i1-1 of this wave's share (chunk c = wave + 4i) of unit u's staging DMA
+// chunks i0 .. i1-1 of this wave's share (chunk c = wave + 4i) of unit u's staging DMA. Piece (c, lane)'s
+// byte offset from its region's first element (act band, dpooled band or code band of the unit) is
+// the same for every unit: the offsets are computed once per launch into an LDS table (this kernel has
+// no VGPRs to spare) and a piece is one saddr-form DMA from a scalar region base — the per-piece
+// divisions, 64-bit address arithmetic and region branches had cost ~200 cycles per piece beside the
+// MFMAs (16 % of the kernel: dropping the DMA issue took it from 0.414 to 0.346 ms).
+constexpr int WW_PPW = (WW_NCH + WW_WAVES - 1) / WW_WAVES;   // 13 pieces per wave and unit
+constexpr int WW_TQ = (WW_PPW + 3) / 4;                      // uint4 table entries per lane
+__device__ __forceinline__ uint32_t ww_piece_offset(int c, int lane) {
+    if (c < WF_CHUNKS) {
+        const int p = min(c * 64 + lane, WF_PIECES - 1);
+        const int ci = p / 65, k = p - 65 * (p / 65);
+        return (uint32_t)(ci * A_PIX + 4 * k) * 4u;
+    } else if (c < WF_CHUNKS + WW_DP_CH) {
+        const int p = (c - WF_CHUNKS) * 64 + lane;
+        const int co = p / 13, k = min(p - 13 * (p / 13), 11);
+        return (uint32_t)(co * P_WIN + 4 * k) * 4u;
+    }
+    const int p = (c - WF_CHUNKS - WW_DP_CH) * 64 + lane;
+    const int co = p / WW_CD_PC, k = min(p - WW_CD_PC * (p / WW_CD_PC), 2);
+    return (uint32_t)(co * P_WIN + 16 * k);
+}
+__device__ __forceinline__ void ww_dma_table(uint4* tab, int wave, int lane) {
+#pragma unroll
+    for (int q = 0; q < WW_TQ; ++q) {
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = wave + WW_WAVES * (4 * q + j);
+            o[j] = c < WW_NCH ? ww_piece_offset(c, lane) : 0u;
+        }
+        tab[(wave * WW_TQ + q) * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
 __device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const float* __restrict__ dpool,
                                             const uint8_t* __restrict__ code, int u, const float* dst, int wave,
-                                            int lane, int i0 = 0, int i1 = 1 << 20) {
+                                            int lane, const uint4* tab, int i0 = 0, int i1 = 1 << 20) {
     if (SLK_WW_ABL & 1024) u = blockIdx.x;
     const int b = u / 3, band = u - 3 * (u / 3);
-    const uint32_t base = (uint32_t)(uintptr_t)dst;
-    const float* asrc = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
-    const float* dsrc = dpool + (size_t)b * P_SAMPLE + band * 48;
-    const uint8_t* csrc = code + (size_t)b * P_SAMPLE + band * 48;
-#pragma unroll 1
-    for (int c = wave + WW_WAVES * i0; c < WW_NCH && c < wave + WW_WAVES * i1; c += WW_WAVES) {
-        const void* src;
-        if (c < WF_CHUNKS) {
-            const int p = min(c * 64 + lane, WF_PIECES - 1);
-            const int ci = p / 65, k = p - 65 * (p / 65);
-            src = asrc + ci * A_PIX + 4 * k;
-        } else if (c < WF_CHUNKS + WW_DP_CH) {
-            const int p = (c - WF_CHUNKS) * 64 + lane;
-            const int co = p / 13, k = min(p - 13 * (p / 13), 11);
-            src = dsrc + co * P_WIN + 4 * k;
-        } else {
-            const int p = (c - WF_CHUNKS - WW_DP_CH) * 64 + lane;
-            const int co = p / WW_CD_PC, k = min(p - WW_CD_PC * (p / WW_CD_PC), 2);
-            src = csrc + co * P_WIN + 16 * k;
-        }
-        glds16(src, __builtin_amdgcn_readfirstlane(base + c * 1024));
+    wave &= WW_WAVES - 1;   // (known range: the chunk bound below folds away for i < WW_PPW - 1)
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+    const void* asrc = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
+    const void* dsrc = dpool + (size_t)b * P_SAMPLE + band * 48;
+    const void* csrc = code + (size_t)b * P_SAMPLE + band * 48;
+    uint4 o[WW_TQ];
+#pragma unroll
+    for (int q = 0; q < WW_TQ; ++q) o[q] = tab[(wave * WW_TQ + q) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < WW_PPW; ++i) {
+        const int c = wave + WW_WAVES * i;
+        if (c >= WW_NCH || i < i0 || i >= i1) continue;
+        const uint4 oq = o[i >> 2];
+        const uint32_t off = (i & 3) == 0 ? oq.x : (i & 3) == 1 ? oq.y : (i & 3) == 2 ? oq.z : oq.w;
+        const void* src = c < WF_CHUNKS ? asrc : (c < WF_CHUNKS + WW_DP_CH ? dsrc : csrc);
+        glds16_so(src, off, base + c * 1024);
     }
 }
 
@@ -944,8 +988,9 @@ __device__ __forceinline__ void wino_filter_grad(const float (&du)[16], float (&
 __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
     const float* __restrict__ act, const float* __restrict__ dpool, const uint8_t* __restrict__ code,
     float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(16))) float smem[WW_NBUF * WW_BSTR + 5 * WW_LUTS];
+    __shared__ __attribute__((aligned(16))) float smem[WW_NBUF * WW_BSTR + 5 * WW_LUTS + WW_WAVES * WW_TQ * 64 * 4];
     float* lutz = smem + WW_NBUF * WW_BSTR;  // ZT[c][16], rows WW_LUTS floats apart
+    uint4* dtab = reinterpret_cast<uint4*>(lutz + ((5 * WW_LUTS + 3) & ~3));  // DMA piece offsets
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
@@ -957,7 +1002,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
 #endif
 
     int u = blockIdx.x;
-    if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wu, lane);
+    ww_dma_table(dtab, wu, lane);   // read back only by the same lane: no barrier
+    if (u < nunit) ww_dma_unit(act, dpool, code, u, smem, wu, lane, dtab);
     if (tid < 5 * 16) {
         const int c = tid >> 4, i = (tid >> 2) & 3, j = tid & 3;
         const float ai = (c & 2) ? (i == 0 ? 0.f : (i == 1 ? 1.f : -1.f)) : (i == 3 ? 0.f : 1.f);
@@ -973,7 +1019,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             for (int ij = 0; ij < 16; ++ij) acc[m][n][ij] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dbp[2] = {0.f, 0.f};
     if (WW_NBUF > 2 && u + (int)gridDim.x < nunit)
-        ww_dma_unit(act, dpool, code, u + gridDim.x, smem + WW_BSTR, wu, lane);
+        ww_dma_unit(act, dpool, code, u + gridDim.x, smem + WW_BSTR, wu, lane, dtab);
 
     int buf = 0;
 #pragma unroll 1
@@ -995,7 +1041,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             if (!(SLK_WW_ABL & 128)) lds_barrier();
             if (nu < nunit && !(SLK_WW_ABL & 256) && !WW_SPREAD) {
                 const int nb = buf + WW_NBUF - 1 >= WW_NBUF ? buf - 1 : buf + WW_NBUF - 1;
-                ww_dma_unit(act, dpool, code, nu, smem + nb * WW_BSTR, wu, lane);
+                ww_dma_unit(act, dpool, code, nu, smem + nb * WW_BSTR, wu, lane, dtab);
             }
         }
         const float* img = smem + buf * WW_BSTR;
@@ -1071,7 +1117,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         for (int j = 0; j < 6; ++j) {
             // (SLK_WW_SPREAD) the next unit's staging DMA, two or three pieces per K step
             if (WW_SPREAD && !(SLK_WW_ABL & (16 | 256)) && nu < nunit)
-                ww_dma_unit(act, dpool, code, nu, dma_dst, wu, lane, 2 * j, j == 5 ? 1 << 20 : 2 * j + 2);
+                ww_dma_unit(act, dpool, code, nu, dma_dst, wu, lane, dtab, 2 * j, j == 5 ? 1 << 20 : 2 * j + 2);
             if (j < 5) zload(cd[(j + 1) & 1], E);                                  // under these MFMAs
             if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // likewise
             __builtin_amdgcn_sched_barrier(0);
