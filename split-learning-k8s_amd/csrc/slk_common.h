@@ -110,10 +110,10 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 }
 // Scalar base + per-lane 32-bit byte offset (saddr form): with the lane offsets computed once per
 // launch, a piece costs no VALU address arithmetic at all (sbase is wave-uniform).
-// m0 is declared clobbered instead of saved and restored (two scalar moves per piece fewer).
 __device__ __forceinline__ void glds16_so(const void* sbase, uint32_t voff, uint32_t lds_dst) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                 :: "v"(voff), "s"(sbase), "s"(lds_dst) : "memory", "m0");
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
 }
 __device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_dst) {
     uint32_t keep;
