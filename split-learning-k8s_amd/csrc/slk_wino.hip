@@ -894,11 +894,13 @@ constexpr int WW_SLAB = W2_N + C2;
 #endif
 constexpr int WW_NBUF = SLK_WW_NBUF;
 // SLK_WW_SPREAD = 1 issues the next unit's DMA two or three pieces per K step instead of all at the
-// unit start: no gain (0.4175 vs 0.4153 ms), and neither with 3 buffers (0.4286). The DMA's cost
-// (dropping its issue entirely: 0.414 -> 0.346 ms at an unchanged 2.31 GHz in-kernel clock) is not
-// its latency nor its issue burst.
+// unit start. With the per-piece address code of round 1 it gained nothing (0.4175 vs 0.4153 ms; 3
+// buffers 0.4286) — that code, not the DMA's latency or burst, was the cost (dropping the issue
+// entirely: 0.414 -> 0.346 ms at an unchanged 2.31 GHz in-kernel clock). With the offset table the
+// spread form is the faster one (0.3808 vs 0.3859 ms, same box, profiles/r02_ab_dma_offsets.txt).
+// (3 buffers no longer fit beside the table.)
 #ifndef SLK_WW_SPREAD
-#define SLK_WW_SPREAD 0
+#define SLK_WW_SPREAD 1
 #endif
 constexpr bool WW_SPREAD = SLK_WW_SPREAD;
 // glds16 instructions of wave w per unit (chunks w, w+4, ...): the counted wait leaves the newer
