@@ -132,6 +132,23 @@ int slk_conv2_wgrad_direct(const float* act, const float* dpooled, const uint8_t
                            int B, void* stream);
 int slk_conv2_wgrad_direct_nslab(int B);
 
+/* ---------------------------------------------------------------- conv2 on the f16 MFMA, fp32-grade ("x3")
+ * The same ops as slk_conv2_fwd_pool / _dgrad / _wgrad, computed as direct implicit GEMMs whose f32
+ * operands are split after an exact power-of-two scale into f16 hi + lo, each product formed by three
+ * v_mfma_f32_16x16x32_f16 (hi*hi + hi*lo + lo*hi) into an f32 accumulator: per-product relative error
+ * <= ~7e-7 (csrc/slk_x3.hip). Operand scales: weights per launch (from max|W2|), data per sample from a
+ * caller-supplied per-sample max |.| (slk_row_amax, or a producer that emits it); the arrays must bound
+ * their rows (a too-small bound overflows f16 to inf). Replace the same reference lines as the f32 ops. */
+
+/* amax[r] = max_i |x[r*n + i]| for r < rows (NaNs ignored). */
+int slk_row_amax(const float* x, int rows, int n, float* amax, void* stream);
+/* slk_conv2_fwd_pool on the x3 path; act_amax[B] = per-sample max |act| (model_def.py:25-27). */
+int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* W2, const float* b2, float* pooled,
+                          uint8_t* code, int B, void* stream);
+/* slk_conv2_dgrad on the x3 path; dp_amax[B] = per-sample max |dpooled| (server_part.py:45,51,57). */
+int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                       float* cut_grad, int B, void* stream);
+
 /* ---------------------------------------------------------------- reductions / optimizer */
 
 /* out[i] = (accumulate ? out[i] : 0) + sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed slab order).

@@ -1,0 +1,472 @@
+// slk_x3.hip — conv2 of the reference split CNN (src/model_def.py:18,25-27) as a direct implicit GEMM
+// on the f16 MFMA with fp32-grade operands ("x3"): every f32 operand v is split, after an exact
+// power-of-two scale 2^s, into v*2^s = h + l + r with h = f16(v*2^s), l = f16(v*2^s - h) (both RNE),
+// |r| <= 2^-22 |v*2^s|, and each product is formed as h_a*h_b + h_a*l_b + l_a*h_b by three
+// v_mfma_f32_16x16x32_f16 into one f32 accumulator (dropped: l_a*l_b <= 2^-22 |ab|). Per product that is
+// a relative error of at most ~3 * 2^-22 = 7e-7 — an order of the f32 MFMA's own 2^-24 rounding per
+// accumulation step, and below the error the Winograd F(2x2,3x3) transforms add to the f32 path — at
+// 3 f16 MFMAs (48 cycles) per 16x16x32 block instead of 8 f32 MFMAs (256 cycles).
+//
+// Scales (exact powers of two, so unscaling the f32 accumulator is exact):
+//   - weights: one per launch, from max|W2| (every workgroup reduces W2 itself in its prologue);
+//   - data operands: one per SAMPLE, from a per-sample max |.| array (slk_row_amax, or fused into the
+//     producer), so that the largest element lands in [2^13, 2^14): nothing overflows f16's 65504 and
+//     nothing that matters reaches f16's subnormal range (values 2^-38 below a sample's max lose
+//     relative precision, which is below f32's own resolution of that sum).
+// Routing/pool/ReLU semantics are those of the f32 kernels (torch CPU: first max wins, strict >).
+#include "slk_common.h"
+
+using namespace slk;
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+namespace {
+
+// s such that amax * 2^s < 2^14 (amax in [2^13, 2^14) after scaling); 0 for zero / non-finite amax.
+__device__ __forceinline__ int x3_exp(float amax) {
+    if (!(amax > 0.f) || !__builtin_isfinite(amax)) return 0;
+    int e;
+    (void)frexpf(amax, &e);  // amax = m * 2^e, m in [0.5, 1)
+    return 14 - e;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// 8 scaled f32 values -> 8 f16 hi + 8 f16 lo (v_cvt_pk_f16_f32, RNE).
+__device__ __forceinline__ void x3_split8(const float* v, float sc, f16x8& h, f16x8& l) {
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        const float a = v[k] * sc, b = v[k + 1] * sc;
+        const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+        h[k] = ha;
+        h[k + 1] = hb;
+        l[k] = (_Float16)(a - (float)ha);
+        l[k + 1] = (_Float16)(b - (float)hb);
+    }
+}
+
+__device__ __forceinline__ f32x4 mfma_f16(const f16x8& a, const f16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// acc += (ah + al)(bh + bl) - al*bl
+__device__ __forceinline__ f32x4 mfma_x3(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, f32x4 c) {
+    c = mfma_f16(ah, bh, c);
+    c = mfma_f16(ah, bl, c);
+    return mfma_f16(al, bh, c);
+}
+
+}  // namespace
+
+// ============================================================================ per-row max |x|
+// amax[r] = max_i |x[r*n + i]| (NaNs ignored). The x3 kernels' per-sample operand scales.
+__global__ __launch_bounds__(256) void row_amax_kernel(const float* __restrict__ x, int n, float* __restrict__ amax) {
+    __shared__ float red[4];
+    const float* row = x + (size_t)blockIdx.x * n;
+    float m = 0.f;
+    if ((n & 3) == 0 && ((reinterpret_cast<size_t>(x) & 15) == 0)) {
+        const float4* r4 = reinterpret_cast<const float4*>(row);
+        for (int i = threadIdx.x; i < n / 4; i += 256) {
+            const float4 v = r4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(row[i]));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) amax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// ============================================================================ conv2 forward + pool
+// Unit = (sample, third): output rows 8t..8t+7 (window rows 4t..4t+3), input rows 8t..8t+9 (the
+// unit's 32 channel segments of 260 floats are contiguous runs of act). Staging, two units ahead:
+//   1. LDS-DMA copies the unit's raw f32 rows into a raw buffer [ci][260] (2,080 16-byte pieces, the
+//      per-lane source offsets computed once per launch), issued at the top of unit u for unit u+2;
+//   2. during unit u+1's MFMAs each thread reads its items (pixel, 8-ci chunk) from the raw buffer
+//      (8 conflict-free ds_read_b32), scales, splits and writes them as two f16 planes [pixel][ci]
+//      (64 B per pixel; chunk slot kc ^ (x & 2) makes every ds_read_b128 of the MFMA loop
+//      conflict-free, tools-checked for all 9 taps).
+// One `s_waitcnt vmcnt` (allowing the previous epilogue's 12 stores to stay in flight) + barrier per
+// unit. 8 waves (2 per SIMD): wave = (co half ch, window row wr); its 2 x 9 taps x (h, l) weight
+// fragments (144 VGPRs) stay in registers for the launch. (4 waves holding all 64 co, 288 registers,
+// one per SIMD: 0.375 ms vs 0.262 — hipcc copies the AGPR-resident weights back per MFMA.) A = input (M = 16 pixels = 4 pool windows x
+// 4 positions), B = weights (N = 16 co), K = 32 ci of one tap; the C/D layout puts the 4 positions of
+// one window in one lane's 4 accumulators, so ReLU + 2x2 max-pool + routing code are in-register.
+constexpr int X3F_WAVES = 8;
+constexpr int X3F_THREADS = 64 * X3F_WAVES;
+constexpr int X3F_NT = 2;                        // co tiles per wave
+constexpr int X3F_ROWS = 10;
+constexpr int X3F_PIX = X3F_ROWS * A_HW;          // 260 pixels per unit
+constexpr int X3F_PLANE = X3F_PIX * 64;           // 16,640 B per f16 plane
+constexpr int X3F_BUF = 2 * X3F_PLANE;            // h + l
+constexpr int X3F_RAW = C1 * X3F_PIX * 4;         // 33,280 B raw f32 rows
+constexpr int X3F_PIECES16 = X3F_RAW / 16;        // 2,080 16-byte DMA pieces per unit
+constexpr int X3F_WPIECES = (X3F_PIECES16 / 64 + 1 + X3F_WAVES - 1) / X3F_WAVES;  // DMA wave-instructions per wave
+constexpr int X3F_ITEMS = X3F_PIX * 4;            // (pixel, 8-ci chunk) split items
+constexpr int X3F_IPT = (X3F_ITEMS + X3F_THREADS - 1) / X3F_THREADS;  // 3
+constexpr int X3F_GRID = 256;
+constexpr int X3F_STORES = 6 * X3F_NT;            // epilogue global stores per wave and unit
+static_assert(X3F_RAW % 1024 == 512, "the last DMA wave-instruction is a half piece");
+
+__device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave, int lane, const uint32_t* voff,
+                                              uint32_t raw_lds) {
+    const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+    const char* base = reinterpret_cast<const char*>(act + (size_t)b * A_SAMPLE + t3 * 8 * A_HW);
+#pragma unroll
+    for (int k = 0; k < X3F_WPIECES; ++k) {
+        const int piece = wave + X3F_WAVES * k;
+        if (piece < X3F_PIECES16 / 64) {
+            glds16_so(base, voff[k], raw_lds + piece * 1024);
+        } else if (piece == X3F_PIECES16 / 64 && lane < 32) {
+            glds16_so(base, voff[k], raw_lds + piece * 1024);
+        }
+    }
+}
+
+__global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
+    const float* __restrict__ act, const float* __restrict__ amax, const float* __restrict__ W2,
+    const float* __restrict__ b2, float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3F_BUF + 2 * X3F_RAW];
+    __shared__ float red[X3F_WAVES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ch = wave & 1, wr = wave >> 1;
+    const int n16 = lane & 15, kc = lane >> 4;
+    char* const raw0 = smem + 2 * X3F_BUF;
+
+    const int U = 3 * B;
+    const int G = gridDim.x;
+    int u = blockIdx.x;
+    // DMA source offsets (bytes within a unit): piece g = 64k' + lane -> channel g / 65, 16-B run g % 65
+    uint32_t voff[X3F_WPIECES];
+#pragma unroll
+    for (int k = 0; k < X3F_WPIECES; ++k) {
+        const int g = (wave + X3F_WAVES * k) * 64 + lane;
+        const int c = g / 65, r = g - (g / 65) * 65;
+        voff[k] = (uint32_t)(c * A_PIX * 4 + r * 16);
+    }
+    if (u < U) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
+    if (u + G < U) x3f_issue_raw(act, u + G, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
+
+    // weight scale: max |W2| over the whole tensor
+    float wm = 0.f;
+    for (int e = tid; e < W2_N; e += X3F_THREADS) wm = fmaxf(wm, fabsf(W2[e]));
+    wm = wave_max(wm);
+    if (lane == 0) red[wave] = wm;
+    __syncthreads();
+    wm = red[0];
+#pragma unroll
+    for (int i = 1; i < X3F_WAVES; ++i) wm = fmaxf(wm, red[i]);
+    const int sw = x3_exp(wm);
+    const float wsc = ldexpf(1.f, sw);
+
+    // B fragments: lane (n16, kc) holds W2[co][8kc .. 8kc+7][tap], co = 16nt + n16
+    f16x8 wh[X3F_NT][9], wl[X3F_NT][9];
+    float bias[X3F_NT];
+#pragma unroll
+    for (int nt = 0; nt < X3F_NT; ++nt) {
+        const int co = 32 * ch + 16 * nt + n16;
+        bias[nt] = b2[co];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = W2[(co * C1 + 8 * kc + j) * 9 + tap];
+            x3_split8(v, wsc, wh[nt][tap], wl[nt][tap]);
+        }
+    }
+    // A fragment bases per (mt, kx): M row m = n16 -> window wx = 4mt + (m >> 2), position q = m & 3;
+    // the pixel's chunk slot is kc ^ (x & 2) (x = its column in the unit)
+    int abase[3][3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int q = n16 & 3, wx = 4 * mt + (n16 >> 2);
+            const int x = 2 * wx + (q & 1) + kx;
+            abase[mt][kx] = ((2 * wr + (q >> 1)) * A_HW + x) * 64 + ((kc ^ (x & 2)) * 16);
+        }
+    // split items: (pixel p, chunk c8) -> raw read offset, f16 write offset
+    int rd[X3F_IPT], wo[X3F_IPT];
+#pragma unroll
+    for (int it = 0; it < X3F_IPT; ++it) {
+        const int i = tid + it * X3F_THREADS;
+        const int c8 = i / X3F_PIX, p = i - (i / X3F_PIX) * X3F_PIX;
+        const int x = p % A_HW;
+        rd[it] = (8 * c8 * X3F_PIX + p) * 4;
+        wo[it] = p * 64 + ((c8 ^ (x & 2)) * 16);
+    }
+    auto split_unit = [&](int uu, const char* raw, char* buf) {
+        const float sc = ldexpf(1.f, x3_exp(amax[uu / 3]));
+#pragma unroll
+        for (int it = 0; it < X3F_IPT; ++it) {
+            if (it < X3F_IPT - 1 || tid + it * X3F_THREADS < X3F_ITEMS) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(raw + rd[it] + j * X3F_PIX * 4);
+                f16x8 h, l;
+                x3_split8(v, sc, h, l);
+                *reinterpret_cast<f16x8*>(buf + wo[it]) = h;
+                *reinterpret_cast<f16x8*>(buf + X3F_PLANE + wo[it]) = l;
+            }
+        }
+    };
+
+    // prologue: unit u's raw rows landed -> split into f16 buffer 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (u < U) split_unit(u, raw0, smem);
+    int k = 0;
+#pragma unroll 1
+    for (; u < U; u += G, ++k) {
+        const int cb = k & 1;
+        // unit u+G's raw rows (issued one unit ago) have landed; the previous epilogue's stores may stay
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES) : "memory");
+        __syncthreads();
+        if (u + 2 * G < U) x3f_issue_raw(act, u + 2 * G, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
+        const char* cur = smem + cb * X3F_BUF;
+        f32x4 acc[3][X3F_NT];
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+#pragma unroll
+            for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int ky = tap / 3, kx = tap % 3;
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(cur + abase[mt][kx] + ky * A_HW * 64);
+                const f16x8 al = *reinterpret_cast<const f16x8*>(cur + X3F_PLANE + abase[mt][kx] + ky * A_HW * 64);
+#pragma unroll
+                for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = mfma_x3(ah, al, wh[nt][tap], wl[nt][tap], acc[mt][nt]);
+            }
+            if (mt == 0 && u + G < U) split_unit(u + G, raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+        }
+        // epilogue: unscale (exact), bias, ReLU, 2x2 max-pool, routing code
+        const int b = u / 3, t3 = u - (u / 3) * 3;
+        const float us = ldexpf(1.f, -(x3_exp(amax[b]) + sw));
+        const int wy = 4 * t3 + wr;
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+            const int wx = 4 * mt + kc;
+#pragma unroll
+            for (int nt = 0; nt < X3F_NT; ++nt) {
+                const int co = 32 * ch + 16 * nt + n16;
+                float m = -__builtin_inff();
+                int idx = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float v = acc[mt][nt][q] * us + bias[nt];
+                    v = v > 0.f ? v : 0.f;
+                    if (v > m) { m = v; idx = q; }
+                }
+                const size_t o = (size_t)b * P_SAMPLE + co * P_WIN + wy * P_HW + wx;
+                pooled[o] = m;
+                code[o] = (uint8_t)(m > 0.f ? idx : CODE_NONE);
+            }
+        }
+    }
+}
+
+// ============================================================================ conv2 dgrad (cut gradient)
+// g[ci][y][x] = sum_{co,ky,kx} W2[co][ci][ky][kx] * dY[co][y-ky][x-kx], dY = the max-pool/ReLU routing of
+// dpooled by `code` (src/server_part.py:51 through model_def.py:25-27). GEMM per sample: M = output
+// pixels (676 -> 43 tiles of 16 consecutive linear pixels p = 26y + x, so a lane's 4 accumulators are 4
+// consecutive pixels = one float4 store), N = 32 ci, K = 64 co x 9 taps (K-step = 32 co of one tap).
+// The routed dY of a unit (sample, co half) is expanded into ONE LDS image with row stride 26 and two
+// zero rows above and below: dY(Y, X) at pixel (Y + 2) * 26 + X, columns 24-25 zero — the 24-wide dY in
+// the 26-wide grid carries exactly the 2-column halo a 3x3 tap needs, so tap (ky, kx) of output pixel
+// p reads image pixel p + 52 - 26 ky - kx: every A fragment address is a per-tile base + an immediate.
+// Pixel records are [8 h chunks... 4 h chunks | 4 l chunks | 32 B pad] = 160 B: conflict-free
+// ds_read_b128 for every tap (tools-checked; 64-B records are 2-way). The image (116 KB) is not
+// double-buffered: the expansion (from pooled values + codes that LDS-DMA staged one unit ahead) sits
+// between two barriers. 8 waves: wave = (ci tile nt, M group g: tiles g, g+4, ...); its weight fragments
+// for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its 11 accumulators live across the
+// sample's two units.
+constexpr int X3D_THREADS = 512;
+constexpr int X3D_REC = 160;                       // bytes per image pixel: h 64 | l 64 | pad 32
+constexpr int X3D_PIX = 28 * A_HW;                 // 728 image pixels (rows -2 .. 25 of dY)
+constexpr int X3D_DY = X3D_PIX * X3D_REC;          // 116,480 B
+constexpr int X3D_RAWDP = 32 * P_WIN * 4;          // 18,432 B pooled gradient of a co half
+constexpr int X3D_RAWC = 32 * P_WIN;               // 4,608 B its codes
+constexpr int X3D_RAW = X3D_RAWDP + X3D_RAWC;      // 23,040 B
+constexpr int X3D_WI = X3D_RAWDP / 1024 + (X3D_RAWC + 1023) / 1024;  // 18 + 5 DMA wave-instructions
+constexpr int X3D_MT = 43;                         // M tiles per sample
+constexpr int X3D_MPW = 11;                        // M tiles per wave (max)
+constexpr int X3D_ITEMS = P_WIN * 4;               // (window, 8-co chunk) expansion items
+constexpr int X3D_GRID = 256;
+static_assert(X3D_DY + 2 * X3D_RAW <= 163840, "LDS");
+
+__device__ __forceinline__ void x3d_issue_raw(const float* dpooled, const uint8_t* code, int b, int h, int wave,
+                                              int lane, uint32_t raw_lds) {
+    const char* dps = reinterpret_cast<const char*>(dpooled + (size_t)b * P_SAMPLE + h * 32 * P_WIN);
+    const char* cds = reinterpret_cast<const char*>(code + (size_t)b * P_SAMPLE + h * 32 * P_WIN);
+#pragma unroll
+    for (int r = 0; r < (X3D_WI + 7) / 8; ++r) {
+        const int k = wave + 8 * r;
+        if (k < X3D_RAWDP / 1024) {
+            glds16_so(dps, (uint32_t)(k * 1024 + lane * 16), raw_lds + k * 1024);
+        } else if (k < X3D_WI) {
+            const int kk = k - X3D_RAWDP / 1024;
+            if (kk * 1024 + lane * 16 < X3D_RAWC)
+                glds16_so(cds, (uint32_t)(kk * 1024 + lane * 16), raw_lds + X3D_RAWDP + kk * 1024);
+        }
+    }
+}
+
+__global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
+    const float* __restrict__ dpooled, const float* __restrict__ amax, const uint8_t* __restrict__ code,
+    const float* __restrict__ W2, float* __restrict__ cut_grad, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[X3D_DY + 2 * X3D_RAW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nt = wave & 1, g = wave >> 1;
+    const int n16 = lane & 15, kc = lane >> 4;
+    char* const dy = smem;
+    char* const raw0 = smem + X3D_DY;
+    const int G = gridDim.x;
+    int b = blockIdx.x;
+    if (b < B) x3d_issue_raw(dpooled, code, b, 0, wave, lane, lds_u32(raw0));
+
+    // zero the dY image once: its halo rows / columns are never written again
+    for (int o = tid * 16; o < X3D_DY; o += X3D_THREADS * 16) *reinterpret_cast<uint4*>(dy + o) = make_uint4(0, 0, 0, 0);
+
+    // weight scale (max |W2|), reduced through the second raw buffer (not in use yet)
+    float* red = reinterpret_cast<float*>(raw0 + X3D_RAW);
+    float wm = 0.f;
+    for (int e = tid; e < W2_N; e += X3D_THREADS) wm = fmaxf(wm, fabsf(W2[e]));
+    wm = wave_max(wm);
+    if (lane == 0) red[wave] = wm;
+    __syncthreads();
+    wm = red[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) wm = fmaxf(wm, red[i]);
+    const int sw = x3_exp(wm);
+    const float wsc = ldexpf(1.f, sw);
+    // B fragments: lane (n16, kc) holds W2[32h + 8kc + j][ci][tap], ci = 16nt + n16
+    f16x8 wh[2][9], wl[2][9];
+    {
+        const int ci = 16 * nt + n16;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = W2[((32 * h + 8 * kc + j) * C1 + ci) * 9 + tap];
+                x3_split8(v, wsc, wh[h][tap], wl[h][tap]);
+            }
+    }
+    // A fragment bases: tile g + 4i, row n16 -> image pixel 16(g + 4i) + n16 + 52 (tap (2, 2)); two
+    // bases so every (i, tap) offset is a 16-bit immediate
+    const int a0 = (16 * g + n16) * X3D_REC + kc * 16;
+    const int a1 = a0 + 6 * 64 * X3D_REC;
+
+    auto expand = [&](const char* raw, float sc) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = tid + r * X3D_THREADS;
+            if (r == 0 || i < X3D_ITEMS) {
+                const int c8 = i / P_WIN, w = i - (i / P_WIN) * P_WIN;
+                float v[8];
+                uint32_t cw0 = 0, cw1 = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    v[j] = *reinterpret_cast<const float*>(raw + ((8 * c8 + j) * P_WIN + w) * 4);
+                    const uint32_t c = *reinterpret_cast<const uint8_t*>(raw + X3D_RAWDP + (8 * c8 + j) * P_WIN + w);
+                    if (j < 4) cw0 |= c << (8 * j);
+                    else cw1 |= c << (8 * (j - 4));
+                }
+                f16x8 hh, ll;
+                x3_split8(v, sc, hh, ll);
+                const uint4 hv = __builtin_bit_cast(uint4, hh), lv = __builtin_bit_cast(uint4, ll);
+                const uint32_t cA = __builtin_amdgcn_perm(0u, cw0, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw0, 0x03030202u);
+                const uint32_t cC = __builtin_amdgcn_perm(0u, cw1, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw1, 0x03030202u);
+                const int wy = w / P_HW, wx = w - (w / P_HW) * P_HW;
+                char* rec = dy + ((2 * wy + 2) * A_HW + 2 * wx) * X3D_REC + c8 * 16;
+#pragma unroll
+                for (int pos = 0; pos < 4; ++pos) {
+                    const uint32_t T = 0xFFu << (8 * pos);
+                    const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
+                    const uint32_t mC = __builtin_amdgcn_perm(0u, T, cC), mD = __builtin_amdgcn_perm(0u, T, cD);
+                    char* o = rec + ((pos >> 1) * A_HW + (pos & 1)) * X3D_REC;
+                    *reinterpret_cast<uint4*>(o) = make_uint4(hv.x & mA, hv.y & mB, hv.z & mC, hv.w & mD);
+                    *reinterpret_cast<uint4*>(o + 64) = make_uint4(lv.x & mA, lv.y & mB, lv.z & mC, lv.w & mD);
+                }
+            }
+        }
+    };
+
+    int rb = 0;  // raw buffer of the current unit
+#pragma unroll 1
+    for (; b < B; b += G) {
+        const float sc = ldexpf(1.f, x3_exp(amax[b]));
+        f32x4 acc[X3D_MPW];
+#pragma unroll
+        for (int i = 0; i < X3D_MPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // raw(b, h) landed everywhere; every wave is done with the dY image
+            const int nb = h ? b + G : b, nh = h ^ 1;
+            if (nb < B) x3d_issue_raw(dpooled, code, nb, nh, wave, lane, lds_u32(raw0 + (rb ^ 1) * X3D_RAW));
+            expand(raw0 + rb * X3D_RAW, sc);
+            __syncthreads();
+            rb ^= 1;
+#pragma unroll
+            for (int i = 0; i < X3D_MPW; ++i) {
+                if (g + 4 * i < X3D_MT) {
+                    const char* ab = dy + (i < 6 ? a0 + i * 64 * X3D_REC : a1 + (i - 6) * 64 * X3D_REC);
+#pragma unroll
+                    for (int tap = 0; tap < 9; ++tap) {
+                        const int o = (52 - 26 * (tap / 3) - tap % 3) * X3D_REC;
+                        const f16x8 ah = *reinterpret_cast<const f16x8*>(ab + o);
+                        const f16x8 al = *reinterpret_cast<const f16x8*>(ab + o + 64);
+                        acc[i] = mfma_x3(ah, al, wh[h][tap], wl[h][tap], acc[i]);
+                    }
+                }
+            }
+        }
+        // epilogue: unscale (exact) and store 4 consecutive pixels per lane
+        const float us = ldexpf(1.f, -(x3_exp(amax[b]) + sw));
+        float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
+#pragma unroll
+        for (int i = 0; i < X3D_MPW; ++i) {
+            const int p = 16 * (g + 4 * i) + 4 * kc;
+            if (g + 4 * i < X3D_MT && p < A_PIX)
+                *reinterpret_cast<float4*>(gb + p) = make_float4(acc[i][0] * us, acc[i][1] * us, acc[i][2] * us, acc[i][3] * us);
+        }
+    }
+}
+
+// ============================================================================ C-ABI
+extern "C" int slk_row_amax(const float* x, int rows, int n, float* amax, void* stream) {
+    SLK_CHECK_ARG(rows >= 0 && n > 0 && (rows == 0 || (x && amax)));
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(row_amax_kernel, dim3(rows), dim3(256), 0, slk_stream(stream), x, n, amax);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* W2, const float* b2,
+                                     float* pooled, uint8_t* code, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code);
+    if (B == 0) return 0;
+    const int U = 3 * B;
+    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
+                       slk_stream(stream), act, act_amax, W2, b2, pooled, code, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                                  float* cut_grad, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && dpooled && dp_amax && code && W2 && cut_grad);
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel, dim3(B < X3D_GRID ? B : X3D_GRID), dim3(X3D_THREADS), 0,
+                       slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B);
+    return slk_launch_status();
+}

@@ -49,6 +49,9 @@ _SIGS = {
     "slk_conv2_wgrad_nslab": [_I],
     "slk_conv2_wgrad_direct": [_P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad_direct_nslab": [_I],
+    "slk_row_amax": [_P, _I, _I, _P, _P],
+    "slk_conv2_fwd_pool_x3": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_dgrad_x3": [_P, _P, _P, _P, _P, _I, _P],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
     "slk_sgd": [_P, _P, _I, _F, _P],

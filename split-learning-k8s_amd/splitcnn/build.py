@@ -19,7 +19,7 @@ CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include")
 LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
 SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip", "slk_wide.hip",
-           "slk_wide_head.hip", "slk_wino.hip", "slk_codec.hip"]
+           "slk_wide_head.hip", "slk_wino.hip", "slk_codec.hip", "slk_x3.hip"]
 ARCH = "gfx950"
 # Per-source extra hipcc flags (none needed at present; profiling variants pass -D defines).
 EXTRA_FLAGS: dict = {}

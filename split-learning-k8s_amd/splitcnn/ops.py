@@ -90,12 +90,39 @@ def conv1_wgrad_remask_slabs(x, W1, b1, cut_grad, slabs=None):
 
 
 # ------------------------------------------------------------------------------------ server stage
-def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False):
-    """Winograd F(2x2,3x3) kernel; direct=True runs the direct implicit-GEMM kernel (cross-check)."""
+def row_amax(x, out=None):
+    """out[r] = max |x[r]| over each row of a [rows, ...] tensor (the x3 kernels' per-sample scales)."""
+    rows = int(x.shape[0])
+    n = x.numel() // max(rows, 1)
+    out = _out(out, (rows,), x, name="amax")
+    _lib.call("slk_row_amax", _dev(x, "x"), rows, n, _dev(out, "amax"), _stream(x))
+    return out
+
+
+def _impl(direct, impl):
+    if impl is None:
+        return "direct" if direct else "wino"
+    if impl not in ("wino", "direct", "x3"):
+        raise ValueError(f"conv2 impl must be 'wino', 'direct' or 'x3', got {impl!r}")
+    return impl
+
+
+def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None):
+    """impl: 'wino' (Winograd F(2x2,3x3) on the f32 MFMA, default), 'direct' (direct f32 MFMA kernel,
+    cross-check; also direct=True) or 'x3' (direct on the f16 MFMA with split operands; act_amax =
+    per-sample max |act|, computed here when not given)."""
+    impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
     pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
     code = _out(code, (B, 64, 12, 12), act, torch.uint8, "code")
-    _lib.call("slk_conv2_fwd_pool_direct" if direct else "slk_conv2_fwd_pool", _dev(act, "act"),
+    if impl == "x3":
+        if act_amax is None:
+            act_amax = row_amax(act)
+        _lib.call("slk_conv2_fwd_pool_x3", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)),
+                  _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
+                  _dev(code, "code", dtype=torch.uint8), B, _stream(act))
+        return pooled, code
+    _lib.call("slk_conv2_fwd_pool_direct" if impl == "direct" else "slk_conv2_fwd_pool", _dev(act, "act"),
               _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
               _dev(code, "code", dtype=torch.uint8), B, _stream(act))
     return pooled, code
@@ -171,9 +198,18 @@ def _dpooled_batch(dpooled):
     return _pooled_batch(dpooled)
 
 
-def conv2_dgrad(dpooled, code, W2, out=None, direct=False):
+def conv2_dgrad(dpooled, code, W2, out=None, direct=False, impl=None, dp_amax=None):
+    impl = _impl(direct, impl)
     B = _dpooled_batch(dpooled)
     cut_grad = _out(out, (B, 32, 26, 26), dpooled, name="cut_grad")
+    if impl == "x3":
+        if dp_amax is None:
+            dp_amax = row_amax(dpooled)
+        _lib.call("slk_conv2_dgrad_x3", _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
+                  _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+                  _dev(cut_grad, "cut_grad"), B, _stream(dpooled))
+        return cut_grad
+    direct = impl == "direct"
     _lib.call("slk_conv2_dgrad_direct" if direct else "slk_conv2_dgrad", _dev(dpooled, "dpooled"),
               _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
               _dev(cut_grad, "cut_grad"), B, _stream(dpooled))

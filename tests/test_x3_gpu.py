@@ -1,0 +1,122 @@
+"""GPU: the "x3" conv2 kernels (direct implicit GEMM on the f16 MFMA with hi/lo-split operands,
+csrc/slk_x3.hip) against the fp64 oracle and against the f32-MFMA kernels on identical inputs.
+
+Tolerances: the same bars as the Winograd path (tests/test_wino_gpu.py): 1e-5 of max |ref|, routing
+differences only at numerical ties of the fp64 conv output. The x3 error is also compared with the
+f32 Winograd path's own error against fp64 (it must not be worse by more than 2x: an fp32-grade path,
+not a reduced-precision one)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(gpu, B, seed):
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage
+    a, b = init_models(seed=seed)
+    x, y = SyntheticMNIST(seed + 1).batch(B)
+    act = ClientStage(a, device=gpu).forward(x.to(gpu)).clone()
+    p = {k: v.detach().to(gpu).contiguous() for k, v in
+         {"W2": b.conv2.weight, "b2": b.conv2.bias, "W3": b.fc1.weight, "b3": b.fc1.bias}.items()}
+    return act, p, y.to(gpu)
+
+
+def test_row_amax(gpu):
+    from splitcnn import ops
+    x = torch.randn(37, 21632, device=gpu) * torch.logspace(-8, 8, 37, device=gpu)[:, None]
+    x[3] = 0
+    x[5, 7] = float("nan")
+    got = ops.row_amax(x).cpu()
+    want = torch.nan_to_num(x.cpu(), nan=0.0).abs().amax(dim=1)
+    assert torch.equal(got, want)
+    odd = torch.randn(5, 33, device=gpu)
+    assert torch.equal(ops.row_amax(odd).cpu(), odd.cpu().abs().amax(dim=1))
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 130, 777])
+def test_x3_fwd_matches_oracle(gpu, B):
+    from oracle.split_step import conv3x3, relu, tie_discrepancies
+    from splitcnn import ops
+    act, p, _ = _inputs(gpu, B, seed=B)
+    px, cx = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3")
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    a64 = act.double().cpu().numpy()
+    r = relu(conv3x3(a64, p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
+    pr = r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))
+    n, ok = tie_discrepancies(r, cw.cpu().numpy().astype(np.int64), cx.cpu().numpy().astype(np.int64))
+    assert ok, f"{n} routing differences that are not ties"
+    ex = rel_err(px.cpu().numpy(), pr)
+    ew = rel_err(pw.cpu().numpy(), pr)
+    assert ex <= 1e-5
+    assert ex <= max(2 * ew, 1e-6), (ex, ew)
+
+
+def test_x3_fwd_scale_invariance(gpu):
+    """Per-sample power-of-two scales: scaling one sample's act by 2^k (exact) scales its pooled output
+    by 2^k bit for bit (bias 0), whatever the other samples hold — incl. magnitudes far outside f16."""
+    from splitcnn import ops
+    B = 6
+    act, p, _ = _inputs(gpu, B, seed=9)
+    b0 = torch.zeros_like(p["b2"])
+    base, cb = ops.conv2_fwd_pool(act, p["W2"], b0, impl="x3")
+    k = torch.tensor([0, -40, 30, 0, 60, -100], device=gpu, dtype=torch.float32)
+    sc = torch.pow(2.0, k)
+    out, co = ops.conv2_fwd_pool(act * sc[:, None, None, None], p["W2"], b0, impl="x3")
+    assert torch.equal(co, cb)
+    assert torch.equal(out, base * sc[:, None, None, None])
+    # weights scaled by 2^k: the launch scale absorbs it
+    out2, _ = ops.conv2_fwd_pool(act, p["W2"] * 2.0 ** -30, b0, impl="x3")
+    assert torch.equal(out2, base * 2.0 ** -30)
+
+
+def test_x3_fwd_deterministic_and_full_size(gpu):
+    from splitcnn import ops
+    B = 4096
+    act, p, _ = _inputs(gpu, B, seed=21)
+    r1 = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3")
+    r2 = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3")
+    assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
+    pd, cd = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="direct")
+    same = r1[1] == cd
+    assert same.float().mean().item() > 0.9999
+    assert rel_err(r1[0][same].cpu().numpy(), pd[same].cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 130, 777])
+def test_x3_dgrad_matches_oracle(gpu, B):
+    from oracle.split_step import conv3x3_dgrad, maxpool2_bwd
+    from splitcnn import ops
+    act, p, y = _inputs(gpu, B, seed=B + 100)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    gx = ops.conv2_dgrad(dp, cw, p["W2"], impl="x3")
+    gw = ops.conv2_dgrad(dp, cw, p["W2"])
+    codes = cw.cpu().numpy().astype(np.int64)
+    dp64 = dp.double().cpu().numpy().reshape(B, 64, 12, 12)
+    dc = maxpool2_bwd(np.where(codes < 4, dp64, 0.0), np.minimum(codes, 3), (B, 64, 24, 24))
+    ref = conv3x3_dgrad(dc, p["W2"].double().cpu().numpy())
+    ex = rel_err(gx.cpu().numpy(), ref)
+    ew = rel_err(gw.cpu().numpy(), ref)
+    assert ex <= 1e-5
+    assert ex <= max(2 * ew, 1e-6), (ex, ew)
+    # every sample on its own (a misrouted unit would hit one sample)
+    g64 = torch.from_numpy(ref)
+    num = (gx.cpu().double() - g64).abs().flatten(1).max(dim=1).values
+    den = g64.abs().flatten(1).max(dim=1).values.clamp_min(1e-30)
+    assert (num / den).max().item() <= 1e-5
+
+
+def test_x3_dgrad_scale_invariance(gpu):
+    from splitcnn import ops
+    B = 6
+    act, p, y = _inputs(gpu, B, seed=19)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    base = ops.conv2_dgrad(dp, cw, p["W2"], impl="x3")
+    sc = torch.pow(2.0, torch.tensor([0, -40, 30, 0, 60, -90], device=gpu, dtype=torch.float32))
+    out = ops.conv2_dgrad((dp.reshape(B, -1) * sc[:, None]).reshape(dp.shape).contiguous(), cw, p["W2"], impl="x3")
+    assert torch.equal(out, base * sc[:, None, None, None])
