@@ -71,6 +71,12 @@ def parse():
                     help="k2 = reference split CNN fp32 (headline); k5 = widened bf16 split CNN")
     ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
     ap.add_argument("--k5-batch", type=int, default=4096)
+    ap.add_argument("--conv", default=None, choices=["x3", "f32"],
+                    help="K2 conv2 kernels: x3 = f16 MFMA with hi/lo-split fp32 operands (fwd, dgrad) + "
+                         "Winograd wgrad; f32 = Winograd F(2x2,3x3) on the f32 MFMA throughout "
+                         "(default: splitcnn.engine.CONV_DEFAULT)")
+    ap.add_argument("--no-conv-compare", action="store_true",
+                    help="skip the short run of the other conv preset reported beside the headline")
     return ap.parse_args()
 
 
@@ -156,20 +162,35 @@ def pmc_traffic(name, B):
         return None
 
 
-def roofline_from(kern, B):
+def conv_roofline(name, avg_ms, B, impl):
+    """Roofline of one conv2 launch. wino: its transform-domain GEMM FLOPs on the f32 MFMA peak; x3: the
+    f16 MFMA FLOPs it executes (3 products per direct-conv multiply-add) on the dense f16 peak."""
+    direct_eq = CONV2_FLOP_PER_SAMPLE * B / (avg_ms * 1e-3) / 1e12
+    if impl == "x3":
+        flops, peak = 3 * CONV2_FLOP_PER_SAMPLE * B, BF16_PEAK_TFLOPS
+        algo = ("direct implicit GEMM on v_mfma_f32_16x16x32_f16, f32 operands split hi/lo (3 MFMAs per "
+                "product, f32 accumulate; flop_per_launch = the f16 MFMA FLOPs executed)")
+    else:
+        flops, peak = WINO_FLOP_PER_SAMPLE[name] * B, FP32_PEAK_TFLOPS
+        algo = "Winograd F(2x2,3x3), f32 MFMA (flop_per_launch = its transform-domain GEMMs)"
+    ach = flops / (avg_ms * 1e-3) / 1e12
+    return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": pmc_traffic(name + ("_x3" if impl == "x3" else ""), B),
+            "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "algorithm": algo,
+            "direct_conv_equivalent_tflops": round(direct_eq, 2)}
+
+
+def roofline_from(kern, B, impls=None):
     conv = {k: v for k, v in kern.items() if k.startswith("conv2_")}
     if not conv:
         return None
+    impls = impls or {}
     name = max(conv, key=lambda k: conv[k]["avg_ms"])
-    flops = WINO_FLOP_PER_SAMPLE[name] * B
-    ach = flops / (conv[name]["avg_ms"] * 1e-3) / 1e12
-    direct_eq = CONV2_FLOP_PER_SAMPLE * B / (conv[name]["avg_ms"] * 1e-3) / 1e12
-    traffic = pmc_traffic(name, B)
-    return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-            "flop_per_launch": flops, "avg_ms": round(conv[name]["avg_ms"], 4),
-            "algorithm": "Winograd F(2x2,3x3), f32 MFMA (flop_per_launch = its transform-domain GEMMs)",
-            "direct_conv_equivalent_tflops": round(direct_eq, 2)}
+    r = conv_roofline(name, conv[name]["avg_ms"], B, impls.get(name, "wino"))
+    r["per_kernel"] = {k: {kk: conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino"))[kk]
+                           for kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops")}
+                       for k, v in conv.items()}
+    return r
 
 
 def run_single(args, out):
@@ -180,23 +201,37 @@ def run_single(args, out):
     dev = torch.device("cuda:0")
     B = args.batch
     X, Y = make_pool(B, 4, dev)
+    from splitcnn.engine import CONV_DEFAULT, CONV_PRESETS
+    conv = args.conv or CONV_DEFAULT
     a, b = init_models(seed=0)
-    tr = SplitTrainer(a, b, device=dev, graph=not args.no_graph)
+    tr = SplitTrainer(a, b, device=dev, graph=not args.no_graph, conv=conv)
     step = lambda i: tr.step(X[i % 4], Y[i % 4])  # noqa: E731
     dt = timed(step, args.steps, args.warmup, dev)
     losses = tr.loss_log.flush()
     out.update(value=args.steps * B / dt, ms_per_step=dt / args.steps * 1e3)
+    fi, di, wi = CONV_PRESETS[conv]
     out["config"] = {"workload": "K2: split CNN (model_def.py ModelPartA+ModelPartB) both stages fused on "
                                  "1xMI355X, synthetic 1x28x28 MNIST-shape batches, fp32, HIP-graph step",
                      "global_batch": B, "per_gpu_batch": B, "topology": "fused-1gpu",
-                     "graph": not args.no_graph}
+                     "graph": not args.no_graph, "conv": conv,
+                     "conv2_kernels": {"fwd_pool": fi, "dgrad": di, "wgrad": wi},
+                     "arithmetic": "fp32 tensors, f32 accumulation; conv2 'x3' kernels multiply f32 operands split "
+                                   "into f16 hi + lo (3 MFMA products, per-product error <= ~7e-7 relative, "
+                                   "checked vs fp64 at the f32 path's bars), 'wino' = Winograd on the f32 MFMA"}
     out["loss_first_last"] = [round(losses[0][1], 5), round(losses[-1][1], 5)] if losses else None
+    if not args.no_conv_compare:
+        other = "f32" if conv == "x3" else "x3"
+        tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
+        dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
+        out["conv_presets"] = {conv: round(out["value"], 1), other: round(args.steps * B / dto, 1)}
+        del tro
     if not args.no_kernel_pass:
-        tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False)
+        tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False, conv=conv)
         kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)
         out["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
-        out["roofline"] = roofline_from(kern, B)
-    out["step_roofline_frac"] = round(out["value"] * STEP_FLOP_EXECUTED / (FP32_PEAK_TFLOPS * 1e12), 4)
+        out["roofline"] = roofline_from(kern, B, {"conv2_fwd_pool": fi, "conv2_dgrad": di, "conv2_wgrad": wi})
+    if conv == "f32":  # every conv2 FLOP on the f32 MFMA: one peak prices the whole step
+        out["step_roofline_frac"] = round(out["value"] * STEP_FLOP_EXECUTED / (FP32_PEAK_TFLOPS * 1e12), 4)
     out["step_direct_equivalent_tflops"] = round(out["value"] * FLOP_PER_SAMPLE / 1e12, 2)
 
 

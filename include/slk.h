@@ -58,6 +58,11 @@ const char* slk_build_id(void);
  * Replaces ModelPartA.forward (src/model_def.py:11-12) as called at src/client_part.py:114. */
 int slk_conv1_fwd(const float* x, const float* W1, const float* b1, float* act, int B, void* stream);
 
+/* slk_conv1_fwd that also writes act_amax[b] = max(act[b]) (>= 0): the per-sample scale of the x3 conv2
+ * kernels, fused so the 354 MB cut is not re-read at B = 4096. */
+int slk_conv1_fwd_amax(const float* x, const float* W1, const float* b1, float* act, float* act_amax, int B,
+                       void* stream);
+
 /* Client backward: relu-bwd mask (act > 0) applied to the cut gradient, then conv1 weight/bias
  * gradient. No input gradient (the data needs none). Writes per-group partial slabs
  * [slk_conv1_wgrad_nslab(B)][320] into `slabs`; reduce them with slk_sgd_from_slabs or
@@ -106,6 +111,11 @@ int slk_fc_xent(const float* pooled, const float* W3, const float* b3, const int
                 float* logits, float* loss_i, float* dlogits, float* dpooled, float grad_scale,
                 int* err_flag, int B, void* stream);
 
+/* slk_fc_xent that also writes dp_amax[b] = max |dpooled[b]| (the x3 conv2 backward kernels' scales). */
+int slk_fc_xent_amax(const float* pooled, const float* W3, const float* b3, const int64_t* labels, float* logits,
+                     float* loss_i, float* dlogits, float* dpooled, float* dp_amax, float grad_scale, int* err_flag,
+                     int B, void* stream);
+
 /* fc1 weight/bias gradient partials: slabs [slk_fc_wgrad_nslab(B)][92170] laid out as
  * [dW3 (10*9216) | db3 (10)], i.e. the tail of the server flat block. */
 int slk_fc_wgrad(const float* dlogits, const float* pooled, float* slabs, int B, void* stream);
@@ -148,6 +158,12 @@ int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* 
 /* slk_conv2_dgrad on the x3 path; dp_amax[B] = per-sample max |dpooled| (server_part.py:45,51,57). */
 int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
                        float* cut_grad, int B, void* stream);
+/* slk_conv2_wgrad on the x3 path: slabs [slk_conv2_wgrad_x3_nslab(B)][18496] = [dW2 | db2] partials
+ * (fixed-order sum = the gradient). The operand scales are per launch (max over the batch of act_amax /
+ * dp_amax): the reduction spans samples (server_part.py:51). */
+int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
+                       const uint8_t* code, float* slabs, int B, void* stream);
+int slk_conv2_wgrad_x3_nslab(int B);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 

@@ -22,8 +22,10 @@ constexpr int C1F4_G = A_PIX / 4;  // 169
 __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ W1,
                                                              const float* __restrict__ b1,
-                                                             float* __restrict__ act) {
+                                                             float* __restrict__ act,
+                                                             float* __restrict__ act_amax) {
     __shared__ float xs[IN_HW * IN_HW];
+    __shared__ float amx[C1F4_T / 64];
     __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -33,33 +35,47 @@ __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restri
     for (int i = tid; i < C1 * 9; i += C1F4_T) ws[(i / 9) * 10 + i % 9] = W1[i];
     if (tid < C1) ws[tid * 10 + 9] = b1[tid];
     __syncthreads();
-    if (tid >= C1F4_G) return;
-    float xv[4][9];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int p = 4 * tid + u;
-        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
-    }
-    float4* out = reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid;
-#pragma unroll 4
-    for (int c = 0; c < C1; ++c) {
-        const float* w = ws + c * 10;
-        float wk[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) wk[k] = w[k];
-        float o[4];
+    // act_amax (optional): the sample's max act, for the x3 conv2 kernels' per-sample scales; without
+    // it the idle threads leave here
+    const bool active = tid < C1F4_G;
+    if (!active && !act_amax) return;
+    float am = 0.f;
+    if (active) {
+        float xv[4][9];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            // tap order (ky, kx) row-major, bias added last — as conv1_fwd_kernel
-            float s = 0.f;
+            const int p = 4 * tid + u;
+            const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) s = fmaf(xv[u][k], wk[k], s);
-            s += wk[9];
-            o[u] = s > 0.f ? s : 0.f;
+            for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
         }
-        out[c * C1F4_G] = make_float4(o[0], o[1], o[2], o[3]);
+        float4* out = reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid;
+#pragma unroll 4
+        for (int c = 0; c < C1; ++c) {
+            const float* w = ws + c * 10;
+            float wk[10];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) wk[k] = w[k];
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                // tap order (ky, kx) row-major, bias added last — as conv1_fwd_kernel
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) s = fmaf(xv[u][k], wk[k], s);
+                s += wk[9];
+                o[u] = s > 0.f ? s : 0.f;
+            }
+            out[c * C1F4_G] = make_float4(o[0], o[1], o[2], o[3]);
+            am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+        }
+    }
+    if (act_amax) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) am = fmaxf(am, __shfl_xor(am, off, 64));
+        if ((tid & 63) == 0) amx[tid >> 6] = am;
+        __syncthreads();
+        if (tid == 0) act_amax[b] = fmaxf(fmaxf(amx[0], amx[1]), amx[2]);
     }
 }
 
@@ -201,7 +217,16 @@ extern "C" int slk_conv1_fwd(const float* x, const float* W1, const float* b1, f
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(x && W1 && b1 && act);
-    conv1_fwd_kernel<<<B, C1F4_T, 0, slk_stream(stream)>>>(x, W1, b1, act);
+    conv1_fwd_kernel<<<B, C1F4_T, 0, slk_stream(stream)>>>(x, W1, b1, act, nullptr);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv1_fwd_amax(const float* x, const float* W1, const float* b1, float* act, float* act_amax,
+                                  int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(x && W1 && b1 && act && act_amax);
+    conv1_fwd_kernel<<<B, C1F4_T, 0, slk_stream(stream)>>>(x, W1, b1, act, act_amax);
     return slk_launch_status();
 }
 

@@ -541,7 +541,8 @@ template <int MODE>
 __global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
     const float* __restrict__ pooled, const float* __restrict__ W3, const float* __restrict__ b3,
     const int64_t* __restrict__ labels, float* __restrict__ logits, float* __restrict__ loss_i,
-    float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B) {
+    float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B,
+    float* __restrict__ dp_amax = nullptr) {
     __shared__ float red[FC_T / 64][FC_S * NCLS];
     __shared__ float zl[FC_S][NCLS];
     __shared__ float dl[FC_S][NCLS];
@@ -636,6 +637,9 @@ __global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
 
     if (MODE & 4) {
         float4* D4 = reinterpret_cast<float4*>(dpooled + (size_t)b0 * P_SAMPLE);
+        float dmx[FC_S];  // per-sample max |dpooled| (dp_amax, the x3 kernels' scales)
+#pragma unroll
+        for (int s = 0; s < FC_S; ++s) dmx[s] = 0.f;
         for (int k4 = tid; k4 < FC_K4; k4 += FC_T) {
             float4 w[NCLS];
 #pragma unroll
@@ -650,6 +654,28 @@ __global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
                     o.z = fmaf(d, w[jj].z, o.z); o.w = fmaf(d, w[jj].w, o.w);
                 }
                 D4[s * FC_K4 + k4] = o;
+                if (dp_amax) {
+                    const float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+#pragma unroll
+                    for (int t = 0; t < FC_S; ++t) dmx[t] = (t == s) ? fmaxf(dmx[t], mo) : dmx[t];
+                }
+            }
+        }
+        if (dp_amax) {
+            __syncthreads();  // red[] reuse
+#pragma unroll
+            for (int s = 0; s < FC_S; ++s) {
+                float v = dmx[s];
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+                if (lane == 0) red[wave][s] = v;
+            }
+            __syncthreads();
+            if (tid < ns) {
+                float v = red[0][tid];
+#pragma unroll
+                for (int w = 1; w < FC_T / 64; ++w) v = fmaxf(v, red[w][tid]);
+                dp_amax[b0 + tid] = v;
             }
         }
     }
@@ -786,6 +812,17 @@ extern "C" int slk_fc_xent(const float* pooled, const float* W3, const float* b3
     SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits && dpooled);
     fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
         pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_fc_xent_amax(const float* pooled, const float* W3, const float* b3, const int64_t* labels,
+                                float* logits, float* loss_i, float* dlogits, float* dpooled, float* dp_amax,
+                                float grad_scale, int* err_flag, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits && dpooled && dp_amax);
+    fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
+        pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B, dp_amax);
     return slk_launch_status();
 }
 

@@ -16,6 +16,8 @@
 // Routing/pool/ReLU semantics are those of the f32 kernels (torch CPU: first max wins, strict >).
 #include "slk_common.h"
 
+#include <type_traits>
+
 using namespace slk;
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -444,6 +446,281 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     }
 }
 
+// ============================================================================ conv2 wgrad (dW2, db2)
+// dW2[co][ci][ky][kx] = sum_{b,y,x<24} dY[b][co][y][x] * act[b][ci][y+ky][x+kx], db2[co] = sum dY
+// (src/server_part.py:51). GEMM: M = co, N = (tap, ci), K = output pixels of the whole batch. Both
+// operands need 8 consecutive PIXELS per lane, so both LDS images store pixels as rows with the
+// channels contiguous and are read with ds_read_b64_tr_b16 (one 4-pixel x 16-channel block per 16-lane
+// group, delivered column-major): dY image [192 q = 24 y_l + x][32 co], input image [260 px][32 ci], f16
+// (h, l) planes. Unit = (sample, third): output rows 8t..8t+7 (K = 192 = 6 K-steps, no padding);
+// K-chunk c of 8 pixels = row c / 3, columns 8 (c % 3) .. +7, so the input pixel of tap (ky, kx) is a
+// per-(K-step, lane) base + an immediate. dY pixel rows keep the two 32-B co tiles swapped on odd
+// 8-pixel groups (the two 16-lane groups of a half-wave then hit disjoint banks).
+// A workgroup owns one co half (M = 32) and a K share (units ks, ks + nks, ...); the two co halves
+// of a share run on different workgroups, each splitting the same input rows. Scales are per LAUNCH
+// (the max of the per-sample amax arrays): a K sum spans samples. Staging is register-based and two
+// units ahead: unit u+2's input (8 channels of a pixel per item, channel group fastest across lanes so
+// the ds_write_b128 of 8 lanes cover 128 distinct bytes) and pooled gradient + codes are loaded at the
+// top of unit u and split / routed into the other image at the top of unit u+1.
+// 8 waves: wave = (ci half h, K-step parity kp, tap group tg) over BOTH M tiles, so each input fragment
+// read feeds 6 MFMAs; tap group 1 (4 taps) also carries db via one MFMA per M tile against a ones
+// fragment (h = 0: dY_hi, h = 1: dY_lo); parities are summed through LDS at the end.
+constexpr int X3W_THREADS = 512;
+constexpr int X3W_Q = 192;                           // output pixels (K) per unit
+constexpr int X3W_DYP = X3W_Q * 64;                  // 12,288 B per dY plane (32 co)
+constexpr int X3W_XP = 260 * 64;                     // 16,640 B per input plane (32 ci)
+constexpr int X3W_BUF = 2 * X3W_DYP + 2 * X3W_XP;    // 57,856 B per buffer
+constexpr int X3W_NKS = 128;                         // K shares (slabs)
+constexpr int X3W_XITEMS = 260 * 4;                  // (pixel, 8-channel group) input items per unit
+constexpr int X3W_XR = (X3W_XITEMS + X3W_THREADS - 1) / X3W_THREADS;  // 3 (the last partial)
+constexpr int X3W_DYITEMS = 48 * 8;                  // (window, 4-co group) dY items per unit
+static_assert(2 * X3W_BUF <= 163840, "LDS");
+
+__global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
+    const float* __restrict__ act, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
+    const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3W_BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = wave & 1, kp = (wave >> 1) & 1, tg = wave >> 2;
+    const int nks = (int)gridDim.x / 2;
+    const int cohalf = blockIdx.x & 1, ks = blockIdx.x >> 1;
+    const int U = 3 * B;
+    float* red = reinterpret_cast<float*>(smem);  // prologue scratch (image 0, before any staging)
+
+    // launch scales: max over the batch of the per-sample maxima
+    float ma = 0.f, md = 0.f;
+    for (int i = tid; i < B; i += X3W_THREADS) {
+        ma = fmaxf(ma, act_amax[i]);
+        md = fmaxf(md, dp_amax[i]);
+    }
+    ma = wave_max(ma);
+    md = wave_max(md);
+    if (lane == 0) {
+        red[wave] = ma;
+        red[8 + wave] = md;
+    }
+    __syncthreads();
+    ma = red[0];
+    md = red[8];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+        ma = fmaxf(ma, red[i]);
+        md = fmaxf(md, red[8 + i]);
+    }
+    __syncthreads();
+    const int sx = x3_exp(ma), sd = x3_exp(md);
+    const float xsc = ldexpf(1.f, sx), dsc = ldexpf(1.f, sd);
+
+    // input items: i = tid + 512 r -> channel group cg = i & 3, pixel p = i >> 2 of the unit's 260
+    float xv[X3W_XR][8];
+    auto load_x = [&](int uu) {
+        const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+        const float* base = act + (size_t)b * A_SAMPLE + t3 * 8 * A_HW;
+#pragma unroll
+        for (int r = 0; r < X3W_XR; ++r) {
+            const int i = tid + r * X3W_THREADS;
+            if (r < X3W_XR - 1 || i < X3W_XITEMS) {
+                const int cg = i & 3, p = i >> 2;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[r][j] = base[(8 * cg + j) * A_PIX + p];
+            }
+        }
+    };
+    auto split_x = [&](char* img) {
+#pragma unroll
+        for (int r = 0; r < X3W_XR; ++r) {
+            const int i = tid + r * X3W_THREADS;
+            if (r < X3W_XR - 1 || i < X3W_XITEMS) {
+                const int cg = i & 3, p = i >> 2;
+                f16x8 hh, ll;
+                x3_split8(xv[r], xsc, hh, ll);
+                char* o = img + 2 * X3W_DYP + p * 64 + cg * 16;
+                *reinterpret_cast<f16x8*>(o) = hh;
+                *reinterpret_cast<f16x8*>(o + X3W_XP) = ll;
+            }
+        }
+    };
+    // dY items of a unit: item i < 384 = (4-co group dg = i & 7 of the co half, window dw = i >> 3)
+    const bool dyitem = tid < X3W_DYITEMS;
+    const int dg = tid & 7, dw = tid >> 3;
+    float dv[4];
+    uint32_t dc = 0;
+    auto load_dy = [&](int uu) {
+        if (!dyitem) return;
+        const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+        const int w = (4 * t3 + dw / 12) * P_HW + dw % 12;
+        const size_t o = (size_t)b * P_SAMPLE + (32 * cohalf + 4 * dg) * P_WIN + w;
+        dc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            dv[j] = dpooled[o + j * P_WIN];
+            dc |= (uint32_t)code[o + j * P_WIN] << (8 * j);
+        }
+    };
+    auto store_dy = [&](char* img) {
+        if (!dyitem) return;
+        uint32_t hv[2], lv[2];
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+            const float a = dv[j] * dsc, c = dv[j + 1] * dsc;
+            const _Float16 ha = (_Float16)a, hc = (_Float16)c;
+            const _Float16 la = (_Float16)(a - (float)ha), lc = (_Float16)(c - (float)hc);
+            hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
+            lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
+        }
+        const uint32_t cA = __builtin_amdgcn_perm(0u, dc, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dc, 0x03030202u);
+        const int wy = dw / 12, wx = dw % 12;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos) {
+            const uint32_t T = 0xFFu << (8 * pos);
+            const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
+            const int q = (2 * wy + (pos >> 1)) * 24 + 2 * wx + (pos & 1);
+            // co tile (dg >> 2) sits in slot (dg >> 2) ^ ((q >> 3) & 1)
+            char* o = img + q * 64 + ((((dg >> 2) ^ (q >> 3)) & 1) * 32) + 8 * (dg & 3);
+            *reinterpret_cast<uint2*>(o) = make_uint2(hv[0] & mA, hv[1] & mB);
+            *reinterpret_cast<uint2*>(o + X3W_DYP) = make_uint2(lv[0] & mA, lv[1] & mB);
+        }
+    };
+
+    // transposed-read bases: group g4 = lane >> 4 (K-chunk), lane 4qq + pp of the group
+    const int g4 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    int abase[2];  // dY: pixel 8c + qq (+4), co tile mi in slot mi ^ (g4 & 1)
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) abase[mi] = (8 * g4 + qq) * 64 + ((mi ^ (g4 & 1)) * 32) + pp * 8;
+    int xbase[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const int c = 4 * s + g4;
+        xbase[s] = 2 * X3W_DYP + (((c / 3) * A_HW + 8 * (c % 3) + qq) * 64) + (16 * h + 4 * pp) * 2;
+    }
+    typedef __fp16 hf4 __attribute__((__vector_size__(8)));
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) hf4* lp4;
+    auto trr = [&](const char* p) -> f16x8 {
+        const f16x4 lo = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)p));
+        const f16x4 hi = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)(p + 4 * 64)));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    const _Float16 one = (_Float16)1.0f;
+    const f16x8 ones = {one, one, one, one, one, one, one, one};
+
+    // wave = (ci half h, K-step parity kp, tap group tg: taps 0-4 or 5-8 + db); waves w and w + 4 share
+    // a SIMD, so every SIMD carries one wave of each tap group
+    f32x4 acc[2][5];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+
+    auto kstep = [&](const char* img, int s, auto TG) {
+        constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
+        f16x8 ah[2], al[2];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+            ah[mi] = trr(img + abase[mi] + s * 2048);
+            al[mi] = trr(img + X3W_DYP + abase[mi] + s * 2048);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int tap = T0 + t;
+            const int to = ((tap / 3) * A_HW + tap % 3) * 64;
+            const f16x8 bh = trr(img + xbase[s] + to);
+            const f16x8 bl = trr(img + X3W_XP + xbase[s] + to);
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) acc[mi][t] = mfma_x3(ah[mi], al[mi], bh, bl, acc[mi][t]);
+        }
+        if constexpr (decltype(TG)::value == 1) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) accb[mi] = mfma_f16(h ? al[mi] : ah[mi], ones, accb[mi]);
+        }
+    };
+
+    int u = ks;
+    if (u < U) {
+        load_x(u);
+        load_dy(u);
+        split_x(smem);
+        store_dy(smem);
+        if (u + nks < U) {
+            load_x(u + nks);
+            load_dy(u + nks);
+        }
+    }
+    int k = 0;
+#pragma unroll 1
+    for (; u < U; u += nks, ++k) {
+        __syncthreads();  // image k&1 complete; image (k+1)&1 free
+        const int nx = u + nks, nx2 = u + 2 * nks;
+        const char* img = smem + (k & 1) * X3W_BUF;
+        char* nimg = smem + ((k & 1) ^ 1) * X3W_BUF;
+        if (nx < U) {
+            // unit u+1's rows and dY were requested a whole unit ago
+            split_x(nimg);
+            store_dy(nimg);
+            if (nx2 < U) {
+                load_x(nx2);
+                load_dy(nx2);
+            }
+        }
+        if (tg == 0) {
+#pragma unroll
+            for (int s = kp; s < 6; s += 2) kstep(img, s, std::integral_constant<int, 0>{});
+        } else {
+#pragma unroll
+            for (int s = kp; s < 6; s += 2) kstep(img, s, std::integral_constant<int, 1>{});
+        }
+    }
+    __syncthreads();
+    // K parities: kp = 1 waves hand their sums to kp = 0 through LDS (region per (h, tg))
+    constexpr int XN = 2 * 5 * 4 + 8;  // floats per lane
+    float* xch = reinterpret_cast<float*>(smem) + (h + 2 * tg) * (XN * 64);
+    if (kp == 1) {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xch[((mi * 5 + t) * 4 + r) * 64 + lane] = acc[mi][t][r];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xch[(40 + mi * 4 + r) * 64 + lane] = accb[mi][r];
+        }
+    }
+    __syncthreads();
+    // db: column 0 of each ci half's ones product (tap group 1); h = 1 parks its sum for h = 0
+    float* dbx = reinterpret_cast<float*>(smem) + 4 * XN * 64;
+    if (kp == 0 && tg == 1 && h == 1 && (lane & 15) == 0)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dbx[(mi * 4 + (lane >> 4)) * 4 + r] = accb[mi][r] + xch[(40 + mi * 4 + r) * 64 + lane];
+    __syncthreads();
+    if (kp == 0) {
+        const float us = ldexpf(1.f, -(sx + sd)), ub = ldexpf(1.f, -sd);
+        float* slab = slabs + (size_t)ks * (W2_N + C2);
+        const int ci = 16 * h + (lane & 15);
+        const int nt = tg ? 4 : 5;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+                if (t < nt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int co = 32 * cohalf + 16 * mi + 4 * (lane >> 4) + r;
+                        slab[(co * C1 + ci) * 9 + 5 * tg + t] = (acc[mi][t][r] + xch[((mi * 5 + t) * 4 + r) * 64 + lane]) * us;
+                    }
+            if (tg == 1 && h == 0 && (lane & 15) == 0)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = 32 * cohalf + 16 * mi + 4 * (lane >> 4) + r;
+                    slab[W2_N + co] = (accb[mi][r] + xch[(40 + mi * 4 + r) * 64 + lane] + dbx[(mi * 4 + (lane >> 4)) * 4 + r]) * ub;
+                }
+        }
+    }
+}
+
 // ============================================================================ C-ABI
 extern "C" int slk_row_amax(const float* x, int rows, int n, float* amax, void* stream) {
     SLK_CHECK_ARG(rows >= 0 && n > 0 && (rows == 0 || (x && amax)));
@@ -468,5 +745,17 @@ extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, co
     if (B == 0) return 0;
     hipLaunchKernelGGL(conv2_dgrad_x3_kernel, dim3(B < X3D_GRID ? B : X3D_GRID), dim3(X3D_THREADS), 0,
                        slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_wgrad_x3_nslab(int B) { return B <= 0 ? 0 : (3 * B < X3W_NKS ? 3 * B : X3W_NKS); }
+
+extern "C" int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
+                                  const uint8_t* code, float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act && act_amax && dpooled && dp_amax && code && slabs);
+    if (B == 0) return 0;
+    const int nks = slk_conv2_wgrad_x3_nslab(B);
+    hipLaunchKernelGGL(conv2_wgrad_x3_kernel, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), act, act_amax,
+                       dpooled, dp_amax, code, slabs, B);
     return slk_launch_status();
 }

@@ -32,6 +32,7 @@ _SIGS = {
     "slk_error_string": [_I],
     "slk_build_id": [],
     "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],
+    "slk_conv1_fwd_amax": [_P, _P, _P, _P, _P, _I, _P],
     "slk_conv1_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_conv1_wgrad_nslab": [_I],
     "slk_conv1_wgrad_remask": [_P, _P, _P, _P, _P, _I, _P],
@@ -41,6 +42,7 @@ _SIGS = {
     "slk_xent_fwd_bwd": [_P, _P, _P, _P, _F, _P, _I, _P],
     "slk_fc_dgrad": [_P, _P, _P, _I, _P],
     "slk_fc_xent": [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _I, _P],
+    "slk_fc_xent_amax": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _I, _P],
     "slk_fc_wgrad": [_P, _P, _P, _I, _P],
     "slk_fc_wgrad_nslab": [_I],
     "slk_conv2_dgrad": [_P, _P, _P, _P, _I, _P],
@@ -52,6 +54,8 @@ _SIGS = {
     "slk_row_amax": [_P, _I, _I, _P, _P],
     "slk_conv2_fwd_pool_x3": [_P, _P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_dgrad_x3": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad_x3": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad_x3_nslab": [_I],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
     "slk_sgd": [_P, _P, _I, _F, _P],

@@ -90,9 +90,24 @@ def _loss_sum(values, scale, out):
         out.copy_((values.double().sum() * scale).to(out.dtype).reshape(1))
 
 
+def _pair_amax(client, server):
+    """Same-device client/server pair: let the client's conv1 emit the cut's per-sample max when the
+    server runs the x3 conv2 kernels (saves re-reading the cut)."""
+    if "x3" in (getattr(server, "impl_fwd", None), getattr(server, "impl_wgrad", None)) and hasattr(client, "emit_amax"):
+        client.emit_amax = True
+
+
+def _compute(server, client, act, y, scale):
+    amax = getattr(client, "_act_amax", None)
+    if amax is not None:
+        return server.compute(act, y, scale, act_amax=amax)
+    return server.compute(act, y, scale)
+
+
 class Replicated:
     def __init__(self, client, server, group=None, device=None):
         self.client, self.server = client, server
+        _pair_amax(client, server)
         self.group = group
         self.world = dist.get_world_size(group)
         dev = device if device is not None else client.grads.device
@@ -107,7 +122,7 @@ class Replicated:
         B = x.shape[0]
         scale = 1.0 / (self.world * B)
         act = self.client.forward(x)
-        cut, loss_i = self.server.compute(act, y, scale)
+        cut, loss_i = _compute(self.server, self.client, act, y, scale)
         _loss_sum(loss_i, scale, self.loss_slot)
         if self.overlap:
             # the server gradients (+ loss) are final here: their all-reduce (442 KB) runs on the
@@ -488,6 +503,7 @@ class FedAvg:
 
     def __init__(self, client, server, group=None, device=None):
         self.client, self.server = client, server
+        _pair_amax(client, server)
         self.group = group
         dev = device if device is not None else client.params.device
         self.n = CLIENT_N + SERVER_N
@@ -500,7 +516,7 @@ class FedAvg:
     def local_step(self, x, y):
         B = x.shape[0]
         act = self.client.forward(x)
-        cut, loss_i = self.server.compute(act, y, 1.0 / B)
+        cut, loss_i = _compute(self.server, self.client, act, y, 1.0 / B)
         self.client.backward(cut)
         self.client.step()
         self.server.step()

@@ -142,6 +142,13 @@ class LossLog:
         return out
 
 
+# conv2 implementations per op (forward+pool, dgrad, wgrad): "f32" = the Winograd F(2x2,3x3) kernels
+# on the f32 MFMA; "x3" = the f16-MFMA kernels with hi/lo-split f32 operands (csrc/slk_x3.hip) where
+# they are faster (forward, dgrad), Winograd for wgrad.
+CONV_PRESETS = {"f32": ("wino", "wino", "wino"), "x3": ("x3", "x3", "wino")}
+CONV_DEFAULT = "x3"
+
+
 class ClientStage:
     """Client half: ModelPartA on one device + SGD (src/client_part.py:16-17,112-133).
 
@@ -159,6 +166,8 @@ class ClientStage:
         self._buf = _Buffers()
         self._x = None
         self._act = None
+        self._act_amax = None
+        self.emit_amax = False  # forward also writes the per-sample max of act (x3 server kernels)
 
     @property
     def W1(self):
@@ -179,9 +188,10 @@ class ClientStage:
         """act = relu(conv1(x)) (client_part.py:114). Keeps x/act for the backward."""
         B = x.shape[0]
         act = out if out is not None else self._buf.get("act", (B, 32, 26, 26), torch.float32, self.device)
+        amax = self._buf.get("act_amax", (B,), torch.float32, self.device) if self.emit_amax else None
         with TIMER("conv1_fwd"):
-            ops.conv1_fwd(x, self.W1.detach(), self.b1.detach(), out=act)
-        self._x, self._act = x, act
+            ops.conv1_fwd(x, self.W1.detach(), self.b1.detach(), out=act, act_amax=amax)
+        self._x, self._act, self._act_amax = x, act, amax
         return act
 
     def _slabs(self, cut_grad, x, act, tag="slabs"):
@@ -219,8 +229,10 @@ class ServerStage:
     """Server half: ModelPartB + CrossEntropyLoss + SGD + loss log (src/server_part.py:14-16,25-58)."""
 
     def __init__(self, model: Optional[ModelPartB] = None, lr: float = LR, device="cuda",
-                 loss_log: Optional[LossLog] = None):
+                 loss_log: Optional[LossLog] = None, conv: str = CONV_DEFAULT):
         self.device = torch.device(device)
+        self.conv = conv
+        self.impl_fwd, self.impl_dgrad, self.impl_wgrad = CONV_PRESETS[conv]
         self.model = (model if model is not None else ModelPartB()).to(self.device)
         self.lr = lr
         m = self.model
@@ -244,28 +256,36 @@ class ServerStage:
         return self._buf.get(name, shape, dtype, self.device)
 
     def forward_backward(self, act: torch.Tensor, labels: torch.Tensor, grad_scale: float,
-                         cut_grad: Optional[torch.Tensor] = None):
+                         cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None):
         """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
-        conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss)."""
+        conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
+        of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise."""
         B = act.shape[0]
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
         W3, b3 = m.fc1.weight.detach(), m.fc1.bias.detach()
+        fi, di, wi = self.impl_fwd, self.impl_dgrad, self.impl_wgrad
+        if act_amax is None and "x3" in (fi, wi):
+            with TIMER("act_amax"):
+                act_amax = ops.row_amax(act, out=self._b("act_amax", (B,)))
+        dp_amax = self._b("dp_amax", (B,)) if "x3" in (di, wi) else None
         with TIMER("conv2_fwd_pool"):
             pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
-                                              code=self._b("code", (B, 64, 12, 12), torch.uint8))
+                                              code=self._b("code", (B, 64, 12, 12), torch.uint8), impl=fi,
+                                              act_amax=act_amax)
         with TIMER("fc_xent"):
             _, loss_i, dlogits, dpooled = ops.fc_xent(
                 pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
                 loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
-                dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag)
+                dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
         if cut_grad is None:
             cut_grad = self._b("cut_grad", (B, 32, 26, 26))
         with TIMER("conv2_dgrad"):
-            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad)
+            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
         with TIMER("conv2_wgrad"):
             s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
-                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B), ops.CONV2_SLAB)))
+                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
+                                       impl=wi, act_amax=act_amax, dp_amax=dp_amax)
         with TIMER("fc_wgrad"):
             s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3
@@ -281,9 +301,10 @@ class ServerStage:
         ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB], accumulate=accumulate)
         ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:], accumulate=accumulate)
 
-    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None):
+    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act_amax=None):
         """forward_backward + reduce into self.grads; returns (cut_grad, loss_i)."""
-        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, grad_scale, cut_grad=cut_grad)
+        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, grad_scale, cut_grad=cut_grad,
+                                                         act_amax=act_amax)
         self.reduce_grads(s2, s3, accumulate=accumulate)
         return cut_grad, loss_i
 
@@ -300,11 +321,12 @@ class ServerStage:
             self.loss_log.note_step(step)
 
     def step_request(self, act: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
-                     cut_grad: Optional[torch.Tensor] = None):
+                     cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None):
         """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i). The mean
         loss for `step` lands in the device loss log."""
         B = act.shape[0]
-        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad)
+        cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad,
+                                                         act_amax=act_amax)
         if self.fuse_optim:
             # optimizer.step() + log_metric in ONE launch (bit-identical to the three below); measured
             # -10 us per step at B = 4096 (tools/ab_step.py). The client's SGD stays a separate launch
@@ -334,10 +356,13 @@ class SplitTrainer:
     buffers; `step` copies into them unless the caller hands in those very buffers)."""
 
     def __init__(self, client: Optional[ModelPartA] = None, server: Optional[ModelPartB] = None,
-                 lr: float = LR, device="cuda", graph: bool = True, loss_log: Optional[LossLog] = None):
+                 lr: float = LR, device="cuda", graph: bool = True, loss_log: Optional[LossLog] = None,
+                 conv: str = CONV_DEFAULT):
         self.device = torch.device(device)
         self.client = ClientStage(client, lr, self.device)
-        self.server = ServerStage(server, lr, self.device, loss_log)
+        self.server = ServerStage(server, lr, self.device, loss_log, conv=conv)
+        # the cut's per-sample max rides along with the cut (fused into conv1) for the x3 kernels
+        self.client.emit_amax = "x3" in (self.server.impl_fwd, self.server.impl_wgrad)
         self.graph = graph
         self._graphs = {}
         self.global_step = 0
@@ -348,7 +373,7 @@ class SplitTrainer:
 
     def _eager(self, x, y):
         act = self.client.forward(x)
-        cut_grad, _ = self.server.step_request(act, y)
+        cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax)
         self.client.backward_step(cut_grad)
 
     def static_inputs(self, B: int):

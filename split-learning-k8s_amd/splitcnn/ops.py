@@ -56,9 +56,14 @@ def batch_of(x: torch.Tensor, tail: tuple, name: str) -> int:
 
 
 # ------------------------------------------------------------------------------------ client stage
-def conv1_fwd(x, W1, b1, out=None):
+def conv1_fwd(x, W1, b1, out=None, act_amax=None):
+    """act = relu(conv1(x)); with act_amax (a [B] f32 tensor) also its per-sample max, fused."""
     B = batch_of(x, (1, 28, 28), "x")
     act = _out(out, (B, 32, 26, 26), x)
+    if act_amax is not None:
+        _lib.call("slk_conv1_fwd_amax", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)),
+                  _dev(b1, "conv1.bias", (32,)), _dev(act, "act"), _dev(act_amax, "act_amax", (B,)), B, _stream(x))
+        return act
     _lib.call("slk_conv1_fwd", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)),
               _dev(b1, "conv1.bias", (32,)), _dev(act, "act"), B, _stream(x))
     return act
@@ -166,13 +171,20 @@ def fc_dgrad(dlogits, W3, out=None):
 
 
 def fc_xent(pooled, W3, b3, labels, grad_scale, logits=None, loss_i=None, dlogits=None,
-            dpooled=None, err_flag=None):
+            dpooled=None, err_flag=None, dp_amax=None):
+    """dp_amax (a [B] f32 tensor): also write the per-sample max |dpooled|, fused."""
     B = _pooled_batch(pooled)
     logits = _out(logits, (B, 10), pooled, name="logits")
     loss_i = _out(loss_i, (B,), pooled, name="loss_i")
     dlogits = _out(dlogits, (B, 10), pooled, name="dlogits")
     dpooled = _out(dpooled, tuple(pooled.shape), pooled, name="dpooled")
     eptr = _dev(err_flag, "err_flag", (1,), torch.int32) if err_flag is not None else None
+    if dp_amax is not None:
+        _lib.call("slk_fc_xent_amax", _dev(pooled, "pooled"), _dev(W3, "fc1.weight", (10, 9216)),
+                  _dev(b3, "fc1.bias", (10,)), _labels(labels, B), _dev(logits, "logits"),
+                  _dev(loss_i, "loss_i"), _dev(dlogits, "dlogits"), _dev(dpooled, "dpooled"),
+                  _dev(dp_amax, "dp_amax", (B,)), float(grad_scale), eptr, B, _stream(pooled))
+        return logits, loss_i, dlogits, dpooled
     _lib.call("slk_fc_xent", _dev(pooled, "pooled"), _dev(W3, "fc1.weight", (10, 9216)),
               _dev(b3, "fc1.bias", (10,)), _labels(labels, B), _dev(logits, "logits"),
               _dev(loss_i, "loss_i"), _dev(dlogits, "dlogits"), _dev(dpooled, "dpooled"),
@@ -216,15 +228,26 @@ def conv2_dgrad(dpooled, code, W2, out=None, direct=False, impl=None, dp_amax=No
     return cut_grad
 
 
-def conv2_wgrad_nslab(B: int, direct: bool = False) -> int:
-    return _lib.query("slk_conv2_wgrad_direct_nslab" if direct else "slk_conv2_wgrad_nslab", B)
+def conv2_wgrad_nslab(B: int, direct: bool = False, impl=None) -> int:
+    impl = _impl(direct, impl)
+    return _lib.query({"wino": "slk_conv2_wgrad_nslab", "direct": "slk_conv2_wgrad_direct_nslab",
+                       "x3": "slk_conv2_wgrad_x3_nslab"}[impl], B)
 
 
-def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False):
+def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False, impl=None, act_amax=None, dp_amax=None):
+    impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
     if _dpooled_batch(dpooled) != B:
         raise ValueError("act / dpooled batch mismatch")
-    slabs = _out(slabs, (conv2_wgrad_nslab(B, direct), CONV2_SLAB), act, name="slabs")
+    slabs = _out(slabs, (conv2_wgrad_nslab(B, impl=impl), CONV2_SLAB), act, name="slabs")
+    if impl == "x3":
+        act_amax = row_amax(act) if act_amax is None else act_amax
+        dp_amax = row_amax(dpooled) if dp_amax is None else dp_amax
+        _lib.call("slk_conv2_wgrad_x3", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)), _dev(dpooled, "dpooled"),
+                  _dev(dp_amax, "dp_amax", (B,)), _dev(code, "code", (B, 64, 12, 12), torch.uint8),
+                  _dev(slabs, "slabs"), B, _stream(act))
+        return slabs
+    direct = impl == "direct"
     _lib.call("slk_conv2_wgrad_direct" if direct else "slk_conv2_wgrad", _dev(act, "act"), _dev(dpooled, "dpooled"),
               _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(act))
     return slabs

@@ -23,17 +23,18 @@ from typing import Optional
 import torch
 
 from . import ops
-from .engine import LR, TIMER, LossLog, _Buffers, _flatten_params
+from .engine import CONV_DEFAULT, CONV_PRESETS, LR, TIMER, LossLog, _Buffers, _flatten_params
 from .model_def import ModelPartA, ModelPartB
 
 
 class UServerStage:
     """conv2 trunk of ModelPartB (model_def.py:18-20,24-26) + its SGD."""
 
-    def __init__(self, model: Optional[ModelPartB] = None, lr: float = LR, device="cuda"):
+    def __init__(self, model: Optional[ModelPartB] = None, lr: float = LR, device="cuda", conv: str = CONV_DEFAULT):
         self.device = torch.device(device)
         self.model = (model if model is not None else ModelPartB()).to(self.device)
         self.conv2 = self.model.conv2
+        self.impl_fwd, self.impl_dgrad, self.impl_wgrad = CONV_PRESETS[conv]
         self.lr = lr
         self.params, self.grads = _flatten_params([self.conv2.weight, self.conv2.bias], self.device)
         self._buf = _Buffers()
@@ -45,11 +46,15 @@ class UServerStage:
     def forward(self, act: torch.Tensor, pooled: Optional[torch.Tensor] = None) -> torch.Tensor:
         B = act.shape[0]
         W2, b2 = self.conv2.weight.detach(), self.conv2.bias.detach()
+        amax = None
+        if "x3" in (self.impl_fwd, self.impl_wgrad):
+            amax = ops.row_amax(act, out=self._b("act_amax", (B,)))
         with TIMER("conv2_fwd_pool"):
             pooled, code = ops.conv2_fwd_pool(act, W2, b2,
                                               pooled=pooled if pooled is not None else self._b("pooled", (B, 64, 12, 12)),
-                                              code=self._b("code", (B, 64, 12, 12), torch.uint8))
-        self._act, self._code = act, code
+                                              code=self._b("code", (B, 64, 12, 12), torch.uint8),
+                                              impl=self.impl_fwd, act_amax=amax)
+        self._act, self._code, self._amax = act, code, amax
         return pooled
 
     def backward_step(self, dpooled: torch.Tensor, cut_grad: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -58,11 +63,15 @@ class UServerStage:
         B = act.shape[0]
         W2 = self.conv2.weight.detach()
         cut_grad = cut_grad if cut_grad is not None else self._b("cut_grad", (B, 32, 26, 26))
+        dpa = None
+        if "x3" in (self.impl_dgrad, self.impl_wgrad):
+            dpa = ops.row_amax(dpooled, out=self._b("dp_amax", (B,)))
         with TIMER("conv2_dgrad"):
-            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad)
+            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=self.impl_dgrad, dp_amax=dpa)
         with TIMER("conv2_wgrad"):
             s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
-                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B), ops.CONV2_SLAB)))
+                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=self.impl_wgrad), ops.CONV2_SLAB)),
+                                       impl=self.impl_wgrad, act_amax=self._amax, dp_amax=dpa)
         with TIMER("sgd_server"):
             ops.sgd_from_slabs(self.params, self.grads, s2, self.lr)
         return cut_grad
@@ -123,10 +132,10 @@ class UShapedTrainer:
     """Both U-shape halves on one GPU (cut tensors handed over in place)."""
 
     def __init__(self, model_a: Optional[ModelPartA] = None, model_b: Optional[ModelPartB] = None,
-                 lr: float = LR, device="cuda"):
+                 lr: float = LR, device="cuda", conv: str = CONV_DEFAULT):
         model_b = model_b if model_b is not None else ModelPartB()
         self.client = UClientStage(model_a, model_b, lr, device)
-        self.server = UServerStage(model_b, lr, device)
+        self.server = UServerStage(model_b, lr, device, conv=conv)
         self.global_step = 0
 
     @property

@@ -120,3 +120,75 @@ def test_x3_dgrad_scale_invariance(gpu):
     sc = torch.pow(2.0, torch.tensor([0, -40, 30, 0, 60, -90], device=gpu, dtype=torch.float32))
     out = ops.conv2_dgrad((dp.reshape(B, -1) * sc[:, None]).reshape(dp.shape).contiguous(), cw, p["W2"], impl="x3")
     assert torch.equal(out, base * sc[:, None, None, None])
+
+
+@pytest.mark.parametrize("B", [1, 5, 64, 130, 777])
+def test_x3_wgrad_matches_oracle(gpu, B):
+    from oracle.split_step import conv3x3_wgrad, maxpool2_bwd
+    from splitcnn import ops
+    act, p, y = _inputs(gpu, B, seed=B + 200)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    assert ops.conv2_wgrad_nslab(B, impl="x3") == min(3 * B, 128)
+    sx = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, impl="x3")).cpu().numpy()
+    sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw)).cpu().numpy()
+    codes = cw.cpu().numpy().astype(np.int64)
+    dp64 = dp.double().cpu().numpy().reshape(B, 64, 12, 12)
+    dc = maxpool2_bwd(np.where(codes < 4, dp64, 0.0), np.minimum(codes, 3), (B, 64, 24, 24))
+    dW, db = conv3x3_wgrad(act.double().cpu().numpy(), dc)
+    for got, w, ref in ((sx[:18432], sw[:18432], dW.reshape(-1)), (sx[18432:], sw[18432:], db)):
+        ex, ew = rel_err(got, ref), rel_err(w, ref)
+        assert ex <= 1e-5
+        assert ex <= max(2 * ew, 1e-6), (ex, ew)
+
+
+def test_x3_wgrad_deterministic(gpu):
+    from splitcnn import ops
+    B = 300
+    act, p, y = _inputs(gpu, B, seed=3)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    a = ops.conv2_wgrad_slabs(act, dp, cw, impl="x3").clone()
+    b = ops.conv2_wgrad_slabs(act, dp, cw, impl="x3")
+    assert torch.equal(a, b)
+
+
+def test_fused_amax_outputs(gpu):
+    """conv1_fwd's act_amax and fc_xent's dp_amax equal row_amax of their outputs (exact: a max)."""
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    B = 37
+    a, b = init_models(seed=4)
+    x, y = SyntheticMNIST(5).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
+    am = torch.empty(B, device=gpu)
+    act = ops.conv1_fwd(x, W1, b1, act_amax=am)
+    assert torch.equal(act, ops.conv1_fwd(x, W1, b1))
+    assert torch.equal(am, ops.row_amax(act))
+    W2, b2 = b.conv2.weight.detach().to(gpu), b.conv2.bias.detach().to(gpu)
+    W3, b3 = b.fc1.weight.detach().to(gpu), b.fc1.bias.detach().to(gpu)
+    pooled, code = ops.conv2_fwd_pool(act, W2, b2)
+    dpa = torch.empty(B, device=gpu)
+    r1 = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+    r2 = ops.fc_xent(pooled, W3, b3, y, 1.0 / B)
+    for u, v in zip(r1, r2):
+        assert torch.equal(u, v)
+    assert torch.equal(dpa, ops.row_amax(r1[3]))
+
+
+@pytest.mark.parametrize("conv", ["f32", "x3"])
+def test_trainer_conv_presets_match_fixture(gpu, conv):
+    """One fused SplitTrainer step (conv1 emitting the cut's amax for x3) per conv preset against the
+    reference fixture: post-step weights at the fixture bars (conftest.weight_ok)."""
+    from conftest import PARAMS, load_fixture, weight_ok
+    from splitcnn.engine import SplitTrainer
+    from test_gpu_parity import make_models, param_of
+    for name in ("split_step_b4.npz", "split_step_b13.npz"):
+        fx = load_fixture(name)
+        a, b = make_models(fx)
+        tr = SplitTrainer(a, b, device=gpu, graph=False, conv=conv)
+        assert tr.client.emit_amax == (conv == "x3")
+        tr.step(torch.from_numpy(fx["x_1"]).to(gpu), torch.from_numpy(fx["y_1"]).to(gpu))
+        for k in PARAMS:
+            assert weight_ok(param_of(tr.client, tr.server, k), fx[f"post_{k}_1"], fx[f"init_{k}"]), (name, k)

@@ -40,6 +40,10 @@ def main():
         for impl in ("wino", "direct", "x3"):
             g = torch.empty_like(act)
             cases[f"dgrad_{impl}"] = (lambda impl=impl, g=g: ops.conv2_dgrad(dp, code, W2, g, impl=impl, dp_amax=dpa))
+    if "wgrad" in args.ops:
+        for impl in ("wino", "x3"):
+            sl = torch.empty(ops.conv2_wgrad_nslab(args.B, impl=impl), ops.CONV2_SLAB, device=dev)
+            cases[f"wgrad_{impl}"] = (lambda impl=impl, sl=sl: ops.conv2_wgrad_slabs(act, dp, code, sl, impl=impl, act_amax=amax, dp_amax=dpa))
     cases["row_amax"] = lambda: ops.row_amax(act, amax)
     times = {k: [] for k in cases}
     for _ in range(3):
