@@ -280,74 +280,60 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 // dpooled by `code` (src/server_part.py:51 through model_def.py:25-27). GEMM per sample: M = output
 // pixels (676 -> 43 tiles of 16 consecutive linear pixels p = 26y + x, so a lane's 4 accumulators are 4
 // consecutive pixels = one float4 store), N = 32 ci, K = 64 co x 9 taps (K-step = 32 co of one tap).
-// The routed dY of a unit (sample, co half) is expanded into ONE LDS image with row stride 26 and two
-// zero rows above and below: dY(Y, X) at pixel (Y + 2) * 26 + X, columns 24-25 zero — the 24-wide dY in
-// the 26-wide grid carries exactly the 2-column halo a 3x3 tap needs, so tap (ky, kx) of output pixel
-// p reads image pixel p + 52 - 26 ky - kx: every A fragment address is a per-tile base + an immediate.
-// Pixel records are [8 h chunks... 4 h chunks | 4 l chunks | 32 B pad] = 160 B: conflict-free
-// ds_read_b128 for every tap (tools-checked; 64-B records are 2-way). The image (116 KB) is not
-// double-buffered: the expansion (from pooled values + codes that LDS-DMA staged one unit ahead) sits
-// between two barriers. 8 waves: wave = (ci tile nt, M group g: tiles g, g+4, ...); its weight fragments
-// for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its 11 accumulators live across the
-// sample's two units.
+// Unit = (sample, pixel part pt (tiles 0-14 / 15-28 / 29-42), co half h): the routed dY rows the part's
+// taps reach are expanded into an LDS image with row stride 26: dY(Y, X) at image pixel
+// 2 + 26 (Y - Ybase) + X, columns 24-25 and the 2 leading pixels zero (written once) — the 24-wide dY in
+// the 26-wide grid carries exactly the 2-column halo a 3x3 tap needs, so tap (ky, kx) of output pixel p
+// reads image pixel p + 2 - 26 Ybase - 26 ky - kx: a per-tile base + an immediate. Pixel records are
+// [4 h chunks | 4 l chunks | 32 B pad] = 160 B: conflict-free ds_read_b128 for every tap (64-B records
+// are 2-way). Images are double-buffered (2 x 58.6 KB): unit u+1's pooled gradient + codes are loaded to
+// registers at the top of unit u and routed / split / stored into the other image mid-unit (items
+// (window, 4 co), co group fastest across lanes: the ds_write_b64 of 16 lanes cover 128 distinct
+// bytes); one barrier per unit. 8 waves: wave = (ci tile nt, tile group g: tiles T0 + g + 4i); its weight
+// fragments for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its <= 4 accumulators live
+// across the part's two co halves.
 constexpr int X3D_THREADS = 512;
 constexpr int X3D_REC = 160;                       // bytes per image pixel: h 64 | l 64 | pad 32
-constexpr int X3D_PIX = 28 * A_HW;                 // 728 image pixels (rows -2 .. 25 of dY)
-constexpr int X3D_DY = X3D_PIX * X3D_REC;          // 116,480 B
-constexpr int X3D_RAWDP = 32 * P_WIN * 4;          // 18,432 B pooled gradient of a co half
-constexpr int X3D_RAWC = 32 * P_WIN;               // 4,608 B its codes
-constexpr int X3D_RAW = X3D_RAWDP + X3D_RAWC;      // 23,040 B
-constexpr int X3D_WI = X3D_RAWDP / 1024 + (X3D_RAWC + 1023) / 1024;  // 18 + 5 DMA wave-instructions
+constexpr int X3D_NRMAX = 14;                      // image rows (dY rows) of the largest part
+constexpr int X3D_PIX = 2 + X3D_NRMAX * A_HW;      // 366 image pixels
+constexpr int X3D_IMG = X3D_PIX * X3D_REC;         // 58,560 B
 constexpr int X3D_MT = 43;                         // M tiles per sample
-constexpr int X3D_MPW = 11;                        // M tiles per wave (max)
-constexpr int X3D_ITEMS = P_WIN * 4;               // (window, 8-co chunk) expansion items
+constexpr int X3D_MPW = 4;                         // M tiles per wave and part (max)
 constexpr int X3D_GRID = 256;
-static_assert(X3D_DY + 2 * X3D_RAW <= 163840, "LDS");
+constexpr int X3D_ITEMS_MAX = 7 * P_HW * 8;        // (window, 4-co group) items of the largest part (672)
+static_assert(2 * X3D_IMG <= 163840, "LDS");
 
-__device__ __forceinline__ void x3d_issue_raw(const float* dpooled, const uint8_t* code, int b, int h, int wave,
-                                              int lane, uint32_t raw_lds) {
-    const char* dps = reinterpret_cast<const char*>(dpooled + (size_t)b * P_SAMPLE + h * 32 * P_WIN);
-    const char* cds = reinterpret_cast<const char*>(code + (size_t)b * P_SAMPLE + h * 32 * P_WIN);
-#pragma unroll
-    for (int r = 0; r < (X3D_WI + 7) / 8; ++r) {
-        const int k = wave + 8 * r;
-        if (k < X3D_RAWDP / 1024) {
-            glds16_so(dps, (uint32_t)(k * 1024 + lane * 16), raw_lds + k * 1024);
-        } else if (k < X3D_WI) {
-            const int kk = k - X3D_RAWDP / 1024;
-            if (kk * 1024 + lane * 16 < X3D_RAWC)
-                glds16_so(cds, (uint32_t)(kk * 1024 + lane * 16), raw_lds + X3D_RAWDP + kk * 1024);
-        }
-    }
-}
+__device__ __forceinline__ int x3d_t0(int pt) { return pt == 0 ? 0 : (pt == 1 ? 15 : 29); }
+__device__ __forceinline__ int x3d_ybase(int pt) { return pt == 0 ? -2 : (pt == 1 ? 6 : 14); }
+__device__ __forceinline__ int x3d_nwr(int pt) { return pt == 2 ? 7 : 6; }  // image window rows
 
 __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ dpooled, const float* __restrict__ amax, const uint8_t* __restrict__ code,
     const float* __restrict__ W2, float* __restrict__ cut_grad, int B) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3D_DY + 2 * X3D_RAW];
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
     const int n16 = lane & 15, kc = lane >> 4;
-    char* const dy = smem;
-    char* const raw0 = smem + X3D_DY;
     const int G = gridDim.x;
-    int b = blockIdx.x;
-    if (b < B) x3d_issue_raw(dpooled, code, b, 0, wave, lane, lds_u32(raw0));
+    const int U = 6 * B;
 
-    // zero the dY image once: its halo rows / columns are never written again
-    for (int o = tid * 16; o < X3D_DY; o += X3D_THREADS * 16) *reinterpret_cast<uint4*>(dy + o) = make_uint4(0, 0, 0, 0);
+    // zero both images once: the leading pixels and columns 24-25 are never written again
+    for (int o = tid * 16; o < 2 * X3D_IMG; o += X3D_THREADS * 16) *reinterpret_cast<uint4*>(smem + o) = make_uint4(0, 0, 0, 0);
 
-    // weight scale (max |W2|), reduced through the second raw buffer (not in use yet)
-    float* red = reinterpret_cast<float*>(raw0 + X3D_RAW);
+    // weight scale (max |W2|), reduced through the tail of image 1 (outside every image pixel's h|l)
+    float* red = reinterpret_cast<float*>(smem + X3D_IMG + 128);  // pixel 0's pad is never read
     float wm = 0.f;
     for (int e = tid; e < W2_N; e += X3D_THREADS) wm = fmaxf(wm, fabsf(W2[e]));
     wm = wave_max(wm);
+    __syncthreads();  // zeroing done before red[] is written into image 1
     if (lane == 0) red[wave] = wm;
     __syncthreads();
     wm = red[0];
 #pragma unroll
     for (int i = 1; i < 8; ++i) wm = fmaxf(wm, red[i]);
+    __syncthreads();
+    if (tid < 8) red[tid] = 0.f;  // restore the zero image
     const int sw = x3_exp(wm);
     const float wsc = ldexpf(1.f, sw);
     // B fragments: lane (n16, kc) holds W2[32h + 8kc + j][ci][tap], ci = 16nt + n16
@@ -364,73 +350,136 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 x3_split8(v, wsc, wh[h][tap], wl[h][tap]);
             }
     }
-    // A fragment bases: tile g + 4i, row n16 -> image pixel 16(g + 4i) + n16 + 52 (tap (2, 2)); two
-    // bases so every (i, tap) offset is a 16-bit immediate
-    const int a0 = (16 * g + n16) * X3D_REC + kc * 16;
-    const int a1 = a0 + 6 * 64 * X3D_REC;
 
-    auto expand = [&](const char* raw, float sc) {
+    // expansion items of a unit: i = tid + 512 r -> 4-co group c4 = i & 7, window wi = i >> 3 (row-major
+    // over the part's image window rows); rows outside 0..11 expand to zeros
+    float dv[2][4];
+    uint32_t dcw[2];
+    auto load_dy = [&](int uu) {
+        const int b = uu / 6, rr = uu - (uu / 6) * 6, pt = rr >> 1, h = rr & 1;
+        const int wr0 = x3d_ybase(pt) / 2, nwr = x3d_nwr(pt);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int i = tid + r * X3D_THREADS;
-            if (r == 0 || i < X3D_ITEMS) {
-                const int c8 = i / P_WIN, w = i - (i / P_WIN) * P_WIN;
-                float v[8];
-                uint32_t cw0 = 0, cw1 = 0;
+            const int c4 = i & 7, wi = i >> 3;
+            const int wr = wr0 + wi / P_HW, wx = wi - (wi / P_HW) * P_HW;
+            dcw[r] = 0x04040404u;  // CODE_NONE: routes nothing
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    v[j] = *reinterpret_cast<const float*>(raw + ((8 * c8 + j) * P_WIN + w) * 4);
-                    const uint32_t c = *reinterpret_cast<const uint8_t*>(raw + X3D_RAWDP + (8 * c8 + j) * P_WIN + w);
-                    if (j < 4) cw0 |= c << (8 * j);
-                    else cw1 |= c << (8 * (j - 4));
+            for (int j = 0; j < 4; ++j) dv[r][j] = 0.f;
+            if (i < nwr * P_HW * 8 && wr >= 0 && wr < P_HW) {
+                const size_t o = (size_t)b * P_SAMPLE + (32 * h + 4 * c4) * P_WIN + wr * P_HW + wx;
+                dcw[r] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    dv[r][j] = dpooled[o + j * P_WIN];
+                    dcw[r] |= (uint32_t)code[o + j * P_WIN] << (8 * j);
                 }
-                f16x8 hh, ll;
-                x3_split8(v, sc, hh, ll);
-                const uint4 hv = __builtin_bit_cast(uint4, hh), lv = __builtin_bit_cast(uint4, ll);
-                const uint32_t cA = __builtin_amdgcn_perm(0u, cw0, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw0, 0x03030202u);
-                const uint32_t cC = __builtin_amdgcn_perm(0u, cw1, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw1, 0x03030202u);
-                const int wy = w / P_HW, wx = w - (w / P_HW) * P_HW;
-                char* rec = dy + ((2 * wy + 2) * A_HW + 2 * wx) * X3D_REC + c8 * 16;
+            }
+        }
+    };
+    auto store_dy = [&](int uu, char* img) {
+        const int b = uu / 6, pt = (uu - (uu / 6) * 6) >> 1;
+        const int nwr = x3d_nwr(pt);
+        const float sc = ldexpf(1.f, x3_exp(amax[b]));
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = tid + r * X3D_THREADS;
+            if (r == 0 || i < nwr * P_HW * 8) {
+                const int c4 = i & 7, wi = i >> 3;
+                const int wrl = wi / P_HW, wx = wi - (wi / P_HW) * P_HW;
+                uint32_t hv[2], lv[2];
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    const float a = dv[r][j] * sc, c = dv[r][j + 1] * sc;
+                    const _Float16 ha = (_Float16)a, hc = (_Float16)c;
+                    const _Float16 la = (_Float16)(a - (float)ha), lc = (_Float16)(c - (float)hc);
+                    hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
+                    lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
+                }
+                const uint32_t cA = __builtin_amdgcn_perm(0u, dcw[r], 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw[r], 0x03030202u);
+                char* rec = img + (2 + (2 * wrl) * A_HW + 2 * wx) * X3D_REC + c4 * 8;
 #pragma unroll
                 for (int pos = 0; pos < 4; ++pos) {
                     const uint32_t T = 0xFFu << (8 * pos);
                     const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
-                    const uint32_t mC = __builtin_amdgcn_perm(0u, T, cC), mD = __builtin_amdgcn_perm(0u, T, cD);
                     char* o = rec + ((pos >> 1) * A_HW + (pos & 1)) * X3D_REC;
-                    *reinterpret_cast<uint4*>(o) = make_uint4(hv.x & mA, hv.y & mB, hv.z & mC, hv.w & mD);
-                    *reinterpret_cast<uint4*>(o + 64) = make_uint4(lv.x & mA, lv.y & mB, lv.z & mC, lv.w & mD);
+                    *reinterpret_cast<uint2*>(o) = make_uint2(hv[0] & mA, hv[1] & mB);
+                    *reinterpret_cast<uint2*>(o + 64) = make_uint2(lv[0] & mA, lv[1] & mB);
                 }
             }
         }
     };
 
-    int rb = 0;  // raw buffer of the current unit
+    f32x4 acc[X3D_MPW];
+    int u = blockIdx.x;
+    // units of a workgroup: u, u + G, ... — the two co halves of a part must be consecutive for the
+    // accumulators, so a workgroup walks PAIRS: unit index = 2 * (pair) + h with pairs strided by G
+    // (pair = (sample, part))
+    const int P = 3 * B;  // pairs
+    int pr = blockIdx.x;
+    if (pr < P) {
+        load_dy(2 * pr);
+        __syncthreads();  // zeroing / red restore done before the first expansion
+        store_dy(2 * pr, smem);
+        load_dy(2 * pr + 1);
+    }
+    int k = 0;
+    (void)u;
 #pragma unroll 1
-    for (; b < B; b += G) {
-        const float sc = ldexpf(1.f, x3_exp(amax[b]));
-        f32x4 acc[X3D_MPW];
+    for (; pr < P; pr += G) {
+        const int b = pr / 3, pt = pr - (pr / 3) * 3;
+        const int T0 = x3d_t0(pt), T1 = pt == 2 ? X3D_MT : x3d_t0(pt + 1);
+        const int cbase = (2 - A_HW * x3d_ybase(pt) - 54) * X3D_REC;
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // raw(b, h) landed everywhere; every wave is done with the dY image
-            const int nb = h ? b + G : b, nh = h ^ 1;
-            if (nb < B) x3d_issue_raw(dpooled, code, nb, nh, wave, lane, lds_u32(raw0 + (rb ^ 1) * X3D_RAW));
-            expand(raw0 + rb * X3D_RAW, sc);
-            __syncthreads();
-            rb ^= 1;
+        for (int h = 0; h < 2; ++h, ++k) {
+            __syncthreads();  // image k&1 complete; image (k+1)&1 free
+            const char* img = smem + (k & 1) * X3D_IMG;
+            char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
+            const int unx = min(h ? 2 * (pr + G) : 2 * pr + 1, U - 1);   // the unit after this one
+            const int unx2 = min(h ? 2 * (pr + G) + 1 : 2 * (pr + G), U - 1);  // and the one after that
+            // A fragments of (tile i, tap) through a 4-slot ring, read 3 steps ahead of their MFMAs (one
+            // read pair per 3 dependent MFMAs: waiting on each read left the SIMD half idle)
+            const char* abw = img + cbase + ((T0 + g) * 16 + n16) * X3D_REC + kc * 16;
+            auto rd = [&](int i, int tap, f16x8& fh, f16x8& fl) {
+                const char* ab = abw + i * 64 * X3D_REC + (54 - 26 * (tap / 3) - tap % 3) * X3D_REC;
+                fh = *reinterpret_cast<const f16x8*>(ab);
+                fl = *reinterpret_cast<const f16x8*>(ab + 64);
+            };
+            f16x8 fh[4], fl[4];
+            constexpr int NS = 27;  // tiles 0..2 exist for every wave and part
 #pragma unroll
-            for (int i = 0; i < X3D_MPW; ++i) {
-                if (g + 4 * i < X3D_MT) {
-                    const char* ab = dy + (i < 6 ? a0 + i * 64 * X3D_REC : a1 + (i - 6) * 64 * X3D_REC);
+            for (int q = 0; q < 3; ++q) rd(q / 9, q % 9, fh[q], fl[q]);
 #pragma unroll
-                    for (int tap = 0; tap < 9; ++tap) {
-                        const int o = (52 - 26 * (tap / 3) - tap % 3) * X3D_REC;
-                        const f16x8 ah = *reinterpret_cast<const f16x8*>(ab + o);
-                        const f16x8 al = *reinterpret_cast<const f16x8*>(ab + o + 64);
-                        acc[i] = mfma_x3(ah, al, wh[h][tap], wl[h][tap], acc[i]);
-                    }
+            for (int st = 0; st < NS; ++st) {
+                if (st + 3 < NS) rd((st + 3) / 9, (st + 3) % 9, fh[(st + 3) & 3], fl[(st + 3) & 3]);
+                const int i = st / 9, tap = st % 9;
+                acc[i] = mfma_x3(fh[st & 3], fl[st & 3], wh[h][tap], wl[h][tap], acc[i]);
+            }
+            // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
+            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+            // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused)
+            store_dy(unx, nimg);
+            load_dy(unx2);
+            if (T0 + g + 12 < T1) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rd(3, q, fh[q], fl[q]);
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    if (tap + 3 < 9) rd(3, tap + 3, fh[(tap + 3) & 3], fl[(tap + 3) & 3]);
+                    acc[3] = mfma_x3(fh[tap & 3], fl[tap & 3], wh[h][tap], wl[h][tap], acc[3]);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
+                    if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
                 }
             }
         }
@@ -439,8 +488,8 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) {
-            const int p = 16 * (g + 4 * i) + 4 * kc;
-            if (g + 4 * i < X3D_MT && p < A_PIX)
+            const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
+            if (t < T1 && p < A_PIX)
                 *reinterpret_cast<float4*>(gb + p) = make_float4(acc[i][0] * us, acc[i][1] * us, acc[i][2] * us, acc[i][3] * us);
         }
     }
@@ -743,7 +792,8 @@ extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, co
                                   float* cut_grad, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && dpooled && dp_amax && code && W2 && cut_grad);
     if (B == 0) return 0;
-    hipLaunchKernelGGL(conv2_dgrad_x3_kernel, dim3(B < X3D_GRID ? B : X3D_GRID), dim3(X3D_THREADS), 0,
+    const int P = 3 * B;
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
                        slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B);
     return slk_launch_status();
 }
