@@ -663,26 +663,56 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         for (int t = 0; t < 5; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
-    auto kstep = [&](const char* img, int s, auto TG) {
+    // a unit's work for this wave: K-steps kp, kp + 2, kp + 4 x its taps; B fragments (4 transposed reads)
+    // run 2 steps ahead through a 3-slot ring, A fragments (8 reads) one K-step ahead; the
+    // sched_group_barriers keep that order (hipcc otherwise sinks every read next to its MFMAs)
+    auto unit_mfma = [&](const char* img, auto TG) {
         constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
-        f16x8 ah[2], al[2];
+        constexpr bool DB = decltype(TG)::value == 1;
+        constexpr int N = 3 * NT;
+        f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
+        auto rdA = [&](int j, int slot) {
+            const int s = kp + 2 * j;
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-            ah[mi] = trr(img + abase[mi] + s * 2048);
-            al[mi] = trr(img + X3W_DYP + abase[mi] + s * 2048);
-        }
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int tap = T0 + t;
+            for (int mi = 0; mi < 2; ++mi) {
+                Ah[slot][mi] = trr(img + abase[mi] + s * 2048);
+                Al[slot][mi] = trr(img + X3W_DYP + abase[mi] + s * 2048);
+            }
+        };
+        auto xb = [&](int j) { return kp ? xbase[1 + 2 * j] : xbase[2 * j]; };
+        auto rdB = [&](int n, int slot) {
+            const int j = n / NT, tap = T0 + n % NT;
             const int to = ((tap / 3) * A_HW + tap % 3) * 64;
-            const f16x8 bh = trr(img + xbase[s] + to);
-            const f16x8 bl = trr(img + X3W_XP + xbase[s] + to);
+            Bh[slot] = trr(img + xb(j) + to);
+            Bl[slot] = trr(img + X3W_XP + xb(j) + to);
+        };
+        rdA(0, 0);
+        rdB(0, 0);
+        rdB(1, 1);
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi) acc[mi][t] = mfma_x3(ah[mi], al[mi], bh, bl, acc[mi][t]);
+        for (int n = 0; n < N; ++n) {
+            if (n + 2 < N) {
+                rdB(n + 2, (n + 2) % 3);
+                if ((n + 2) % NT == 0) rdA((n + 2) / NT, ((n + 2) / NT) & 1);
+            }
+            const int j = n / NT, t = n % NT;
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+                acc[mi][t] = mfma_x3(Ah[j & 1][mi], Al[j & 1][mi], Bh[n % 3], Bl[n % 3], acc[mi][t]);
+            if (DB && t == NT - 1) {
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi) accb[mi] = mfma_f16(h ? Al[j & 1][mi] : Ah[j & 1][mi], ones, accb[mi]);
+            }
         }
-        if constexpr (decltype(TG)::value == 1) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi) accb[mi] = mfma_f16(h ? al[mi] : ah[mi], ones, accb[mi]);
+        for (int n = 0; n < N; ++n) {
+            if (DB && n % NT == NT - 1) __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            else __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            if (n + 2 < N) {
+                if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+            }
         }
     };
 
@@ -713,13 +743,8 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
                 load_dy(nx2);
             }
         }
-        if (tg == 0) {
-#pragma unroll
-            for (int s = kp; s < 6; s += 2) kstep(img, s, std::integral_constant<int, 0>{});
-        } else {
-#pragma unroll
-            for (int s = kp; s < 6; s += 2) kstep(img, s, std::integral_constant<int, 1>{});
-        }
+        if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
+        else unit_mfma(img, std::integral_constant<int, 1>{});
     }
     __syncthreads();
     // K parities: kp = 1 waves hand their sums to kp = 0 through LDS (region per (h, tg))
