@@ -71,7 +71,7 @@ def parse():
                     help="k2 = reference split CNN fp32 (headline); k5 = widened bf16 split CNN")
     ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
     ap.add_argument("--k5-batch", type=int, default=4096)
-    ap.add_argument("--conv", default=None, choices=["x3", "f32"],
+    ap.add_argument("--conv", default=None, choices=["x3", "x3w", "f32"],
                     help="K2 conv2 kernels: x3 = f16 MFMA with hi/lo-split fp32 operands (fwd, dgrad) + "
                          "Winograd wgrad; f32 = Winograd F(2x2,3x3) on the f32 MFMA throughout "
                          "(default: splitcnn.engine.CONV_DEFAULT)")
@@ -220,11 +220,14 @@ def run_single(args, out):
                                    "checked vs fp64 at the f32 path's bars), 'wino' = Winograd on the f32 MFMA"}
     out["loss_first_last"] = [round(losses[0][1], 5), round(losses[-1][1], 5)] if losses else None
     if not args.no_conv_compare:
-        other = "f32" if conv == "x3" else "x3"
-        tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
-        dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
-        out["conv_presets"] = {conv: round(out["value"], 1), other: round(args.steps * B / dto, 1)}
-        del tro
+        out["conv_presets"] = {conv: round(out["value"], 1)}
+        for other in CONV_PRESETS:
+            if other == conv:
+                continue
+            tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
+            dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
+            out["conv_presets"][other] = round(args.steps * B / dto, 1)
+            del tro
     if not args.no_kernel_pass:
         tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False, conv=conv)
         kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)

@@ -97,8 +97,10 @@ __global__ __launch_bounds__(256) void row_amax_kernel(const float* __restrict__
 //      conflict-free, tools-checked for all 9 taps).
 // One `s_waitcnt vmcnt` (allowing the previous epilogue's 12 stores to stay in flight) + barrier per
 // unit. 8 waves (2 per SIMD): wave = (co half ch, window row wr); its 2 x 9 taps x (h, l) weight
-// fragments (144 VGPRs) stay in registers for the launch. (4 waves holding all 64 co, 288 registers,
-// one per SIMD: 0.375 ms vs 0.262 — hipcc copies the AGPR-resident weights back per MFMA.) A = input (M = 16 pixels = 4 pool windows x
+// fragments (144 VGPRs) stay in registers for the launch. Tried and slower: 4 waves (one per SIMD)
+// holding all 64 co — weights copied back from AGPRs per MFMA by hipcc 0.375 ms; taps 0-7 in AGPRs as
+// asm MFMA operands + tap 8 in VGPRs, A reads 2 steps ahead 0.342 ms (vs 0.254): one wave per SIMD
+// leaves the split/epilogue VALU and the LDS latency uncovered. A = input (M = 16 pixels = 4 pool windows x
 // 4 positions), B = weights (N = 16 co), K = 32 ci of one tap; the C/D layout puts the 4 positions of
 // one window in one lane's 4 accumulators, so ReLU + 2x2 max-pool + routing code are in-register.
 constexpr int X3F_WAVES = 8;

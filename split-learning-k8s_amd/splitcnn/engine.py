@@ -144,8 +144,8 @@ class LossLog:
 
 # conv2 implementations per op (forward+pool, dgrad, wgrad): "f32" = the Winograd F(2x2,3x3) kernels
 # on the f32 MFMA; "x3" = the f16-MFMA kernels with hi/lo-split f32 operands (csrc/slk_x3.hip) where
-# they are faster (forward, dgrad), Winograd for wgrad.
-CONV_PRESETS = {"f32": ("wino", "wino", "wino"), "x3": ("x3", "x3", "wino")}
+# are used for all three ("x3"), or for forward + dgrad with the Winograd wgrad ("x3w").
+CONV_PRESETS = {"f32": ("wino", "wino", "wino"), "x3": ("x3", "x3", "x3"), "x3w": ("x3", "x3", "wino")}
 CONV_DEFAULT = "x3"
 
 

@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=3)
 ap.add_argument("--config", default="k2", choices=["k2", "k5"])
+ap.add_argument("--conv", default=None, help="K2 conv preset (splitcnn.engine.CONV_PRESETS; default CONV_DEFAULT)")
 args = ap.parse_args()
 if args.config == "k5":
     from splitcnn.wide import SyntheticCIFAR, WideTrainer, init_wide_models
@@ -23,7 +24,8 @@ if args.config == "k5":
     tr = WideTrainer(*init_wide_models(seed=0), device="cuda:0", graph=False)
 else:
     x, y = SyntheticMNIST(42).batch(args.batch)
-    tr = SplitTrainer(*init_models(seed=0), device="cuda:0", graph=False)
+    from splitcnn.engine import CONV_DEFAULT
+    tr = SplitTrainer(*init_models(seed=0), device="cuda:0", graph=False, conv=args.conv or CONV_DEFAULT)
 x, y = x.cuda(), y.cuda()
 for _ in range(args.steps):
     tr.step(x, y)

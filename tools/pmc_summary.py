@@ -49,7 +49,9 @@ if args.traffic_out:
     prev = json.load(open(args.traffic_out)) if os.path.exists(args.traffic_out) else {}
     names.update({"conv2_fwd_pool_wino_kernel": "conv2_fwd_pool", "conv2_fwd_pool_wino2_kernel": "conv2_fwd_pool",
                   "conv2_dgrad_wino_kernel": "conv2_dgrad",
-                  "conv2_wgrad_wino_kernel": "conv2_wgrad", "fc_head_kernel<8>": "fc_xent"})
+                  "conv2_wgrad_wino_kernel": "conv2_wgrad", "fc_head_kernel<8>": "fc_xent",
+                  "conv2_fwd_pool_x3_kernel": "conv2_fwd_pool_x3", "conv2_dgrad_x3_kernel": "conv2_dgrad_x3",
+                  "conv2_wgrad_x3_kernel": "conv2_wgrad_x3"})
     # widened (K5) template instantiations -> bench.py's kernel names (csrc/slk_wide.hip:824-836, 1055)
     wide = [("wide_conv32_kernel<Conv32Cfg<64, 128, 32", "wide_conv2_fwd"),
             ("wide_conv_kernel<ConvCfg<64, 128, 32", "wide_conv2_fwd"),
