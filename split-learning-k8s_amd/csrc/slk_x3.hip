@@ -535,7 +535,12 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = wave & 1, kp = (wave >> 1) & 1, tg = wave >> 2;
     const int nks = (int)gridDim.x / 2;
-    const int cohalf = blockIdx.x & 1, ks = blockIdx.x >> 1;
+    // the two co halves of a K share read the same input rows: put them on one XCD (blocks b and b + 8
+    // share one, round-robin dispatch) so the second read is an L2 hit
+    const int bid = blockIdx.x;
+    const bool xcd = (nks & 7) == 0;
+    const int cohalf = xcd ? (bid >> 3) & 1 : bid & 1;
+    const int ks = xcd ? (bid >> 4) * 8 + (bid & 7) : bid >> 1;
     const int U = 3 * B;
     float* red = reinterpret_cast<float*>(smem);  // prologue scratch (image 0, before any staging)
 
