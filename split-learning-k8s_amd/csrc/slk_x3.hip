@@ -197,11 +197,12 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             const int x = 2 * wx + (q & 1) + kx;
             abase[mt][kx] = ((2 * wr + (q >> 1)) * A_HW + x) * 64 + ((kc ^ (x & 2)) * 16);
         }
-    // split items: (pixel p, chunk c8) -> raw read offset, f16 write offset
+    // split items: (pixel p, chunk c8) -> raw read offset, f16 write offset; threads past the last item
+    // redo it (identical stores): the split has no branch and shares a basic block with the MFMAs
     int rd[X3F_IPT], wo[X3F_IPT];
 #pragma unroll
     for (int it = 0; it < X3F_IPT; ++it) {
-        const int i = tid + it * X3F_THREADS;
+        const int i = min(tid + it * X3F_THREADS, X3F_ITEMS - 1);
         const int c8 = i / X3F_PIX, p = i - (i / X3F_PIX) * X3F_PIX;
         const int x = p % A_HW;
         rd[it] = (8 * c8 * X3F_PIX + p) * 4;
@@ -211,15 +212,13 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         const float sc = ldexpf(1.f, x3_exp(amax[uu / 3]));
 #pragma unroll
         for (int it = 0; it < X3F_IPT; ++it) {
-            if (it < X3F_IPT - 1 || tid + it * X3F_THREADS < X3F_ITEMS) {
-                float v[8];
+            float v[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(raw + rd[it] + j * X3F_PIX * 4);
-                f16x8 h, l;
-                x3_split8(v, sc, h, l);
-                *reinterpret_cast<f16x8*>(buf + wo[it]) = h;
-                *reinterpret_cast<f16x8*>(buf + X3F_PLANE + wo[it]) = l;
-            }
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(raw + rd[it] + j * X3F_PIX * 4);
+            f16x8 h, l;
+            x3_split8(v, sc, h, l);
+            *reinterpret_cast<f16x8*>(buf + wo[it]) = h;
+            *reinterpret_cast<f16x8*>(buf + X3F_PLANE + wo[it]) = l;
         }
     };
 
@@ -249,7 +248,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 #pragma unroll
                 for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = mfma_x3(ah, al, wh[nt][tap], wl[nt][tap], acc[mt][nt]);
             }
-            if (mt == 0 && u + G < U) split_unit(u + G, raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+            // past the last unit this splits a clamped unit's stale raw rows into a buffer nobody reads
+            if (mt == 0) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
         }
         // epilogue: unscale (exact), bias, ReLU, 2x2 max-pool, routing code
         const int b = u / 3, t3 = u - (u / 3) * 3;
@@ -575,35 +575,32 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         const float* base = act + (size_t)b * A_SAMPLE + t3 * 8 * A_HW;
 #pragma unroll
         for (int r = 0; r < X3W_XR; ++r) {
-            const int i = tid + r * X3W_THREADS;
-            if (r < X3W_XR - 1 || i < X3W_XITEMS) {
-                const int cg = i & 3, p = i >> 2;
+            // lanes past the last item redo it (same value to the same place): no exec-masked branch
+            const int i = min(tid + r * X3W_THREADS, X3W_XITEMS - 1);
+            const int cg = i & 3, p = i >> 2;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) xv[r][j] = base[(8 * cg + j) * A_PIX + p];
-            }
+            for (int j = 0; j < 8; ++j) xv[r][j] = base[(8 * cg + j) * A_PIX + p];
         }
     };
     auto split_x = [&](char* img) {
 #pragma unroll
         for (int r = 0; r < X3W_XR; ++r) {
-            const int i = tid + r * X3W_THREADS;
-            if (r < X3W_XR - 1 || i < X3W_XITEMS) {
-                const int cg = i & 3, p = i >> 2;
-                f16x8 hh, ll;
-                x3_split8(xv[r], xsc, hh, ll);
-                char* o = img + 2 * X3W_DYP + p * 64 + cg * 16;
-                *reinterpret_cast<f16x8*>(o) = hh;
-                *reinterpret_cast<f16x8*>(o + X3W_XP) = ll;
-            }
+            const int i = min(tid + r * X3W_THREADS, X3W_XITEMS - 1);
+            const int cg = i & 3, p = i >> 2;
+            f16x8 hh, ll;
+            x3_split8(xv[r], xsc, hh, ll);
+            char* o = img + 2 * X3W_DYP + p * 64 + cg * 16;
+            *reinterpret_cast<f16x8*>(o) = hh;
+            *reinterpret_cast<f16x8*>(o + X3W_XP) = ll;
         }
     };
-    // dY items of a unit: item i < 384 = (4-co group dg = i & 7 of the co half, window dw = i >> 3)
-    const bool dyitem = tid < X3W_DYITEMS;
-    const int dg = tid & 7, dw = tid >> 3;
+    // dY items of a unit: item i < 384 = (4-co group dg = i & 7 of the co half, window dw = i >> 3);
+    // threads past 383 redo item 383 (identical stores, no branch)
+    const int ditem = min(tid, X3W_DYITEMS - 1);
+    const int dg = ditem & 7, dw = ditem >> 3;
     float dv[4];
     uint32_t dc = 0;
     auto load_dy = [&](int uu) {
-        if (!dyitem) return;
         const int b = uu / 3, t3 = uu - (uu / 3) * 3;
         const int w = (4 * t3 + dw / 12) * P_HW + dw % 12;
         const size_t o = (size_t)b * P_SAMPLE + (32 * cohalf + 4 * dg) * P_WIN + w;
@@ -615,7 +612,6 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
     };
     auto store_dy = [&](char* img) {
-        if (!dyitem) return;
         uint32_t hv[2], lv[2];
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
@@ -729,10 +725,8 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         load_dy(u);
         split_x(smem);
         store_dy(smem);
-        if (u + nks < U) {
-            load_x(u + nks);
-            load_dy(u + nks);
-        }
+        load_x(min(u + nks, U - 1));
+        load_dy(min(u + nks, U - 1));
     }
     int k = 0;
 #pragma unroll 1
@@ -741,15 +735,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         const int nx = u + nks, nx2 = u + 2 * nks;
         const char* img = smem + (k & 1) * X3W_BUF;
         char* nimg = smem + ((k & 1) ^ 1) * X3W_BUF;
-        if (nx < U) {
-            // unit u+1's rows and dY were requested a whole unit ago
-            split_x(nimg);
-            store_dy(nimg);
-            if (nx2 < U) {
-                load_x(nx2);
-                load_dy(nx2);
-            }
-        }
+        // unit u+1's rows and dY were requested a whole unit ago. No branch around the staging (past the
+        // last unit it re-stages a clamped valid unit nobody reads), so it shares one basic block with
+        // the MFMAs and its VALU can fill their issue gaps
+        split_x(nimg);
+        store_dy(nimg);
+        load_x(min(nx2, U - 1));
+        load_dy(min(nx2, U - 1));
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
     }
