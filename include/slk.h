@@ -164,6 +164,15 @@ int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t
 int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
                        const uint8_t* code, float* slabs, int B, void* stream);
 int slk_conv2_wgrad_x3_nslab(int B);
+/* The forward that also writes its split f16 input images (act16, slk_conv2_act16_bytes(B) bytes; data
+ * scale = the launch max of act_amax) and the wgrad that moves them by LDS-DMA instead of loading and
+ * splitting act: the wgrad's input staging becomes a copy. Same results as slk_conv2_wgrad_x3 (bitwise:
+ * the same scale, the same f16 values). */
+int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float* W2, const float* b2, float* pooled,
+                           uint8_t* code, uint16_t* act16, int B, void* stream);
+int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled, const float* dp_amax,
+                        const uint8_t* code, float* slabs, int B, void* stream);
+int64_t slk_conv2_act16_bytes(int B);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 

@@ -134,9 +134,13 @@ __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave
     }
 }
 
+// act16 (optional): every unit's f16 image (h plane | l plane, 33,280 B, the layout above) is also
+// written to act16 + u * 33,280 for conv2_wgrad_x3's input operand; the data scale is then the launch
+// max of act_amax (a wgrad K sum spans samples) instead of the per-sample one.
 __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     const float* __restrict__ act, const float* __restrict__ amax, const float* __restrict__ W2,
-    const float* __restrict__ b2, float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
+    const float* __restrict__ b2, float* __restrict__ pooled, uint8_t* __restrict__ code, int B,
+    uint16_t* __restrict__ act16 = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3F_BUF + 2 * X3F_RAW];
     __shared__ float red[X3F_WAVES];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -170,6 +174,21 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     for (int i = 1; i < X3F_WAVES; ++i) wm = fmaxf(wm, red[i]);
     const int sw = x3_exp(wm);
     const float wsc = ldexpf(1.f, sw);
+    // data scale: per sample, or (act16) the launch max of the per-sample maxima
+    int sxg = 0;
+    if (act16) {
+        float am = 0.f;
+        for (int i = tid; i < B; i += X3F_THREADS) am = fmaxf(am, amax[i]);
+        am = wave_max(am);
+        __syncthreads();
+        if (lane == 0) red[wave] = am;
+        __syncthreads();
+        am = red[0];
+#pragma unroll
+        for (int i = 1; i < X3F_WAVES; ++i) am = fmaxf(am, red[i]);
+        sxg = x3_exp(am);
+    }
+    auto sexp = [&](int b) { return act16 ? sxg : x3_exp(amax[b]); };
 
     // B fragments: lane (n16, kc) holds W2[co][8kc .. 8kc+7][tap], co = 16nt + n16
     f16x8 wh[X3F_NT][9], wl[X3F_NT][9];
@@ -209,7 +228,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         wo[it] = p * 64 + ((c8 ^ (x & 2)) * 16);
     }
     auto split_unit = [&](int uu, const char* raw, char* buf) {
-        const float sc = ldexpf(1.f, x3_exp(amax[uu / 3]));
+        const float sc = ldexpf(1.f, sexp(uu / 3));
 #pragma unroll
         for (int it = 0; it < X3F_IPT; ++it) {
             float v[8];
@@ -250,10 +269,19 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             }
             // past the last unit this splits a clamped unit's stale raw rows into a buffer nobody reads
             if (mt == 0) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+            if (mt == 1 && act16) {
+                // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
+                char* dst = reinterpret_cast<char*>(act16) + (size_t)u * X3F_BUF;
+#pragma unroll
+                for (int r = 0; r < (X3F_BUF / 16 + X3F_THREADS - 1) / X3F_THREADS; ++r) {
+                    const int i = min(tid + r * X3F_THREADS, X3F_BUF / 16 - 1);
+                    *reinterpret_cast<uint4*>(dst + i * 16) = *reinterpret_cast<const uint4*>(cur + i * 16);
+                }
+            }
         }
         // epilogue: unscale (exact), bias, ReLU, 2x2 max-pool, routing code
         const int b = u / 3, t3 = u - (u / 3) * 3;
-        const float us = ldexpf(1.f, -(x3_exp(amax[b]) + sw));
+        const float us = ldexpf(1.f, -(sexp(b) + sw));
         const int wy = 4 * t3 + wr;
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
@@ -527,9 +555,14 @@ constexpr int X3W_XR = (X3W_XITEMS + X3W_THREADS - 1) / X3W_THREADS;  // 3 (the 
 constexpr int X3W_DYITEMS = 48 * 8;                  // (window, 4-co group) dY items per unit
 static_assert(2 * X3W_BUF <= 163840, "LDS");
 
+// X16 = true: the input image of a unit is the f16 image conv2_fwd_pool_x3 wrote (act16, launch-max
+// scale, chunk slot kc ^ (x & 2), i.e. the 32-B ci-half slot h ^ ((x >> 1) & 1)), moved by LDS-DMA
+// one unit ahead straight into the image buffer: no gather loads, no split VALU.
+template <bool X16>
 __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     const float* __restrict__ act, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
-    const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
+    const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B,
+    const uint16_t* __restrict__ act16 = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3W_BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -640,12 +673,32 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     int abase[2];  // dY: pixel 8c + qq (+4), co tile mi in slot mi ^ (g4 & 1)
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) abase[mi] = (8 * g4 + qq) * 64 + ((mi ^ (g4 & 1)) * 32) + pp * 8;
-    int xbase[6];
+    // input bases per (this wave's K-step j, kx); X16 images keep ci half h in slot h ^ ((x >> 1) & 1)
+    int xbase[3][3];
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-        const int c = 4 * s + g4;
-        xbase[s] = 2 * X3W_DYP + (((c / 3) * A_HW + 8 * (c % 3) + qq) * 64) + (16 * h + 4 * pp) * 2;
-    }
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int c = 4 * (kp + 2 * j) + g4;
+            const int x = 8 * (c % 3) + qq + kx;
+            const int slot = X16 ? (h ^ ((x >> 1) & 1)) : h;
+            xbase[j][kx] = 2 * X3W_DYP + (((c / 3) * A_HW + x) * 64) + slot * 32 + pp * 8;
+        }
+    // X16 staging: 2,080 16-B pieces per unit, lane-contiguous (the image is stored as it sits in LDS)
+    auto issue_x16 = [&](int uu, char* img) {
+        const char* src = reinterpret_cast<const char*>(act16) + (size_t)uu * (2 * X3W_XP);
+        const uint32_t dst = lds_u32(img + 2 * X3W_DYP);
+        const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const int piece = wave_ + 8 * r;  // 1 KiB wave-instructions: 32.5 of them
+            if (piece < (2 * X3W_XP) / 1024) {
+                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
+            } else if (piece == (2 * X3W_XP) / 1024 && lane < 32) {
+                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
+            }
+        }
+    };
     typedef __fp16 hf4 __attribute__((__vector_size__(8)));
     typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) hf4* lp4;
@@ -682,12 +735,11 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
                 Al[slot][mi] = trr(img + X3W_DYP + abase[mi] + s * 2048);
             }
         };
-        auto xb = [&](int j) { return kp ? xbase[1 + 2 * j] : xbase[2 * j]; };
         auto rdB = [&](int n, int slot) {
             const int j = n / NT, tap = T0 + n % NT;
-            const int to = ((tap / 3) * A_HW + tap % 3) * 64;
-            Bh[slot] = trr(img + xb(j) + to);
-            Bl[slot] = trr(img + X3W_XP + xb(j) + to);
+            const int to = (tap / 3) * A_HW * 64;
+            Bh[slot] = trr(img + xbase[j][tap % 3] + to);
+            Bl[slot] = trr(img + X3W_XP + xbase[j][tap % 3] + to);
         };
         rdA(0, 0);
         rdB(0, 0);
@@ -721,16 +773,21 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 
     int u = ks;
     if (u < U) {
-        load_x(u);
+        if constexpr (X16) {
+            issue_x16(u, smem);
+        } else {
+            load_x(u);
+        }
         load_dy(u);
-        split_x(smem);
+        if constexpr (!X16) split_x(smem);
         store_dy(smem);
-        load_x(min(u + nks, U - 1));
+        if constexpr (!X16) load_x(min(u + nks, U - 1));
         load_dy(min(u + nks, U - 1));
     }
     int k = 0;
 #pragma unroll 1
     for (; u < U; u += nks, ++k) {
+        if constexpr (X16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this unit's image DMA landed
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
         const int nx = u + nks, nx2 = u + 2 * nks;
         const char* img = smem + (k & 1) * X3W_BUF;
@@ -738,9 +795,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // unit u+1's rows and dY were requested a whole unit ago. No branch around the staging (past the
         // last unit it re-stages a clamped valid unit nobody reads), so it shares one basic block with
         // the MFMAs and its VALU can fill their issue gaps
-        split_x(nimg);
+        if constexpr (X16) {
+            issue_x16(min(nx, U - 1), nimg);
+        } else {
+            split_x(nimg);
+        }
         store_dy(nimg);
-        load_x(min(nx2, U - 1));
+        if constexpr (!X16) load_x(min(nx2, U - 1));
         load_dy(min(nx2, U - 1));
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
@@ -802,6 +863,17 @@ extern "C" int slk_row_amax(const float* x, int rows, int n, float* amax, void* 
     return slk_launch_status();
 }
 
+extern "C" int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float* W2, const float* b2,
+                                      float* pooled, uint8_t* code, uint16_t* act16, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code && act16);
+    if (B == 0) return 0;
+    const int U = 3 * B;
+    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
+                       slk_stream(stream), act, act_amax, W2, b2, pooled, code, B, act16);
+    return slk_launch_status();
+}
+extern "C" int64_t slk_conv2_act16_bytes(int B) { return B > 0 ? (int64_t)3 * B * X3F_BUF : 0; }
+
 extern "C" int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* W2, const float* b2,
                                      float* pooled, uint8_t* code, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code);
@@ -829,7 +901,17 @@ extern "C" int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const
     SLK_CHECK_ARG(B >= 0 && act && act_amax && dpooled && dp_amax && code && slabs);
     if (B == 0) return 0;
     const int nks = slk_conv2_wgrad_x3_nslab(B);
-    hipLaunchKernelGGL(conv2_wgrad_x3_kernel, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), act, act_amax,
-                       dpooled, dp_amax, code, slabs, B);
+    hipLaunchKernelGGL(conv2_wgrad_x3_kernel<false>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), act,
+                       act_amax, dpooled, dp_amax, code, slabs, B, nullptr);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled,
+                                   const float* dp_amax, const uint8_t* code, float* slabs, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act16 && act_amax && dpooled && dp_amax && code && slabs);
+    if (B == 0) return 0;
+    const int nks = slk_conv2_wgrad_x3_nslab(B);
+    hipLaunchKernelGGL(conv2_wgrad_x3_kernel<true>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), nullptr,
+                       act_amax, dpooled, dp_amax, code, slabs, B, act16);
     return slk_launch_status();
 }

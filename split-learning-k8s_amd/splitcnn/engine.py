@@ -233,6 +233,7 @@ class ServerStage:
         self.device = torch.device(device)
         self.conv = conv
         self.impl_fwd, self.impl_dgrad, self.impl_wgrad = CONV_PRESETS[conv]
+        self.share_images = True  # x3: the forward's split input images feed the wgrad (act16)
         self.model = (model if model is not None else ModelPartB()).to(self.device)
         self.lr = lr
         m = self.model
@@ -269,10 +270,13 @@ class ServerStage:
             with TIMER("act_amax"):
                 act_amax = ops.row_amax(act, out=self._b("act_amax", (B,)))
         dp_amax = self._b("dp_amax", (B,)) if "x3" in (di, wi) else None
+        # x3 forward + x3 wgrad: the forward hands its split input images to the wgrad (LDS-DMA copy)
+        act16 = (self._b("act16", (ops.conv2_act16_bytes(B),), torch.uint8)
+                 if fi == "x3" and wi == "x3" and self.share_images else None)
         with TIMER("conv2_fwd_pool"):
             pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
                                               code=self._b("code", (B, 64, 12, 12), torch.uint8), impl=fi,
-                                              act_amax=act_amax)
+                                              act_amax=act_amax, act16=act16)
         with TIMER("fc_xent"):
             _, loss_i, dlogits, dpooled = ops.fc_xent(
                 pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
@@ -285,7 +289,7 @@ class ServerStage:
         with TIMER("conv2_wgrad"):
             s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
                                        slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
-                                       impl=wi, act_amax=act_amax, dp_amax=dp_amax)
+                                       impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
         with TIMER("fc_wgrad"):
             s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3

@@ -112,10 +112,21 @@ def _impl(direct, impl):
     return impl
 
 
-def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None):
+def conv2_act16_bytes(B: int) -> int:
+    """Bytes of the f16 input images conv2_fwd_pool(impl='x3', act16=...) writes for the x3 wgrad."""
+    return _lib.query("slk_conv2_act16_bytes", B)
+
+
+def _act16(t, B):
+    _dev(t, "act16", (conv2_act16_bytes(B),), torch.uint8)
+    return t.data_ptr()
+
+
+def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None, act16=None):
     """impl: 'wino' (Winograd F(2x2,3x3) on the f32 MFMA, default), 'direct' (direct f32 MFMA kernel,
     cross-check; also direct=True) or 'x3' (direct on the f16 MFMA with split operands; act_amax =
-    per-sample max |act|, computed here when not given)."""
+    per-sample max |act|, computed here when not given). act16 (x3 only, a uint8 tensor of
+    conv2_act16_bytes(B)): also write the split input images for conv2_wgrad_slabs(act16=...)."""
     impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
     pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
@@ -123,6 +134,11 @@ def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None,
     if impl == "x3":
         if act_amax is None:
             act_amax = row_amax(act)
+        if act16 is not None:
+            _lib.call("slk_conv2_fwd_pool_x3s", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)),
+                      _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
+                      _dev(code, "code", dtype=torch.uint8), _act16(act16, B), B, _stream(act))
+            return pooled, code
         _lib.call("slk_conv2_fwd_pool_x3", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)),
                   _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
                   _dev(code, "code", dtype=torch.uint8), B, _stream(act))
@@ -234,7 +250,10 @@ def conv2_wgrad_nslab(B: int, direct: bool = False, impl=None) -> int:
                        "x3": "slk_conv2_wgrad_x3_nslab"}[impl], B)
 
 
-def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False, impl=None, act_amax=None, dp_amax=None):
+def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False, impl=None, act_amax=None, dp_amax=None,
+                      act16=None):
+    """act16 (x3 only): the forward's split input images (conv2_fwd_pool(..., act16=...), same act and
+    act_amax) — the kernel then moves them by LDS-DMA instead of loading and splitting act."""
     impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
     if _dpooled_batch(dpooled) != B:
@@ -243,6 +262,11 @@ def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False, impl=None, a
     if impl == "x3":
         act_amax = row_amax(act) if act_amax is None else act_amax
         dp_amax = row_amax(dpooled) if dp_amax is None else dp_amax
+        if act16 is not None:
+            _lib.call("slk_conv2_wgrad_x3s", _act16(act16, B), _dev(act_amax, "act_amax", (B,)),
+                      _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
+                      _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(act))
+            return slabs
         _lib.call("slk_conv2_wgrad_x3", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)), _dev(dpooled, "dpooled"),
                   _dev(dp_amax, "dp_amax", (B,)), _dev(code, "code", (B, 64, 12, 12), torch.uint8),
                   _dev(slabs, "slabs"), B, _stream(act))

@@ -13,7 +13,7 @@ from conftest import ROOT, load_fixture
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "slk.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+char\*|int)\s+(slk_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\*|int64_t|int)\s+(slk_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():

@@ -192,3 +192,25 @@ def test_trainer_conv_presets_match_fixture(gpu, conv):
         tr.step(torch.from_numpy(fx["x_1"]).to(gpu), torch.from_numpy(fx["y_1"]).to(gpu))
         for k in PARAMS:
             assert weight_ok(param_of(tr.client, tr.server, k), fx[f"post_{k}_1"], fx[f"init_{k}"]), (name, k)
+
+
+@pytest.mark.parametrize("B", [1, 7, 300])
+def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
+    """The forward's split input images (act16) fed to the wgrad by LDS-DMA give the same slabs bit for
+    bit as the wgrad that loads and splits act itself (same launch scale, same f16 values); the
+    forward in that mode (launch scale) still meets the oracle bar."""
+    from oracle.split_step import conv3x3, relu, tie_discrepancies
+    from splitcnn import ops
+    act, p, y = _inputs(gpu, B, seed=B + 300)
+    am = ops.row_amax(act)
+    a16 = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu)
+    ps, cs = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=am, act16=a16)
+    _, _, _, dp = ops.fc_xent(ps, p["W3"], p["b3"], y, 1.0 / B)
+    s1 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am)
+    s2 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am, act16=a16)
+    assert torch.equal(s1, s2)
+    r = relu(conv3x3(act.double().cpu().numpy(), p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    n, ok = tie_discrepancies(r, cw.cpu().numpy().astype(np.int64), cs.cpu().numpy().astype(np.int64))
+    assert ok, n
+    assert rel_err(ps.cpu().numpy(), r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))) <= 1e-5

@@ -36,6 +36,11 @@ def main():
             po, co = torch.empty_like(pooled), torch.empty_like(code)
             cases[f"fwd_{impl}"] = (lambda impl=impl, po=po, co=co: ops.conv2_fwd_pool(
                 act, W2, b2, po, co, impl=impl, act_amax=amax))
+        if "fwd" in args.ops and impl == "x3":
+            a16 = torch.empty(ops.conv2_act16_bytes(args.B), dtype=torch.uint8, device=dev)
+            po, co = torch.empty_like(pooled), torch.empty_like(code)
+            cases["fwd_x3s"] = (lambda po=po, co=co, a16=a16: ops.conv2_fwd_pool(
+                act, W2, b2, po, co, impl="x3", act_amax=amax, act16=a16))
     if "dgrad" in args.ops:
         for impl in ("wino", "direct", "x3"):
             g = torch.empty_like(act)
@@ -44,6 +49,11 @@ def main():
         for impl in ("wino", "x3"):
             sl = torch.empty(ops.conv2_wgrad_nslab(args.B, impl=impl), ops.CONV2_SLAB, device=dev)
             cases[f"wgrad_{impl}"] = (lambda impl=impl, sl=sl: ops.conv2_wgrad_slabs(act, dp, code, sl, impl=impl, act_amax=amax, dp_amax=dpa))
+    if "wgrad" in args.ops:
+        a16 = torch.empty(ops.conv2_act16_bytes(args.B), dtype=torch.uint8, device=dev)
+        ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amax, act16=a16)
+        sl = torch.empty(ops.conv2_wgrad_nslab(args.B, impl="x3"), ops.CONV2_SLAB, device=dev)
+        cases["wgrad_x3s"] = (lambda sl=sl, a16=a16: ops.conv2_wgrad_slabs(act, dp, code, sl, impl="x3", act_amax=amax, dp_amax=dpa, act16=a16))
     cases["row_amax"] = lambda: ops.row_amax(act, amax)
     times = {k: [] for k in cases}
     for _ in range(3):
