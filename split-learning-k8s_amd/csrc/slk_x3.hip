@@ -23,6 +23,13 @@ using namespace slk;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef SLK_X3ABL
+#define SLK_X3ABL 0  // profiling-only ablation bits (wrong results): see the dgrad kernel
+#endif
+#ifndef SLK_X3D_STG
+#define SLK_X3D_STG 0
+#endif
+
 namespace {
 
 // s such that amax * 2^s < 2^14 (amax in [2^13, 2^14) after scaling); 0 for zero / non-finite amax.
@@ -383,37 +390,49 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 
     // expansion items of a unit: i = tid + 512 r -> 4-co group c4 = i & 7, window wi = i >> 3 (row-major
     // over the part's image window rows); rows outside 0..11 expand to zeros
-    float dv[2][4];
-    uint32_t dcw[2];
+    // SLK_X3D_STG = 1: only waves 4-7 stage (3 items each), waves 0-3 run MFMAs only
+    constexpr int STG = SLK_X3D_STG;
+    constexpr int NR = STG ? 3 : 2, SSTR = STG ? 256 : X3D_THREADS;
+    static_assert(NR * SSTR >= X3D_ITEMS_MAX, "staging items");
+    const int stid = STG ? tid - 256 : tid;
+    float dv[NR][4];
+    uint32_t dcb[NR][4];
+    float ld_amax = 0.f;
     auto load_dy = [&](int uu) {
+        if (STG && wave < 4) return;
         const int b = uu / 6, rr = uu - (uu / 6) * 6, pt = rr >> 1, h = rr & 1;
+        ld_amax = amax[b];  // used by the store_dy of this unit (one unit later)
         const int wr0 = x3d_ybase(pt) / 2, nwr = x3d_nwr(pt);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int i = tid + r * X3D_THREADS;
+        for (int r = 0; r < NR; ++r) {
+            const int i = stid + r * SSTR;
             const int c4 = i & 7, wi = i >> 3;
             const int wr = wr0 + wi / P_HW, wx = wi - (wi / P_HW) * P_HW;
-            dcw[r] = 0x04040404u;  // CODE_NONE: routes nothing
 #pragma unroll
-            for (int j = 0; j < 4; ++j) dv[r][j] = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                dv[r][j] = 0.f;
+                dcb[r][j] = CODE_NONE;  // routes nothing
+            }
             if (i < nwr * P_HW * 8 && wr >= 0 && wr < P_HW) {
                 const size_t o = (size_t)b * P_SAMPLE + (32 * h + 4 * c4) * P_WIN + wr * P_HW + wx;
-                dcw[r] = 0;
+                // code bytes stay one per register until store_dy: combining them here made the
+                // compiler wait for the loads on the spot (a full memory latency per unit)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     dv[r][j] = dpooled[o + j * P_WIN];
-                    dcw[r] |= (uint32_t)code[o + j * P_WIN] << (8 * j);
+                    dcb[r][j] = code[o + j * P_WIN];
                 }
             }
         }
     };
     auto store_dy = [&](int uu, char* img) {
-        const int b = uu / 6, pt = (uu - (uu / 6) * 6) >> 1;
+        if (STG && wave < 4) return;
+        const int pt = (uu - (uu / 6) * 6) >> 1;
         const int nwr = x3d_nwr(pt);
-        const float sc = ldexpf(1.f, x3_exp(amax[b]));
+        const float sc = ldexpf(1.f, x3_exp(ld_amax));
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int i = tid + r * X3D_THREADS;
+        for (int r = 0; r < NR; ++r) {
+            const int i = stid + r * SSTR;
             if (r == 0 || i < nwr * P_HW * 8) {
                 const int c4 = i & 7, wi = i >> 3;
                 const int wrl = wi / P_HW, wx = wi - (wi / P_HW) * P_HW;
@@ -426,7 +445,8 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
                     lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
                 }
-                const uint32_t cA = __builtin_amdgcn_perm(0u, dcw[r], 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw[r], 0x03030202u);
+                const uint32_t dcw = dcb[r][0] | (dcb[r][1] << 8) | (dcb[r][2] << 16) | (dcb[r][3] << 24);
+                const uint32_t cA = __builtin_amdgcn_perm(0u, dcw, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw, 0x03030202u);
                 char* rec = img + (2 + (2 * wrl) * A_HW + 2 * wx) * X3D_REC + c4 * 8;
 #pragma unroll
                 for (int pos = 0; pos < 4; ++pos) {
@@ -459,6 +479,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     for (; pr < P; pr += G) {
         const int b = pr / 3, pt = pr - (pr / 3) * 3;
         const int T0 = x3d_t0(pt), T1 = pt == 2 ? X3D_MT : x3d_t0(pt + 1);
+        const float amax_b = amax[b];  // for the epilogue, loaded early
         const int cbase = (2 - A_HW * x3d_ybase(pt) - 54) * X3D_REC;
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -473,10 +494,24 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // read pair per 3 dependent MFMAs: waiting on each read left the SIMD half idle)
             const char* abw = img + cbase + ((T0 + g) * 16 + n16) * X3D_REC + kc * 16;
             auto rd = [&](int i, int tap, f16x8& fh, f16x8& fl) {
+                if (SLK_X3ABL & 2) {  // operands from registers (timing only)
+                    fh = wh[1][tap];
+                    fl = wl[1][(tap + i) % 9];
+                    return;
+                }
                 const char* ab = abw + i * 64 * X3D_REC + (54 - 26 * (tap / 3) - tap % 3) * X3D_REC;
                 fh = *reinterpret_cast<const f16x8*>(ab);
                 fl = *reinterpret_cast<const f16x8*>(ab + 64);
             };
+            // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused).
+            // Half the waves stage before their MFMAs, half after, so the two waves of a SIMD overlap
+            // one's staging with the other's MFMAs (both staging at once left the SIMD's MFMA idle).
+            const bool sfirst = (SLK_X3ABL & 8) ? (wave & 1) : ((SLK_X3ABL & 16) ? false : wave >= 4);
+            // (SLK_X3D_STG: store_dy/load_dy return at once on waves 0-3)
+            if (!(SLK_X3ABL & 1) && sfirst) {
+                store_dy(unx, nimg);
+                load_dy(unx2);
+            }
             f16x8 fh[4], fl[4];
             constexpr int NS = 27;  // tiles 0..2 exist for every wave and part
 #pragma unroll
@@ -494,10 +529,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
                 if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
-            // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused)
-            store_dy(unx, nimg);
-            load_dy(unx2);
-            if (T0 + g + 12 < T1) {
+            if (!(SLK_X3ABL & 1) && !sfirst) {
+                store_dy(unx, nimg);
+                load_dy(unx2);
+            }
+            if (!(SLK_X3ABL & 4) && T0 + g + 12 < T1) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) rd(3, q, fh[q], fl[q]);
 #pragma unroll
@@ -514,7 +550,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             }
         }
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
-        const float us = ldexpf(1.f, -(x3_exp(amax[b]) + sw));
+        const float us = ldexpf(1.f, -(x3_exp(amax_b) + sw));
         float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) {
