@@ -668,16 +668,15 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     const int ditem = min(tid, X3W_DYITEMS - 1);
     const int dg = ditem & 7, dw = ditem >> 3;
     float dv[4];
-    uint32_t dc = 0;
+    uint32_t dcb[4];  // code bytes one per register until store_dy (combining here waits for the loads)
     auto load_dy = [&](int uu) {
         const int b = uu / 3, t3 = uu - (uu / 3) * 3;
         const int w = (4 * t3 + dw / 12) * P_HW + dw % 12;
         const size_t o = (size_t)b * P_SAMPLE + (32 * cohalf + 4 * dg) * P_WIN + w;
-        dc = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             dv[j] = dpooled[o + j * P_WIN];
-            dc |= (uint32_t)code[o + j * P_WIN] << (8 * j);
+            dcb[j] = code[o + j * P_WIN];
         }
     };
     auto store_dy = [&](char* img) {
@@ -690,6 +689,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
             lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
         }
+        const uint32_t dc = dcb[0] | (dcb[1] << 8) | (dcb[2] << 16) | (dcb[3] << 24);
         const uint32_t cA = __builtin_amdgcn_perm(0u, dc, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dc, 0x03030202u);
         const int wy = dw / 12, wx = dw % 12;
 #pragma unroll
@@ -823,7 +823,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     int k = 0;
 #pragma unroll 1
     for (; u < U; u += nks, ++k) {
-        if constexpr (X16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this unit's image DMA landed
+        // X16: this unit's image DMA landed; the 8 dY loads of load_dy, every wave's last memory
+        // instructions (issued after its DMA), may stay in flight
+        const bool dfirst = !X16 || (SLK_X3ABL & 64) || tg == 1;
+        if constexpr (X16) {
+            if (SLK_X3ABL & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
         const int nx = u + nks, nx2 = u + 2 * nks;
         const char* img = smem + (k & 1) * X3W_BUF;
@@ -831,16 +837,26 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // unit u+1's rows and dY were requested a whole unit ago. No branch around the staging (past the
         // last unit it re-stages a clamped valid unit nobody reads), so it shares one basic block with
         // the MFMAs and its VALU can fill their issue gaps
+        // X16: the tap-group-1 waves (the lighter MFMA share) route dY before their MFMAs, the tap-group-0
+        // waves after theirs, so the two waves of a SIMD overlap routing with MFMAs. store_dy goes before
+        // the DMA issue: the compiler does not count the asm DMAs, so its wait for the dY registers
+        // would otherwise also wait for the DMA just issued
+        if (!(SLK_X3ABL & 32) && dfirst) store_dy(nimg);
         if constexpr (X16) {
             issue_x16(min(nx, U - 1), nimg);
         } else {
             split_x(nimg);
         }
-        store_dy(nimg);
-        if constexpr (!X16) load_x(min(nx2, U - 1));
-        load_dy(min(nx2, U - 1));
+        if (!(SLK_X3ABL & 32) && dfirst) {
+            if constexpr (!X16) load_x(min(nx2, U - 1));
+            load_dy(min(nx2, U - 1));
+        }
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
+        if (!(SLK_X3ABL & 32) && !dfirst) {
+            store_dy(nimg);
+            load_dy(min(nx2, U - 1));
+        }
     }
     __syncthreads();
     // K parities: kp = 1 waves hand their sums to kp = 0 through LDS (region per (h, tg))
