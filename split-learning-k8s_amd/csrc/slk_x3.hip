@@ -253,6 +253,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     __syncthreads();
     if (u < U) split_unit(u, raw0, smem);
     int k = 0;
+    const int sph = (SLK_X3ABL & 512) ? 7 : (SLK_X3ABL & 256) ? 0 : (wave >= 4 ? 0 : ((SLK_X3ABL & 1024) ? 2 : 1));
 #pragma unroll 1
     for (; u < U; u += G, ++k) {
         const int cb = k & 1;
@@ -274,9 +275,11 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 #pragma unroll
                 for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = mfma_x3(ah, al, wh[nt][tap], wl[nt][tap], acc[mt][nt]);
             }
-            // past the last unit this splits a clamped unit's stale raw rows into a buffer nobody reads
-            if (mt == 0) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
-            if (mt == 1 && act16) {
+            // staging after M tile 0 on waves 4-7 and after M tile 1 on waves 0-3 (waves w and w + 4
+            // share a SIMD; measured: 0/1 beats 0/0 and 0/2). Past the last unit this splits a clamped
+            // unit's stale raw rows into a buffer nobody reads
+            if (mt == sph) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+            if (mt == sph && act16) {
                 // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
                 char* dst = reinterpret_cast<char*>(act16) + (size_t)u * X3F_BUF;
 #pragma unroll

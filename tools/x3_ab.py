@@ -1,0 +1,79 @@
+"""Profiling only: the x3 conv2 kernels of several libslk builds (tools/build_variant.sh outputs) timed
+side by side in ONE process, interleaved rounds, HIP events on one stream, B = 4096, real activations.
+usage: python tools/x3_ab.py lib0.so lib1.so ... [--rounds 30] [--ops fwd,dgrad,wgrad]"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "split-learning-k8s_amd"), ROOT]
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=30)
+    ap.add_argument("--B", type=int, default=4096)
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    args = ap.parse_args()
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage
+    B = args.B
+    dev = torch.device("cuda:0")
+    a, b = init_models(seed=1)
+    x, y = SyntheticMNIST(2).batch(B)
+    act = ClientStage(a, device=dev).forward(x.to(dev)).clone()
+    W2, b2 = b.conv2.weight.detach().to(dev).contiguous(), b.conv2.bias.detach().to(dev).contiguous()
+    W3, b3 = b.fc1.weight.detach().to(dev).contiguous(), b.fc1.bias.detach().to(dev).contiguous()
+    amax = ops.row_amax(act)
+    pooled, code = ops.conv2_fwd_pool(act, W2, b2)
+    _, _, _, dp = ops.fc_xent(pooled, W3, b3, y.to(dev), 1.0 / B)
+    dpa = ops.row_amax(dp)
+    a16 = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=dev)
+    ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amax, act16=a16)
+    P = ctypes.c_void_p
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    cases = {}
+    for li, path in enumerate(args.libs):
+        L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_DEEPBIND)  # own symbols first
+        for n in ("slk_conv2_fwd_pool_x3s", "slk_conv2_dgrad_x3", "slk_conv2_wgrad_x3s", "slk_conv2_wgrad_x3_nslab"):
+            getattr(L, n).restype = ctypes.c_int
+        tag = os.path.basename(path).replace(".so", "")
+        if "fwd" in args.ops:
+            po, co, a16o = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16)
+            L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
+            cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
+                p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+        if "dgrad" in args.ops:
+            g = torch.empty_like(act)
+            L.slk_conv2_dgrad_x3.argtypes = [P] * 5 + [ctypes.c_int, P]
+            cases[f"dgrad {tag}"] = (lambda L=L, g=g: L.slk_conv2_dgrad_x3(p(dp), p(dpa), p(code), p(W2), p(g), B, st))
+        if "wgrad" in args.ops:
+            sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
+            L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
+            cases[f"wgrad {tag}"] = (lambda L=L, sl=sl: L.slk_conv2_wgrad_x3s(p(a16), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
+    times = {k: [] for k in cases}
+    for _ in range(3):
+        for f in cases.values():
+            assert f() == 0
+    torch.cuda.synchronize()
+    for _ in range(args.rounds):
+        for k, f in cases.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            f()
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1))
+    for k, v in sorted(times.items()):
+        v.sort()
+        print(f"{k:24s} median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
