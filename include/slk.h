@@ -164,15 +164,25 @@ int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t
 int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
                        const uint8_t* code, float* slabs, int B, void* stream);
 int slk_conv2_wgrad_x3_nslab(int B);
-/* The forward that also writes its split f16 input images (act16, slk_conv2_act16_bytes(B) bytes; data
- * scale = the launch max of act_amax) and the wgrad that moves them by LDS-DMA instead of loading and
+/* The forward that also writes its split f16 input images (act16, slk_conv2_act16_bytes(B) bytes; each
+ * sample at its own scale from act_amax) and the wgrad that moves them by LDS-DMA instead of loading and
  * splitting act: the wgrad's input staging becomes a copy. Same results as slk_conv2_wgrad_x3 (bitwise:
- * the same scale, the same f16 values). */
+ * the same scales, the same f16 values). */
 int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float* W2, const float* b2, float* pooled,
                            uint8_t* code, uint16_t* act16, int B, void* stream);
 int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled, const float* dp_amax,
                         const uint8_t* code, float* slabs, int B, void* stream);
 int64_t slk_conv2_act16_bytes(int B);
+
+/* The client's conv1 + ReLU (replaces slk_conv1_fwd_amax inside a fused step, src/client_part.py:114)
+ * writing the x3 server operand directly: act_amax and the act16 images (bit-identical to those
+ * slk_conv2_fwd_pool_x3s writes), plus the f32 act when act != NULL. The server forward then reads the
+ * images (slk_conv2_fwd_pool_x3i: same pooled / code as slk_conv2_fwd_pool_x3 on the f32 act, bitwise)
+ * and so does the wgrad (slk_conv2_wgrad_x3s). */
+int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1, float* act, float* act_amax, uint16_t* act16,
+                     int B, void* stream);
+int slk_conv2_fwd_pool_x3i(const uint16_t* act16, const float* act_amax, const float* W2, const float* b2,
+                           float* pooled, uint8_t* code, int B, void* stream);
 
 /* ---------------------------------------------------------------- reductions / optimizer */
 

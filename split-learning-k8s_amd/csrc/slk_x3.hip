@@ -141,13 +141,16 @@ __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave
     }
 }
 
-// act16 (optional): every unit's f16 image (h plane | l plane, 33,280 B, the layout above) is also
-// written to act16 + u * 33,280 for conv2_wgrad_x3's input operand; the data scale is then the launch
-// max of act_amax (a wgrad K sum spans samples) instead of the per-sample one.
+// act16 (optional): every unit's f16 image (h plane | l plane, 33,280 B, the layout above, the
+// sample's own scale) is also written to act16 + u * 33,280 for conv2_wgrad_x3's input operand.
+// IN16 = true: the input IS such an image array (slk_conv1_fwd_x3 wrote it): each unit's image is moved
+// by LDS-DMA two units ahead into a 3-deep ring of f16 buffers — no f32 rows, no split.
+template <bool IN16>
 __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     const float* __restrict__ act, const float* __restrict__ amax, const float* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ pooled, uint8_t* __restrict__ code, int B,
     uint16_t* __restrict__ act16 = nullptr) {
+    static_assert(3 * X3F_BUF <= 2 * X3F_BUF + 2 * X3F_RAW, "IN16 ring fits");
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3F_BUF + 2 * X3F_RAW];
     __shared__ float red[X3F_WAVES];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -167,8 +170,27 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         const int c = g / 65, r = g - (g / 65) * 65;
         voff[k] = (uint32_t)(c * A_PIX * 4 + r * 16);
     }
-    if (u < U) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
-    if (u + G < U) x3f_issue_raw(act, u + G, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
+    // IN16: unit uu's image (33,280 contiguous bytes) -> ring slot; 32.5 1-KiB wave-instructions
+    auto issue_img = [&](int uu, char* dstp) {
+        const char* src = reinterpret_cast<const char*>(act16) + (size_t)uu * X3F_BUF;
+        const uint32_t dst = lds_u32(dstp);
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const int piece = wave + X3F_WAVES * r;
+            if (piece < X3F_BUF / 1024) {
+                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
+            } else if (piece == X3F_BUF / 1024 && lane < 32) {
+                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
+            }
+        }
+    };
+    if constexpr (IN16) {
+        if (u < U) issue_img(u, smem);
+        if (u + G < U) issue_img(u + G, smem + X3F_BUF);
+    } else {
+        if (u < U) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
+        if (u + G < U) x3f_issue_raw(act, u + G, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
+    }
 
     // weight scale: max |W2| over the whole tensor
     float wm = 0.f;
@@ -181,21 +203,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     for (int i = 1; i < X3F_WAVES; ++i) wm = fmaxf(wm, red[i]);
     const int sw = x3_exp(wm);
     const float wsc = ldexpf(1.f, sw);
-    // data scale: per sample, or (act16) the launch max of the per-sample maxima
-    int sxg = 0;
-    if (act16) {
-        float am = 0.f;
-        for (int i = tid; i < B; i += X3F_THREADS) am = fmaxf(am, amax[i]);
-        am = wave_max(am);
-        __syncthreads();
-        if (lane == 0) red[wave] = am;
-        __syncthreads();
-        am = red[0];
-#pragma unroll
-        for (int i = 1; i < X3F_WAVES; ++i) am = fmaxf(am, red[i]);
-        sxg = x3_exp(am);
-    }
-    auto sexp = [&](int b) { return act16 ? sxg : x3_exp(amax[b]); };
+    // data scale: per sample
+    auto sexp = [&](int b) { return x3_exp(amax[b]); };
 
     // B fragments: lane (n16, kc) holds W2[co][8kc .. 8kc+7][tap], co = 16nt + n16
     f16x8 wh[X3F_NT][9], wl[X3F_NT][9];
@@ -248,20 +257,28 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         }
     };
 
-    // prologue: unit u's raw rows landed -> split into f16 buffer 0
+    // prologue: unit u's raw rows landed -> split into f16 buffer 0 (IN16: its image is there)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (u < U) split_unit(u, raw0, smem);
+    if (!IN16 && u < U) split_unit(u, raw0, smem);
     int k = 0;
     const int sph = (SLK_X3ABL & 512) ? 7 : (SLK_X3ABL & 256) ? 0 : (wave >= 4 ? 0 : ((SLK_X3ABL & 1024) ? 2 : 1));
 #pragma unroll 1
     for (; u < U; u += G, ++k) {
         const int cb = k & 1;
         // unit u+G's raw rows (issued one unit ago) have landed; the previous epilogue's stores may stay
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES) : "memory");
+        // IN16: unit u's image (issued two units ago) has landed; unit u+G's DMA (at most 5 wave-
+        // instructions, issued one unit ago) and the previous epilogue's stores may stay in flight
+        if constexpr (IN16) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES + 4) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES) : "memory");
         __syncthreads();
-        if (u + 2 * G < U) x3f_issue_raw(act, u + 2 * G, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
-        const char* cur = smem + cb * X3F_BUF;
+        const int kr = k % 3;  // IN16 ring slot of unit u
+        if constexpr (IN16) {
+            if (u + 2 * G < U) issue_img(u + 2 * G, smem + (kr == 0 ? 2 : kr - 1) * X3F_BUF);
+        } else {
+            if (u + 2 * G < U) x3f_issue_raw(act, u + 2 * G, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
+        }
+        const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
         f32x4 acc[3][X3F_NT];
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
@@ -278,8 +295,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             // staging after M tile 0 on waves 4-7 and after M tile 1 on waves 0-3 (waves w and w + 4
             // share a SIMD; measured: 0/1 beats 0/0 and 0/2). Past the last unit this splits a clamped
             // unit's stale raw rows into a buffer nobody reads
-            if (mt == sph) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
-            if (mt == sph && act16) {
+            if (!IN16 && mt == sph) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+            if (!IN16 && mt == sph && act16) {
                 // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
                 char* dst = reinterpret_cast<char*>(act16) + (size_t)u * X3F_BUF;
 #pragma unroll
@@ -575,14 +592,17 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 // per-(K-step, lane) base + an immediate. dY pixel rows keep the two 32-B co tiles swapped on odd
 // 8-pixel groups (the two 16-lane groups of a half-wave then hit disjoint banks).
 // A workgroup owns one co half (M = 32) and a K share (units ks, ks + nks, ...); the two co halves
-// of a share run on different workgroups, each splitting the same input rows. Scales are per LAUNCH
-// (the max of the per-sample amax arrays): a K sum spans samples. Staging is register-based and two
+// of a share run on different workgroups, each splitting the same input rows. A K sum spans samples,
+// so every product must carry ONE scale: the input keeps its sample's 2^s_b (the act16 images' scale)
+// and the sample's dY takes 2^(sd + sx - s_b) (sx, sd: the launch scales from the maxima of the
+// per-sample amax arrays; s_b >= sx, so dY never exceeds its launch range). Staging is register-based and two
 // units ahead: unit u+2's input (8 channels of a pixel per item, channel group fastest across lanes so
 // the ds_write_b128 of 8 lanes cover 128 distinct bytes) and pooled gradient + codes are loaded at the
 // top of unit u and split / routed into the other image at the top of unit u+1.
 // 8 waves: wave = (ci half h, K-step parity kp, tap group tg) over BOTH M tiles, so each input fragment
-// read feeds 6 MFMAs; tap group 1 (4 taps) also carries db via one MFMA per M tile against a ones
-// fragment (h = 0: dY_hi, h = 1: dY_lo); parities are summed through LDS at the end.
+// read feeds 6 MFMAs; parities are summed through LDS at the end. db is summed in f32 from the pooled
+// gradients as they are staged (the dY images carry per-sample scales, so a ones-fragment MFMA would
+// mix them).
 constexpr int X3W_THREADS = 512;
 constexpr int X3W_Q = 192;                           // output pixels (K) per unit
 constexpr int X3W_DYP = X3W_Q * 64;                  // 12,288 B per dY plane (32 co)
@@ -637,8 +657,10 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         md = fmaxf(md, red[8 + i]);
     }
     __syncthreads();
+    // the input operand carries its SAMPLE's scale 2^s_b (as the act16 images do); its dY is scaled by
+    // 2^(sd + sx - s_b) (<= 2^sd: s_b >= sx), so every product carries 2^(sx + sd)
     const int sx = x3_exp(ma), sd = x3_exp(md);
-    const float xsc = ldexpf(1.f, sx), dsc = ldexpf(1.f, sd);
+    int sb_ld = 0;  // s_b of the unit load_dy last requested (its store_dy / split_x come one unit later)
 
     // input items: i = tid + 512 r -> channel group cg = i & 3, pixel p = i >> 2 of the unit's 260
     float xv[X3W_XR][8];
@@ -655,6 +677,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
     };
     auto split_x = [&](char* img) {
+        const float xsc = ldexpf(1.f, sb_ld);
 #pragma unroll
         for (int r = 0; r < X3W_XR; ++r) {
             const int i = min(tid + r * X3W_THREADS, X3W_XITEMS - 1);
@@ -681,8 +704,16 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             dv[j] = dpooled[o + j * P_WIN];
             dcb[j] = code[o + j * P_WIN];
         }
+        sb_ld = x3_exp(act_amax[b]);
     };
-    auto store_dy = [&](char* img) {
+    // db[co] = sum of the routed dY = the pooled gradients whose code routes them (code != NONE): summed
+    // in f32 from the raw values as they are staged (a thread keeps one (4-co group, window) item)
+    float dbacc[4] = {0.f, 0.f, 0.f, 0.f};
+    auto store_dy = [&](char* img, bool real) {
+        const float dsc = ldexpf(1.f, sd + sx - sb_ld);
+        const bool mine = real && tid < X3W_DYITEMS;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dbacc[j] = (mine && dcb[j] != (uint32_t)CODE_NONE) ? dbacc[j] + dv[j] : dbacc[j];
         uint32_t hv[2], lv[2];
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
@@ -746,8 +777,6 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         const f16x4 hi = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)(p + 4 * 64)));
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
-    const _Float16 one = (_Float16)1.0f;
-    const f16x8 ones = {one, one, one, one, one, one, one, one};
 
     // wave = (ci half h, K-step parity kp, tap group tg: taps 0-4 or 5-8 + db); waves w and w + 4 share
     // a SIMD, so every SIMD carries one wave of each tap group
@@ -756,14 +785,12 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
     // a unit's work for this wave: K-steps kp, kp + 2, kp + 4 x its taps; B fragments (4 transposed reads)
     // run 2 steps ahead through a 3-slot ring, A fragments (8 reads) one K-step ahead; the
     // sched_group_barriers keep that order (hipcc otherwise sinks every read next to its MFMAs)
     auto unit_mfma = [&](const char* img, auto TG) {
         constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
-        constexpr bool DB = decltype(TG)::value == 1;
         constexpr int N = 3 * NT;
         f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
         auto rdA = [&](int j, int slot) {
@@ -793,16 +820,11 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
                 acc[mi][t] = mfma_x3(Ah[j & 1][mi], Al[j & 1][mi], Bh[n % 3], Bl[n % 3], acc[mi][t]);
-            if (DB && t == NT - 1) {
-#pragma unroll
-                for (int mi = 0; mi < 2; ++mi) accb[mi] = mfma_f16(h ? Al[j & 1][mi] : Ah[j & 1][mi], ones, accb[mi]);
-            }
         }
         __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
         for (int n = 0; n < N; ++n) {
-            if (DB && n % NT == NT - 1) __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-            else __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
             if (n + 2 < N) {
                 if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
                 else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -819,7 +841,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
         load_dy(u);
         if constexpr (!X16) split_x(smem);
-        store_dy(smem);
+        store_dy(smem, true);
         if constexpr (!X16) load_x(min(u + nks, U - 1));
         load_dy(min(u + nks, U - 1));
     }
@@ -844,7 +866,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // waves after theirs, so the two waves of a SIMD overlap routing with MFMAs. store_dy goes before
         // the DMA issue: the compiler does not count the asm DMAs, so its wait for the dY registers
         // would otherwise also wait for the DMA just issued
-        if (!(SLK_X3ABL & 32) && dfirst) store_dy(nimg);
+        if (!(SLK_X3ABL & 32) && dfirst) store_dy(nimg, nx < U);
         if constexpr (X16) {
             issue_x16(min(nx, U - 1), nimg);
         } else {
@@ -857,13 +879,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
         if (!(SLK_X3ABL & 32) && !dfirst) {
-            store_dy(nimg);
+            store_dy(nimg, nx < U);
             load_dy(min(nx2, U - 1));
         }
     }
     __syncthreads();
     // K parities: kp = 1 waves hand their sums to kp = 0 through LDS (region per (h, tg))
-    constexpr int XN = 2 * 5 * 4 + 8;  // floats per lane
+    constexpr int XN = 2 * 5 * 4;  // floats per lane
     float* xch = reinterpret_cast<float*>(smem) + (h + 2 * tg) * (XN * 64);
     if (kp == 1) {
 #pragma unroll
@@ -872,21 +894,22 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             for (int t = 0; t < 5; ++t)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) xch[((mi * 5 + t) * 4 + r) * 64 + lane] = acc[mi][t][r];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) xch[(40 + mi * 4 + r) * 64 + lane] = accb[mi][r];
         }
     }
-    __syncthreads();
-    // db: column 0 of each ci half's ones product (tap group 1); h = 1 parks its sum for h = 0
-    float* dbx = reinterpret_cast<float*>(smem) + 4 * XN * 64;
-    if (kp == 0 && tg == 1 && h == 1 && (lane & 15) == 0)
+    // db partials of the staging items -> LDS; co = 32 cohalf + 4 dg + j summed over the 48 windows in order
+    float* dbs = reinterpret_cast<float*>(smem) + 4 * XN * 64;
+    if (tid < X3W_DYITEMS)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dbx[(mi * 4 + (lane >> 4)) * 4 + r] = accb[mi][r] + xch[(40 + mi * 4 + r) * 64 + lane];
+        for (int j = 0; j < 4; ++j) dbs[tid * 4 + j] = dbacc[j];
     __syncthreads();
+    if (tid < 32) {
+        const int g = tid >> 2, j = tid & 3;
+        float sum = 0.f;
+        for (int w = 0; w < 48; ++w) sum += dbs[(w * 8 + g) * 4 + j];
+        slabs[(size_t)ks * (W2_N + C2) + W2_N + 32 * cohalf + tid] = sum;
+    }
     if (kp == 0) {
-        const float us = ldexpf(1.f, -(sx + sd)), ub = ldexpf(1.f, -sd);
+        const float us = ldexpf(1.f, -(sx + sd));
         float* slab = slabs + (size_t)ks * (W2_N + C2);
         const int ci = 16 * h + (lane & 15);
         const int nt = tg ? 4 : 5;
@@ -900,12 +923,112 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
                         const int co = 32 * cohalf + 16 * mi + 4 * (lane >> 4) + r;
                         slab[(co * C1 + ci) * 9 + 5 * tg + t] = (acc[mi][t][r] + xch[((mi * 5 + t) * 4 + r) * 64 + lane]) * us;
                     }
-            if (tg == 1 && h == 0 && (lane & 15) == 0)
+        }
+    }
+}
+
+// ============================================================================ conv1 -> x3 input images
+// The client's conv1 + ReLU (src/model_def.py:8-9, the per-pixel FMA order of slk_client.hip's
+// conv1_fwd_kernel: taps from 0, then + bias) writing the server's x3 operand directly: per sample, the
+// max act (act_amax), then every unit's f16 image in conv2_fwd_pool_x3's act16 layout (per-sample scale
+// 2^s, s = x3_exp(max act): bit-identical to the images that kernel writes from the f32 act), and —
+// when act != nullptr — the f32 act too. One workgroup per sample; pass 1 (thread = 4 consecutive
+// pixels, float4 act stores) computes the maximum, pass 2 recomputes (9 FMAs a value) per (pixel,
+// 8-channel chunk) item and splits: rows 8-9 and 16-17 belong to two units and are written twice.
+constexpr int C1X_T = 192;
+constexpr int C1X_G = A_PIX / 4;  // 169 active threads
+__global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
+                                                             const float* __restrict__ b1, float* __restrict__ act,
+                                                             float* __restrict__ act_amax, uint16_t* __restrict__ act16) {
+    __shared__ float xs[IN_HW * IN_HW];
+    __shared__ float amx[C1X_T / 64];
+    __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* xb = x + (size_t)b * IN_HW * IN_HW;
+    for (int i = tid; i < IN_HW * IN_HW / 4; i += C1X_T)
+        reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xb)[i];
+    for (int i = tid; i < C1 * 9; i += C1X_T) ws[(i / 9) * 10 + i % 9] = W1[i];
+    if (tid < C1) ws[tid * 10 + 9] = b1[tid];
+    __syncthreads();
+    const bool active = tid < C1X_G;
+    float xv[4][9];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int co = 32 * cohalf + 16 * mi + 4 * (lane >> 4) + r;
-                    slab[W2_N + co] = (accb[mi][r] + xch[(40 + mi * 4 + r) * 64 + lane] + dbx[(mi * 4 + (lane >> 4)) * 4 + r]) * ub;
-                }
+    for (int u = 0; u < 4; ++u) {
+        const int p = active ? 4 * tid + u : 0;
+        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
+    }
+    auto conv = [&](int c, float o[4]) {
+        const float* w = ws + c * 10;
+        float wk[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) wk[k] = w[k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sum = fmaf(xv[u][k], wk[k], sum);
+            sum += wk[9];
+            o[u] = sum > 0.f ? sum : 0.f;
+        }
+    };
+    float am = 0.f;
+    if (active) {
+        float4* out = act ? reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid : nullptr;
+#pragma unroll 4
+        for (int c = 0; c < C1; ++c) {
+            float o[4];
+            conv(c, o);
+            if (act) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
+            am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+        }
+    }
+    am = wave_max(am);
+    if ((tid & 63) == 0) amx[tid >> 6] = am;
+    __syncthreads();
+    am = fmaxf(fmaxf(amx[0], amx[1]), amx[2]);
+    if (tid == 0) act_amax[b] = am;
+    const float sc = ldexpf(1.f, x3_exp(am));
+    // pass 2: item = (pixel p, 8-channel chunk c8), lanes on consecutive items, so one store
+    // instruction covers 16 whole 64-B pixel records (1 KiB contiguous); c8 = tid & 3 for every item of a
+    // thread (the stride 192 is a multiple of 4): its 8 channels' weights stay in registers
+    const int c8 = tid & 3;
+    float wr[8][10];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) wr[j][k] = ws[(8 * c8 + j) * 10 + k];
+    char* img = reinterpret_cast<char*>(act16) + (size_t)3 * b * X3F_BUF;
+#pragma unroll 2
+    for (int i = tid; i < A_PIX * 4; i += C1X_T) {
+        const int p = i >> 2;
+        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
+        float xw[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) xw[k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sum = fmaf(xw[k], wr[j][k], sum);
+            sum += wr[j][9];
+            v[j] = sum > 0.f ? sum : 0.f;
+        }
+        f16x8 hh, ll;
+        x3_split8(v, sc, hh, ll);
+        const int slot = (c8 ^ (xx & 2)) * 16;
+        // unit t3 holds rows 8 t3 .. 8 t3 + 9
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3) {
+            const int r = y - 8 * t3;
+            if (r >= 0 && r < X3F_ROWS) {
+                char* o = img + t3 * X3F_BUF + (r * A_HW + xx) * 64 + slot;
+                *reinterpret_cast<f16x8*>(o) = hh;
+                *reinterpret_cast<f16x8*>(o + X3F_PLANE) = ll;
+            }
         }
     }
 }
@@ -923,7 +1046,7 @@ extern "C" int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, c
     SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code && act16);
     if (B == 0) return 0;
     const int U = 3 * B;
-    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
+    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel<false>, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
                        slk_stream(stream), act, act_amax, W2, b2, pooled, code, B, act16);
     return slk_launch_status();
 }
@@ -934,8 +1057,27 @@ extern "C" int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, co
     SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code);
     if (B == 0) return 0;
     const int U = 3 * B;
-    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
-                       slk_stream(stream), act, act_amax, W2, b2, pooled, code, B);
+    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel<false>, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
+                       slk_stream(stream), act, act_amax, W2, b2, pooled, code, B, nullptr);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_fwd_pool_x3i(const uint16_t* act16, const float* act_amax, const float* W2, const float* b2,
+                                      float* pooled, uint8_t* code, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act16 && act_amax && W2 && b2 && pooled && code);
+    if (B == 0) return 0;
+    const int U = 3 * B;
+    hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel<true>, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
+                       slk_stream(stream), nullptr, act_amax, W2, b2, pooled, code, B, const_cast<uint16_t*>(act16));
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1, float* act, float* act_amax,
+                                uint16_t* act16, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && (B == 0 || (x && W1 && b1 && act_amax && act16)));
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(conv1_fwd_x3_kernel, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act, act_amax,
+                       act16);
     return slk_launch_status();
 }
 

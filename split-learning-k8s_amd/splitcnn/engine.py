@@ -167,7 +167,11 @@ class ClientStage:
         self._x = None
         self._act = None
         self._act_amax = None
+        self._act16 = None
         self.emit_amax = False  # forward also writes the per-sample max of act (x3 server kernels)
+        # forward writes the x3 server operand (act16 images + act_amax) instead of the f32 act: the
+        # fused single-GPU step, where the cut never leaves the device (forward then returns None)
+        self.emit_act16 = False
 
     @property
     def W1(self):
@@ -187,6 +191,13 @@ class ClientStage:
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """act = relu(conv1(x)) (client_part.py:114). Keeps x/act for the backward."""
         B = x.shape[0]
+        if self.emit_act16:
+            amax = self._buf.get("act_amax", (B,), torch.float32, self.device)
+            a16 = self._buf.get("act16", (ops.conv2_act16_bytes(B),), torch.uint8, self.device)
+            with TIMER("conv1_fwd"):
+                act = ops.conv1_fwd_x3(x, self.W1.detach(), self.b1.detach(), amax, a16, act=out)
+            self._x, self._act, self._act_amax, self._act16 = x, act, amax, a16
+            return act
         act = out if out is not None else self._buf.get("act", (B, 32, 26, 26), torch.float32, self.device)
         amax = self._buf.get("act_amax", (B,), torch.float32, self.device) if self.emit_amax else None
         with TIMER("conv1_fwd"):
@@ -256,27 +267,36 @@ class ServerStage:
     def _b(self, name, shape, dtype=torch.float32):
         return self._buf.get(name, shape, dtype, self.device)
 
-    def forward_backward(self, act: torch.Tensor, labels: torch.Tensor, grad_scale: float,
-                         cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None):
+    def forward_backward(self, act: Optional[torch.Tensor], labels: torch.Tensor, grad_scale: float,
+                         cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
+                         act16: Optional[torch.Tensor] = None):
         """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
         conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
-        of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise."""
-        B = act.shape[0]
+        of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise.
+        act16 (with act_amax, x3 forward + wgrad only): the client's split input images
+        (ClientStage.emit_act16) — act is then not read and may be None."""
+        B = labels.shape[0]
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
         W3, b3 = m.fc1.weight.detach(), m.fc1.bias.detach()
         fi, di, wi = self.impl_fwd, self.impl_dgrad, self.impl_wgrad
+        if act16 is not None and (fi, wi) != ("x3", "x3") or act16 is not None and act_amax is None:
+            raise ValueError("act16 input needs the x3 forward and wgrad (conv preset 'x3') and act_amax")
         if act_amax is None and "x3" in (fi, wi):
             with TIMER("act_amax"):
                 act_amax = ops.row_amax(act, out=self._b("act_amax", (B,)))
         dp_amax = self._b("dp_amax", (B,)) if "x3" in (di, wi) else None
-        # x3 forward + x3 wgrad: the forward hands its split input images to the wgrad (LDS-DMA copy)
-        act16 = (self._b("act16", (ops.conv2_act16_bytes(B),), torch.uint8)
-                 if fi == "x3" and wi == "x3" and self.share_images else None)
-        with TIMER("conv2_fwd_pool"):
-            pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=self._b("pooled", (B, 64, 12, 12)),
-                                              code=self._b("code", (B, 64, 12, 12), torch.uint8), impl=fi,
-                                              act_amax=act_amax, act16=act16)
+        pooled_b, code_b = self._b("pooled", (B, 64, 12, 12)), self._b("code", (B, 64, 12, 12), torch.uint8)
+        if act16 is not None:
+            with TIMER("conv2_fwd_pool"):
+                pooled, code = ops.conv2_fwd_pool_x3i(act16, act_amax, W2, b2, pooled=pooled_b, code=code_b)
+        else:
+            # x3 forward + x3 wgrad: the forward hands its split input images to the wgrad (LDS-DMA copy)
+            act16 = (self._b("act16", (ops.conv2_act16_bytes(B),), torch.uint8)
+                     if fi == "x3" and wi == "x3" and self.share_images else None)
+            with TIMER("conv2_fwd_pool"):
+                pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=pooled_b, code=code_b, impl=fi,
+                                                  act_amax=act_amax, act16=act16)
         with TIMER("fc_xent"):
             _, loss_i, dlogits, dpooled = ops.fc_xent(
                 pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
@@ -305,10 +325,10 @@ class ServerStage:
         ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB], accumulate=accumulate)
         ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:], accumulate=accumulate)
 
-    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act_amax=None):
+    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act_amax=None, act16=None):
         """forward_backward + reduce into self.grads; returns (cut_grad, loss_i)."""
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, grad_scale, cut_grad=cut_grad,
-                                                         act_amax=act_amax)
+                                                         act_amax=act_amax, act16=act16)
         self.reduce_grads(s2, s3, accumulate=accumulate)
         return cut_grad, loss_i
 
@@ -324,13 +344,14 @@ class ServerStage:
         if step is not None:
             self.loss_log.note_step(step)
 
-    def step_request(self, act: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
-                     cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None):
+    def step_request(self, act: Optional[torch.Tensor], labels: torch.Tensor, step: Optional[int] = None,
+                     cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
+                     act16: Optional[torch.Tensor] = None):
         """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i). The mean
         loss for `step` lands in the device loss log."""
-        B = act.shape[0]
+        B = labels.shape[0]
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad,
-                                                         act_amax=act_amax)
+                                                         act_amax=act_amax, act16=act16)
         if self.fuse_optim:
             # optimizer.step() + log_metric in ONE launch (bit-identical to the three below); measured
             # -10 us per step at B = 4096 (tools/ab_step.py). The client's SGD stays a separate launch
@@ -361,12 +382,14 @@ class SplitTrainer:
 
     def __init__(self, client: Optional[ModelPartA] = None, server: Optional[ModelPartB] = None,
                  lr: float = LR, device="cuda", graph: bool = True, loss_log: Optional[LossLog] = None,
-                 conv: str = CONV_DEFAULT):
+                 conv: str = CONV_DEFAULT, act16: bool = True):
         self.device = torch.device(device)
         self.client = ClientStage(client, lr, self.device)
         self.server = ServerStage(server, lr, self.device, loss_log, conv=conv)
-        # the cut's per-sample max rides along with the cut (fused into conv1) for the x3 kernels
+        # the cut's per-sample max rides along with the cut (fused into conv1) for the x3 kernels; with the
+        # x3 forward AND wgrad the client writes the server's split input images directly (no f32 cut)
         self.client.emit_amax = "x3" in (self.server.impl_fwd, self.server.impl_wgrad)
+        self.client.emit_act16 = (self.server.impl_fwd, self.server.impl_wgrad) == ("x3", "x3") and act16
         self.graph = graph
         self._graphs = {}
         self.global_step = 0
@@ -377,7 +400,8 @@ class SplitTrainer:
 
     def _eager(self, x, y):
         act = self.client.forward(x)
-        cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax)
+        cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax,
+                                               act16=self.client._act16 if self.client.emit_act16 else None)
         self.client.backward_step(cut_grad)
 
     def static_inputs(self, B: int):

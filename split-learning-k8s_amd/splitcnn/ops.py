@@ -69,6 +69,28 @@ def conv1_fwd(x, W1, b1, out=None, act_amax=None):
     return act
 
 
+def conv1_fwd_x3(x, W1, b1, act_amax, act16, act=None):
+    """conv1 + ReLU writing the x3 server operand: act_amax [B] and the act16 images
+    (conv2_act16_bytes(B) uint8), plus the f32 act when `act` is given. Returns act (or None)."""
+    B = batch_of(x, (1, 28, 28), "x")
+    ap = _dev(act, "act", (B, 32, 26, 26)) if act is not None else None
+    _lib.call("slk_conv1_fwd_x3", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)), _dev(b1, "conv1.bias", (32,)),
+              ap, _dev(act_amax, "act_amax", (B,)), _act16(act16, B), B, _stream(x))
+    return act
+
+
+def conv2_fwd_pool_x3i(act16, act_amax, W2, b2, pooled=None, code=None):
+    """The x3 forward + pool reading the act16 images (conv1_fwd_x3 / conv2_fwd_pool(act16=...)) instead
+    of the f32 act: the same pooled / code bitwise."""
+    B = batch_of(act_amax, (), "act_amax")
+    pooled = _out(pooled, (B, 64, 12, 12), act_amax, name="pooled")
+    code = _out(code, (B, 64, 12, 12), act_amax, torch.uint8, "code")
+    _lib.call("slk_conv2_fwd_pool_x3i", _act16(act16, B), _dev(act_amax, "act_amax", (B,)),
+              _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
+              _dev(code, "code", dtype=torch.uint8), B, _stream(act_amax))
+    return pooled, code
+
+
 def conv1_wgrad_nslab(B: int) -> int:
     return _lib.query("slk_conv1_wgrad_nslab", B)
 
@@ -253,19 +275,25 @@ def conv2_wgrad_nslab(B: int, direct: bool = False, impl=None) -> int:
 def conv2_wgrad_slabs(act, dpooled, code, slabs=None, direct=False, impl=None, act_amax=None, dp_amax=None,
                       act16=None):
     """act16 (x3 only): the forward's split input images (conv2_fwd_pool(..., act16=...), same act and
-    act_amax) — the kernel then moves them by LDS-DMA instead of loading and splitting act."""
+    act_amax, or conv1_fwd_x3) — the kernel then moves them by LDS-DMA instead of loading and splitting
+    act, and act may be None (act_amax is then required)."""
     impl = _impl(direct, impl)
-    B = batch_of(act, (32, 26, 26), "act")
-    if _dpooled_batch(dpooled) != B:
-        raise ValueError("act / dpooled batch mismatch")
-    slabs = _out(slabs, (conv2_wgrad_nslab(B, impl=impl), CONV2_SLAB), act, name="slabs")
+    if act is None:
+        if impl != "x3" or act16 is None or act_amax is None:
+            raise ValueError("conv2_wgrad_slabs: act=None needs impl='x3', act16 and act_amax")
+        B = _dpooled_batch(dpooled)
+    else:
+        B = batch_of(act, (32, 26, 26), "act")
+        if _dpooled_batch(dpooled) != B:
+            raise ValueError("act / dpooled batch mismatch")
+    slabs = _out(slabs, (conv2_wgrad_nslab(B, impl=impl), CONV2_SLAB), dpooled, name="slabs")
     if impl == "x3":
         act_amax = row_amax(act) if act_amax is None else act_amax
         dp_amax = row_amax(dpooled) if dp_amax is None else dp_amax
         if act16 is not None:
             _lib.call("slk_conv2_wgrad_x3s", _act16(act16, B), _dev(act_amax, "act_amax", (B,)),
                       _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
-                      _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(act))
+                      _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(slabs, "slabs"), B, _stream(dpooled))
             return slabs
         _lib.call("slk_conv2_wgrad_x3", _dev(act, "act"), _dev(act_amax, "act_amax", (B,)), _dev(dpooled, "dpooled"),
                   _dev(dp_amax, "dp_amax", (B,)), _dev(code, "code", (B, 64, 12, 12), torch.uint8),

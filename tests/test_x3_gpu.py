@@ -197,8 +197,8 @@ def test_trainer_conv_presets_match_fixture(gpu, conv):
 @pytest.mark.parametrize("B", [1, 7, 300])
 def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
     """The forward's split input images (act16) fed to the wgrad by LDS-DMA give the same slabs bit for
-    bit as the wgrad that loads and splits act itself (same launch scale, same f16 values); the
-    forward in that mode (launch scale) still meets the oracle bar."""
+    bit as the wgrad that loads and splits act itself (same per-sample scales, same f16 values); the
+    forward in that mode is the plain x3 forward bit for bit and meets the oracle bar."""
     from oracle.split_step import conv3x3, relu, tie_discrepancies
     from splitcnn import ops
     act, p, y = _inputs(gpu, B, seed=B + 300)
@@ -209,8 +209,63 @@ def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
     s1 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am)
     s2 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am, act16=a16)
     assert torch.equal(s1, s2)
+    px, cx = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=am)
+    assert torch.equal(px, ps) and torch.equal(cx, cs)
     r = relu(conv3x3(act.double().cpu().numpy(), p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
     pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
     n, ok = tie_discrepancies(r, cw.cpu().numpy().astype(np.int64), cs.cpu().numpy().astype(np.int64))
     assert ok, n
     assert rel_err(ps.cpu().numpy(), r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))) <= 1e-5
+
+
+@pytest.mark.parametrize("B", [1, 6, 257])
+def test_conv1_x3_images_and_forward_from_images_bitwise(gpu, B):
+    """slk_conv1_fwd_x3 writes the same f32 act and act_amax as conv1_fwd(act_amax=...), and the same
+    act16 images as the x3 forward does from that act (bitwise, every byte); the forward reading those
+    images (slk_conv2_fwd_pool_x3i) gives the x3 forward's pooled / code bit for bit, and the wgrad
+    reading them the same slabs."""
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    a, b = init_models(seed=B + 11)
+    x, y = SyntheticMNIST(B + 12).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
+    W2, b2 = b.conv2.weight.detach().to(gpu), b.conv2.bias.detach().to(gpu)
+    W3, b3 = b.fc1.weight.detach().to(gpu), b.fc1.bias.detach().to(gpu)
+    am0 = torch.empty(B, device=gpu)
+    act0 = ops.conv1_fwd(x, W1, b1, act_amax=am0)
+    nb = ops.conv2_act16_bytes(B)
+    am1, i1 = torch.empty(B, device=gpu), torch.full((nb,), 7, dtype=torch.uint8, device=gpu)
+    act1 = ops.conv1_fwd_x3(x, W1, b1, am1, i1, act=torch.empty_like(act0))
+    am2, i2 = torch.empty(B, device=gpu), torch.full((nb,), 9, dtype=torch.uint8, device=gpu)
+    assert ops.conv1_fwd_x3(x, W1, b1, am2, i2) is None
+    assert torch.equal(act1, act0) and torch.equal(am1, am0) and torch.equal(am2, am0)
+    i0 = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    p0, c0 = ops.conv2_fwd_pool(act0, W2, b2, impl="x3", act_amax=am0, act16=i0)
+    assert torch.equal(i1, i0) and torch.equal(i2, i0)
+    p1, c1 = ops.conv2_fwd_pool_x3i(i2, am2, W2, b2)
+    assert torch.equal(p1, p0) and torch.equal(c1, c0)
+    _, _, _, dp = ops.fc_xent(p0, W3, b3, y, 1.0 / B)
+    s0 = ops.conv2_wgrad_slabs(act0, dp, c0, impl="x3", act_amax=am0)
+    s1 = ops.conv2_wgrad_slabs(None, dp, c0, impl="x3", act_amax=am2, act16=i2)
+    assert torch.equal(s0, s1)
+
+
+def test_trainer_client_images_bitwise(gpu):
+    """SplitTrainer with the client writing the x3 images (no f32 cut) and with the f32 cut + the
+    forward writing them: identical parameters and losses after three steps, bit for bit."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    out = []
+    for img in (True, False):
+        a, b = init_models(seed=21)
+        tr = SplitTrainer(a, b, device=gpu, graph=True, conv="x3", act16=img)
+        assert tr.client.emit_act16 == img
+        data = SyntheticMNIST(22)
+        for _ in range(3):
+            x, y = data.batch(96)
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        out.append((tr.client.params.clone(), tr.server.params.clone(), tr.loss_log.flush()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] and len(out[0][2]) == 3
