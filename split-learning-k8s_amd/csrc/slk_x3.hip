@@ -280,6 +280,40 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         }
         const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
         f32x4 acc[3][X3F_NT];
+        if constexpr (IN16 && !(SLK_X3ABL & 2048)) {
+            // no staging in the loop: all 27 (M tile, tap) steps in one stream, A fragments read through
+            // a 3-slot ring two steps ahead
+#pragma unroll
+            for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            f16x8 fh[3], fl[3];
+            auto rdA = [&](int st) {
+                const int mt = st / 9, tap = st % 9, ky = tap / 3, kx = tap % 3;
+                fh[st % 3] = *reinterpret_cast<const f16x8*>(cur + abase[mt][kx] + ky * A_HW * 64);
+                fl[st % 3] = *reinterpret_cast<const f16x8*>(cur + X3F_PLANE + abase[mt][kx] + ky * A_HW * 64);
+            };
+            rdA(0);
+            rdA(1);
+#pragma unroll
+            for (int st = 0; st < 27; ++st) {
+                if (st + 2 < 27) rdA(st + 2);
+                const int mt = st / 9, tap = st % 9;
+#pragma unroll
+                for (int nt = 0; nt < X3F_NT; ++nt)
+                    acc[mt][nt] = mfma_x3(fh[st % 3], fl[st % 3], wh[nt][tap], wl[nt][tap], acc[mt][nt]);
+            }
+            // (measured: leaving the order to the compiler beats pinning it with sched_group_barrier,
+            // 0.243 vs 0.275 ms, and the pre-ring loop 0.260; SLK_X3ABL & 4096 pins it)
+            if (SLK_X3ABL & 4096) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+                for (int st = 0; st < 27; ++st) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+                    if (st + 2 < 27) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
+            }
+        } else
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
 #pragma unroll

@@ -44,11 +44,17 @@ def main():
         for n in ("slk_conv2_fwd_pool_x3s", "slk_conv2_dgrad_x3", "slk_conv2_wgrad_x3s", "slk_conv2_wgrad_x3_nslab"):
             getattr(L, n).restype = ctypes.c_int
         tag = os.path.basename(path).replace(".so", "")
-        if "fwd" in args.ops:
+        if "fwd," in args.ops + "," :
             po, co, a16o = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16)
             L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
             cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
                 p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+        if "fwdi" in args.ops:
+            po2, co2 = torch.empty_like(pooled), torch.empty_like(code)
+            L.slk_conv2_fwd_pool_x3i.restype = ctypes.c_int
+            L.slk_conv2_fwd_pool_x3i.argtypes = [P] * 6 + [ctypes.c_int, P]
+            cases[f"fwdi {tag}"] = (lambda L=L, po=po2, co=co2: L.slk_conv2_fwd_pool_x3i(
+                p(a16), p(amax), p(W2), p(b2), p(po), p(co), B, st))
         if "dgrad" in args.ops:
             g = torch.empty_like(act)
             L.slk_conv2_dgrad_x3.argtypes = [P] * 5 + [ctypes.c_int, P]
