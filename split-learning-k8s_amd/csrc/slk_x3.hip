@@ -577,11 +577,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 acc[i] = mfma_x3(fh[st & 3], fl[st & 3], wh[h][tap], wl[h][tap], acc[i]);
             }
             // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
-            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+            if (!(SLK_X3ABL & 8192)) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-            for (int st = 0; st < NS; ++st) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-                if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                for (int st = 0; st < NS; ++st) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                    if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
             }
             if (!(SLK_X3ABL & 1) && !sfirst) {
                 store_dy(unx, nimg);
@@ -595,11 +597,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     if (tap + 3 < 9) rd(3, tap + 3, fh[(tap + 3) & 3], fl[(tap + 3) & 3]);
                     acc[3] = mfma_x3(fh[tap & 3], fl[tap & 3], wh[h][tap], wl[h][tap], acc[3]);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
+                if (!(SLK_X3ABL & 8192)) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
 #pragma unroll
-                for (int tap = 0; tap < 9; ++tap) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
-                    if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+                    for (int tap = 0; tap < 9; ++tap) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
+                        if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+                    }
                 }
             }
         }
@@ -855,13 +859,15 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             for (int mi = 0; mi < 2; ++mi)
                 acc[mi][t] = mfma_x3(Ah[j & 1][mi], Al[j & 1][mi], Bh[n % 3], Bl[n % 3], acc[mi][t]);
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        if (!(SLK_X3ABL & 16384)) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
-        for (int n = 0; n < N; ++n) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-            if (n + 2 < N) {
-                if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-                else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+            for (int n = 0; n < N; ++n) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+                if (n + 2 < N) {
+                    if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                }
             }
         }
     };
