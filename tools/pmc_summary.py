@@ -51,7 +51,12 @@ if args.traffic_out:
                   "conv2_dgrad_wino_kernel": "conv2_dgrad",
                   "conv2_wgrad_wino_kernel": "conv2_wgrad", "fc_head_kernel<8>": "fc_xent",
                   "conv2_fwd_pool_x3_kernel": "conv2_fwd_pool_x3", "conv2_dgrad_x3_kernel": "conv2_dgrad_x3",
-                  "conv2_wgrad_x3_kernel": "conv2_wgrad_x3"})
+                  "conv2_wgrad_x3_kernel": "conv2_wgrad_x3",
+                  # round 2: the default step's instantiations (client images in) and the f32-cut ones
+                  "conv2_fwd_pool_x3_kernel<true>": "conv2_fwd_pool_x3",
+                  "conv2_fwd_pool_x3_kernel<false>": "conv2_fwd_pool_x3_f32in",
+                  "conv2_wgrad_x3_kernel<true>": "conv2_wgrad_x3", "conv2_wgrad_x3_kernel<false>": "conv2_wgrad_x3_gather",
+                  "conv1_fwd_x3_kernel": "conv1_fwd"})
     # widened (K5) template instantiations -> bench.py's kernel names (csrc/slk_wide.hip:824-836, 1055)
     wide = [("wide_conv32_kernel<Conv32Cfg<64, 128, 32", "wide_conv2_fwd"),
             ("wide_conv_kernel<ConvCfg<64, 128, 32", "wide_conv2_fwd"),
