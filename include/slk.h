@@ -184,6 +184,14 @@ int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1, float* ac
 int slk_conv2_fwd_pool_x3i(const uint16_t* act16, const float* act_amax, const float* W2, const float* b2,
                            float* pooled, uint8_t* code, int B, void* stream);
 
+/* The x3 dgrad with the client's backward fused (src/server_part.py:51 -> src/client_part.py:132 in one
+ * launch, for the single-GPU step): the cut gradient is not written; each workgroup applies the client's
+ * ReLU mask (recomputed from x, W1, b1) and writes one slab [dW1 c*9+tap (288) | db1 c (32)] of the
+ * client gradient (slk_conv2_dgrad_x3_c1w_nslab(B) slabs, reduced by slk_sgd_from_slabs). */
+int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                           const float* x, const float* W1, const float* b1, float* client_slabs, int B, void* stream);
+int slk_conv2_dgrad_x3_c1w_nslab(int B);
+
 /* ---------------------------------------------------------------- reductions / optimizer */
 
 /* out[i] = (accumulate ? out[i] : 0) + sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed slab order).

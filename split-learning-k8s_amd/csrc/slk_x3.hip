@@ -398,10 +398,20 @@ __device__ __forceinline__ int x3d_t0(int pt) { return pt == 0 ? 0 : (pt == 1 ? 
 __device__ __forceinline__ int x3d_ybase(int pt) { return pt == 0 ? -2 : (pt == 1 ? 6 : 14); }
 __device__ __forceinline__ int x3d_nwr(int pt) { return pt == 2 ? 7 : 6; }  // image window rows
 
+// C1W = true (the fused single-GPU step): the cut gradient is not stored; the epilogue applies the
+// client's ReLU mask (recomputed from x, W1, b1 with conv1's exact FMA order, as slk_conv1_wgrad_remask
+// does) and accumulates the conv1 weight gradient dW1[ci][tap] += g * x, db1[ci] += g in registers (a
+// lane owns one ci); each workgroup writes one 320-float client slab (src/client_part.py:132 — the
+// client's act.backward(cut_grad) without the cut gradient ever reaching HBM). x of the next pair is
+// loaded a unit ahead and kept in LDS (2 x 3,136 B).
+template <bool C1W>
 __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ dpooled, const float* __restrict__ amax, const uint8_t* __restrict__ code,
-    const float* __restrict__ W2, float* __restrict__ cut_grad, int B) {
+    const float* __restrict__ W2, float* __restrict__ cut_grad, int B, const float* __restrict__ xin = nullptr,
+    const float* __restrict__ W1 = nullptr, const float* __restrict__ b1 = nullptr, float* __restrict__ c1slabs = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
+    __shared__ float xsm[C1W ? 2 : 1][C1W ? IN_HW * IN_HW : 1];
+    __shared__ float w1s[C1W ? C1 * 10 : 1];  // [c][9 taps | bias]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
@@ -521,13 +531,24 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     // (pair = (sample, part))
     const int P = 3 * B;  // pairs
     int pr = blockIdx.x;
+    // C1W: per-lane conv1 gradient accumulators for ci = 16 nt + n16 (9 taps + bias) and x staging
+    float c1acc[C1W ? 10 : 1];
+#pragma unroll
+    for (int j = 0; j < (C1W ? 10 : 1); ++j) c1acc[j] = 0.f;
+    float2 xr = make_float2(0.f, 0.f);
+    const bool xthr = C1W && tid < IN_HW * IN_HW / 2;
+    if constexpr (C1W) {
+        if (tid < C1 * 9) w1s[(tid / 9) * 10 + tid % 9] = W1[tid];
+        if (tid < C1) w1s[tid * 10 + 9] = b1[tid];
+        if (pr < P && xthr) reinterpret_cast<float2*>(xsm[0])[tid] = reinterpret_cast<const float2*>(xin + (size_t)(pr / 3) * IN_HW * IN_HW)[tid];
+    }
     if (pr < P) {
         load_dy(2 * pr);
         __syncthreads();  // zeroing / red restore done before the first expansion
         store_dy(2 * pr, smem);
         load_dy(2 * pr + 1);
     }
-    int k = 0;
+    int k = 0, q = 0;
     (void)u;
 #pragma unroll 1
     for (; pr < P; pr += G) {
@@ -540,6 +561,12 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h, ++k) {
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
+            if constexpr (C1W) {
+                // x of the next pair: loaded at its h = 0 unit, into LDS at h = 1 (the other buffer)
+                const int np = min(pr + G, P - 1);
+                if (h == 0 && xthr) xr = reinterpret_cast<const float2*>(xin + (size_t)(np / 3) * IN_HW * IN_HW)[tid];
+                if (h == 1 && xthr) reinterpret_cast<float2*>(xsm[(q + 1) & 1])[tid] = xr;
+            }
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
             const int unx = min(h ? 2 * (pr + G) : 2 * pr + 1, U - 1);   // the unit after this one
@@ -609,12 +636,61 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         }
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
         const float us = ldexpf(1.f, -(x3_exp(amax_b) + sw));
-        float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
+        if constexpr (C1W) {
+            // client ReLU backward + conv1 wgrad for this lane's ci and pixels (the cut gradient g is the
+            // value the store below would write)
+            const int ci = 16 * nt + n16;
+            const float* xs = xsm[q & 1];
+            float wk[10];
 #pragma unroll
-        for (int i = 0; i < X3D_MPW; ++i) {
-            const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
-            if (t < T1 && p < A_PIX)
-                *reinterpret_cast<float4*>(gb + p) = make_float4(acc[i][0] * us, acc[i][1] * us, acc[i][2] * us, acc[i][3] * us);
+            for (int j = 0; j < 10; ++j) wk[j] = w1s[ci * 10 + j];
+#pragma unroll
+            for (int i = 0; i < X3D_MPW; ++i) {
+                const int t = T0 + g + 4 * i;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int p = 16 * t + 4 * kc + r;
+                    if (t < T1 && p < A_PIX) {
+                        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
+                        float xv[9];
+#pragma unroll
+                        for (int kk = 0; kk < 9; ++kk) xv[kk] = xs[(y + kk / 3) * IN_HW + xx + kk % 3];
+                        float sum = 0.f;
+#pragma unroll
+                        for (int kk = 0; kk < 9; ++kk) sum = fmaf(xv[kk], wk[kk], sum);
+                        sum += wk[9];
+                        const float gm = sum > 0.f ? acc[i][r] * us : 0.f;
+#pragma unroll
+                        for (int kk = 0; kk < 9; ++kk) c1acc[kk] = fmaf(gm, xv[kk], c1acc[kk]);
+                        c1acc[9] += gm;
+                    }
+                }
+            }
+        } else {
+            float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
+#pragma unroll
+            for (int i = 0; i < X3D_MPW; ++i) {
+                const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
+                if (t < T1 && p < A_PIX)
+                    *reinterpret_cast<float4*>(gb + p) = make_float4(acc[i][0] * us, acc[i][1] * us, acc[i][2] * us, acc[i][3] * us);
+            }
+        }
+        ++q;
+    }
+    if constexpr (C1W) {
+        // slab of this workgroup: ci's 16 partials (4 kc lanes x 4 tile groups) summed in a fixed order
+        __syncthreads();
+        float* part = reinterpret_cast<float*>(smem);  // [wave][lane][10]
+#pragma unroll
+        for (int j = 0; j < 10; ++j) part[(wave * 64 + lane) * 10 + j] = c1acc[j];
+        __syncthreads();
+        if (tid < C1 * 10) {
+            const int ci = tid / 10, j = tid - (tid / 10) * 10;
+            const int ntc = ci >> 4, n = ci & 15;
+            float sum = 0.f;
+            for (int gg = 0; gg < 4; ++gg)
+                for (int kq = 0; kq < 4; ++kq) sum += part[((ntc + 2 * gg) * 64 + kq * 16 + n) * 10 + j];
+            c1slabs[(size_t)blockIdx.x * (C1 * 10) + (j < 9 ? ci * 9 + j : C1 * 9 + ci)] = sum;
         }
     }
 }
@@ -1126,8 +1202,21 @@ extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, co
     SLK_CHECK_ARG(B >= 0 && dpooled && dp_amax && code && W2 && cut_grad);
     if (B == 0) return 0;
     const int P = 3 * B;
-    hipLaunchKernelGGL(conv2_dgrad_x3_kernel, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
-                       slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B);
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
+                       slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B, nullptr, nullptr, nullptr, nullptr);
+    return slk_launch_status();
+}
+
+extern "C" int slk_conv2_dgrad_x3_c1w_nslab(int B) { return B <= 0 ? 0 : (3 * B < X3D_GRID ? 3 * B : X3D_GRID); }
+
+extern "C" int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                                      const float* x, const float* W1, const float* b1, float* client_slabs, int B,
+                                      void* stream) {
+    SLK_CHECK_ARG(B >= 0 && (B == 0 || (dpooled && dp_amax && code && W2 && x && W1 && b1 && client_slabs)));
+    if (B == 0) return 0;
+    const int P = 3 * B;
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel<true>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
+                       slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, x, W1, b1, client_slabs);
     return slk_launch_status();
 }
 

@@ -61,6 +61,8 @@ _SIGS = {
     "slk_conv2_act16_bytes": [_I],
     "slk_conv1_fwd_x3": [_P, _P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_fwd_pool_x3i": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_dgrad_x3_c1w": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_dgrad_x3_c1w_nslab": [_I],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
     "slk_sgd": [_P, _P, _I, _F, _P],

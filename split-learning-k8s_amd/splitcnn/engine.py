@@ -224,6 +224,12 @@ class ClientStage:
         with TIMER("sgd_client"):
             ops.sgd_from_slabs(self.params, self.grads, slabs, self.lr)
 
+    def step_from_slabs(self, slabs: torch.Tensor) -> None:
+        """optimizer.step() from gradient slabs produced elsewhere (the server's fused x3 dgrad,
+        ServerStage.forward_backward(client_fuse=...)): one fused reduce + SGD launch."""
+        with TIMER("sgd_client"):
+            ops.sgd_from_slabs(self.params, self.grads, slabs, self.lr)
+
     def backward(self, cut_grad: torch.Tensor, x: Optional[torch.Tensor] = None,
                  act: Optional[torch.Tensor] = None, accumulate: bool = False) -> None:
         """Weight gradient into self.grads (accumulate=True adds: micro-batches)."""
@@ -269,12 +275,14 @@ class ServerStage:
 
     def forward_backward(self, act: Optional[torch.Tensor], labels: torch.Tensor, grad_scale: float,
                          cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
-                         act16: Optional[torch.Tensor] = None):
+                         act16: Optional[torch.Tensor] = None, client_fuse=None):
         """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
         conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
         of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise.
         act16 (with act_amax, x3 forward + wgrad only): the client's split input images
-        (ClientStage.emit_act16) — act is then not read and may be None."""
+        (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, W1, b1,
+        slabs) (x3 dgrad only, single-GPU step): the dgrad also runs the client's ReLU backward +
+        conv1 wgrad into `slabs` and the cut gradient is not materialised (returned as None)."""
         B = labels.shape[0]
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
@@ -302,10 +310,18 @@ class ServerStage:
                 pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
                 loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
                 dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
-        if cut_grad is None:
-            cut_grad = self._b("cut_grad", (B, 32, 26, 26))
-        with TIMER("conv2_dgrad"):
-            ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
+        if client_fuse is not None:
+            if di != "x3":
+                raise ValueError("client_fuse needs the x3 dgrad (conv preset 'x3' or 'x3w')")
+            cx, cW1, cb1, cslabs = client_fuse
+            with TIMER("conv2_dgrad"):
+                ops.conv2_dgrad_client_slabs(dpooled, code, W2, cx, cW1, cb1, dp_amax=dp_amax, slabs=cslabs)
+            cut_grad = None
+        else:
+            if cut_grad is None:
+                cut_grad = self._b("cut_grad", (B, 32, 26, 26))
+            with TIMER("conv2_dgrad"):
+                ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
         with TIMER("conv2_wgrad"):
             s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
                                        slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
@@ -346,12 +362,12 @@ class ServerStage:
 
     def step_request(self, act: Optional[torch.Tensor], labels: torch.Tensor, step: Optional[int] = None,
                      cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
-                     act16: Optional[torch.Tensor] = None):
+                     act16: Optional[torch.Tensor] = None, client_fuse=None):
         """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i). The mean
         loss for `step` lands in the device loss log."""
         B = labels.shape[0]
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad,
-                                                         act_amax=act_amax, act16=act16)
+                                                         act_amax=act_amax, act16=act16, client_fuse=client_fuse)
         if self.fuse_optim:
             # optimizer.step() + log_metric in ONE launch (bit-identical to the three below); measured
             # -10 us per step at B = 4096 (tools/ab_step.py). The client's SGD stays a separate launch
@@ -382,7 +398,7 @@ class SplitTrainer:
 
     def __init__(self, client: Optional[ModelPartA] = None, server: Optional[ModelPartB] = None,
                  lr: float = LR, device="cuda", graph: bool = True, loss_log: Optional[LossLog] = None,
-                 conv: str = CONV_DEFAULT, act16: bool = True):
+                 conv: str = CONV_DEFAULT, act16: bool = True, fuse_client_backward: bool = True):
         self.device = torch.device(device)
         self.client = ClientStage(client, lr, self.device)
         self.server = ServerStage(server, lr, self.device, loss_log, conv=conv)
@@ -390,6 +406,8 @@ class SplitTrainer:
         # x3 forward AND wgrad the client writes the server's split input images directly (no f32 cut)
         self.client.emit_amax = "x3" in (self.server.impl_fwd, self.server.impl_wgrad)
         self.client.emit_act16 = (self.server.impl_fwd, self.server.impl_wgrad) == ("x3", "x3") and act16
+        # the x3 dgrad also runs the client's ReLU backward + conv1 wgrad (no cut gradient in HBM)
+        self.fuse_client_backward = self.server.impl_dgrad == "x3" and fuse_client_backward
         self.graph = graph
         self._graphs = {}
         self.global_step = 0
@@ -400,8 +418,16 @@ class SplitTrainer:
 
     def _eager(self, x, y):
         act = self.client.forward(x)
-        cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax,
-                                               act16=self.client._act16 if self.client.emit_act16 else None)
+        a16 = self.client._act16 if self.client.emit_act16 else None
+        if self.fuse_client_backward:
+            c = self.client
+            slabs = c._buf.get("c1w_slabs", (ops.conv2_dgrad_c1w_nslab(x.shape[0]), ops.CLIENT_NPARAM),
+                               torch.float32, self.device)
+            self.server.step_request(act, y, act_amax=c._act_amax, act16=a16,
+                                     client_fuse=(x, c.W1.detach(), c.b1.detach(), slabs))
+            c.step_from_slabs(slabs)
+            return
+        cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax, act16=a16)
         self.client.backward_step(cut_grad)
 
     def static_inputs(self, B: int):

@@ -91,6 +91,27 @@ def conv2_fwd_pool_x3i(act16, act_amax, W2, b2, pooled=None, code=None):
     return pooled, code
 
 
+def conv2_dgrad_c1w_nslab(B: int) -> int:
+    return _lib.query("slk_conv2_dgrad_x3_c1w_nslab", B)
+
+
+def conv2_dgrad_client_slabs(dpooled, code, W2, x, W1, b1, dp_amax=None, slabs=None):
+    """x3 dgrad fused with the client's ReLU backward + conv1 wgrad: returns the client's gradient
+    slabs [conv2_dgrad_c1w_nslab(B), 320] (conv1_wgrad_slabs' layout); the cut gradient is not
+    materialised. W1 / b1 must be the weights of the forward that produced the cut."""
+    B = _pooled_batch(dpooled)
+    batch_of(x, (1, 28, 28), "x")
+    if x.shape[0] != B:
+        raise ValueError("x / dpooled batch mismatch")
+    dp_amax = row_amax(dpooled) if dp_amax is None else dp_amax
+    slabs = _out(slabs, (conv2_dgrad_c1w_nslab(B), CLIENT_NPARAM), x, name="slabs")
+    _lib.call("slk_conv2_dgrad_x3_c1w", _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
+              _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+              _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)), _dev(b1, "conv1.bias", (32,)),
+              _dev(slabs, "slabs"), B, _stream(x))
+    return slabs
+
+
 def conv1_wgrad_nslab(B: int) -> int:
     return _lib.query("slk_conv1_wgrad_nslab", B)
 

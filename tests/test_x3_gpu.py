@@ -269,3 +269,64 @@ def test_trainer_client_images_bitwise(gpu):
         out.append((tr.client.params.clone(), tr.server.params.clone(), tr.loss_log.flush()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     assert out[0][2] == out[1][2] and len(out[0][2]) == 3
+
+
+@pytest.mark.parametrize("B", [1, 5, 130])
+def test_dgrad_with_fused_client_backward(gpu, B):
+    """slk_conv2_dgrad_x3_c1w: the client's gradient from the fused dgrad equals the separate path
+    (x3 dgrad -> cut gradient -> conv1_wgrad_remask) up to summation order (1e-5 of max |ref|), and the
+    fp64 oracle at the same bar."""
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    a, b = init_models(seed=B + 40)
+    x, y = SyntheticMNIST(B + 41).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
+    W2, b2 = b.conv2.weight.detach().to(gpu), b.conv2.bias.detach().to(gpu)
+    W3, b3 = b.fc1.weight.detach().to(gpu), b.fc1.bias.detach().to(gpu)
+    act = ops.conv1_fwd(x, W1, b1)
+    pooled, code = ops.conv2_fwd_pool(act, W2, b2, impl="x3")
+    dpa = torch.empty(B, device=gpu)
+    _, _, _, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+    slabs = ops.conv2_dgrad_client_slabs(dp, code, W2, x, W1, b1, dp_amax=dpa)
+    assert slabs.shape == (min(3 * B, 256), 320)
+    fused = ops.reduce_slabs(slabs).cpu().numpy()
+    g = ops.conv2_dgrad(dp, code, W2, impl="x3", dp_amax=dpa)
+    sep = ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, g)).cpu().numpy()
+    ref = _c1_ref64(x, W1, b1, g)
+    for sl in (slice(0, 288), slice(288, 320)):
+        assert rel_err(fused[sl], sep[sl]) <= 1e-5
+        assert rel_err(fused[sl], ref[sl]) <= 1e-5
+
+
+def _c1_ref64(x, W1, b1, g):
+    """fp64 ReLU backward + conv1 weight/bias gradient (the oracle's conv1 restated at the test)."""
+    x, W1, b1, g = (t.double().cpu().numpy() for t in (x, W1, b1, g))
+    B = x.shape[0]
+    win = np.stack([x[:, 0, ky:ky + 26, kx:kx + 26] for ky in range(3) for kx in range(3)], axis=1)  # B,9,26,26
+    s = np.einsum("bkyx,ck->bcyx", win, W1.reshape(32, 9)) + b1[None, :, None, None]
+    gm = np.where(s > 0, g, 0.0)
+    dW = np.einsum("bcyx,bkyx->ck", gm, win)
+    return np.concatenate([dW.reshape(-1), gm.sum(axis=(0, 2, 3))])
+
+
+def test_trainer_fused_client_backward_matches_unfused(gpu):
+    """SplitTrainer with the client's backward fused into the x3 dgrad vs the separate cut-gradient path:
+    the parameter updates of three steps agree to summation-order differences (1e-3 of the largest
+    update; a wrong gradient would be off by the update's own size)."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    out = []
+    for fuse in (True, False):
+        a, b = init_models(seed=31)
+        tr = SplitTrainer(a, b, device=gpu, graph=True, conv="x3", fuse_client_backward=fuse)
+        init = (tr.client.params.cpu().numpy().copy(), tr.server.params.cpu().numpy().copy())
+        assert tr.fuse_client_backward == fuse
+        data = SyntheticMNIST(32)
+        for _ in range(3):
+            x, y = data.batch(200)
+            tr.step(x.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        out.append((tr.client.params.cpu().numpy() - init[0], tr.server.params.cpu().numpy() - init[1]))
+    for u, v in zip(out[0], out[1]):
+        assert np.abs(u - v).max() <= 1e-3 * np.abs(v).max(), (np.abs(u - v).max(), np.abs(v).max())
