@@ -27,6 +27,8 @@ def main():
     a, b = init_models(seed=1)
     x, y = SyntheticMNIST(2).batch(B)
     act = ClientStage(a, device=dev).forward(x.to(dev)).clone()
+    xg = x.to(dev).contiguous()
+    W1, b1 = a.conv1.weight.detach().to(dev).contiguous(), a.conv1.bias.detach().to(dev).contiguous()
     W2, b2 = b.conv2.weight.detach().to(dev).contiguous(), b.conv2.bias.detach().to(dev).contiguous()
     W3, b3 = b.fc1.weight.detach().to(dev).contiguous(), b.fc1.bias.detach().to(dev).contiguous()
     amax = ops.row_amax(act)
@@ -59,6 +61,12 @@ def main():
             g = torch.empty_like(act)
             L.slk_conv2_dgrad_x3.argtypes = [P] * 5 + [ctypes.c_int, P]
             cases[f"dgrad {tag}"] = (lambda L=L, g=g: L.slk_conv2_dgrad_x3(p(dp), p(dpa), p(code), p(W2), p(g), B, st))
+        if "dgc1" in args.ops:
+            sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
+            L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
+            L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 8 + [ctypes.c_int, P]
+            cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1: L.slk_conv2_dgrad_x3_c1w(
+                p(dp), p(dpa), p(code), p(W2), p(xg), p(W1), p(b1), p(sl), B, st))
         if "wgrad" in args.ops:
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
