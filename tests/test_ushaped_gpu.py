@@ -47,7 +47,9 @@ def test_ushaped_bit_identical_to_split_trainer(gpu):
     a1, b1 = init_models(seed=1)
     a2, b2 = init_models(seed=1)
     u = UShapedTrainer(a1, b1, device=gpu)
-    s = SplitTrainer(a2, b2, device=gpu, graph=False)
+    # the U-shaped client runs its conv1 wgrad as its own launch: compare with the unfused SplitTrainer
+    # (the fused one sums the client gradient in another order; tests/test_x3_gpu.py covers that)
+    s = SplitTrainer(a2, b2, device=gpu, graph=False, fuse_client_backward=False)
     for x, y in batches:
         u.step(x, y)
         s.step(x, y)
