@@ -215,6 +215,10 @@ def run_single(args, out):
                      "global_batch": B, "per_gpu_batch": B, "topology": "fused-1gpu",
                      "graph": not args.no_graph, "conv": conv,
                      "conv2_kernels": {"fwd_pool": fi, "dgrad": di, "wgrad": wi},
+                     "cut_handoff": ("client conv1 writes the x3 split input images (slk_conv1_fwd_x3); no f32 cut"
+                                     if tr.client.emit_act16 else "f32 cut"),
+                     "client_backward": ("fused into the x3 dgrad (slk_conv2_dgrad_x3_c1w); no cut gradient in HBM"
+                                         if tr.fuse_client_backward else "cut gradient -> conv1 wgrad"),
                      "arithmetic": "fp32 tensors, f32 accumulation; conv2 'x3' kernels multiply f32 operands split "
                                    "into f16 hi + lo (3 MFMA products, per-product error <= ~7e-7 relative, "
                                    "checked vs fp64 at the f32 path's bars), 'wino' = Winograd on the f32 MFMA"}
