@@ -125,6 +125,30 @@ constexpr int X3F_IPT = (X3F_ITEMS + X3F_THREADS - 1) / X3F_THREADS;  // 3
 constexpr int X3F_GRID = 256;
 constexpr int X3F_STORES = 6 * X3F_NT;            // epilogue global stores per wave and unit
 static_assert(X3F_RAW % 1024 == 512, "the last DMA wave-instruction is a half piece");
+// act16 images in HBM: per SAMPLE, the whole 26 x 26 cut as an h plane then an l plane ([pixel][32 ci]
+// f16, 64-B pixels, chunk slot c8 ^ (x & 2)), 86,528 B a sample: a unit (sample, third t3) is rows
+// 8 t3 .. 8 t3 + 9 of each plane — two contiguous 16,640-B runs — so no row is stored twice
+constexpr int X3S_PLANE = A_PIX * 64;             // 43,264 B
+constexpr int X3S_SAMPLE = 2 * X3S_PLANE;         // 86,528 B
+constexpr int X3S_UNIT_OFF = 8 * A_HW * 64;       // 13,312 B between consecutive thirds
+static_assert(X3F_PLANE == X3F_ROWS * A_HW * 64 && X3F_PLANE % 1024 == 256, "unit run = 16 KiB + 256 B");
+
+// LDS-DMA of unit uu's image (h run -> lds, l run -> lds + X3F_PLANE) by an 8-wave workgroup: 2 x
+// (16 full 1-KiB wave-instructions + one 256-B quarter), pieces spread over the waves (4 or 5 each)
+__device__ __forceinline__ void x3_issue_unit_img(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
+    const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+    const char* srch = reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t3 * X3S_UNIT_OFF;
+    constexpr int PP = X3F_PLANE / 1024 + 1;  // 17 pieces per plane
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        const int piece = wave + 8 * r;
+        if (piece < 2 * PP) {
+            const int pl = piece >= PP ? 1 : 0, pp = piece - PP * pl;
+            const char* src = srch + pl * X3S_PLANE;
+            if (pp < PP - 1 || lane < 16) glds16_so(src, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3F_PLANE + pp * 1024);
+        }
+    }
+}
 
 __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave, int lane, const uint32_t* voff,
                                               uint32_t raw_lds) {
@@ -141,8 +165,8 @@ __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave
     }
 }
 
-// act16 (optional): every unit's f16 image (h plane | l plane, 33,280 B, the layout above, the
-// sample's own scale) is also written to act16 + u * 33,280 for conv2_wgrad_x3's input operand.
+// act16 (optional): every unit's f16 image (the layout above, the sample's own scale) is also written
+// to the per-sample act16 image (X3S_*) for conv2_wgrad_x3's input operand.
 // IN16 = true: the input IS such an image array (slk_conv1_fwd_x3 wrote it): each unit's image is moved
 // by LDS-DMA two units ahead into a 3-deep ring of f16 buffers — no f32 rows, no split.
 template <bool IN16>
@@ -170,20 +194,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         const int c = g / 65, r = g - (g / 65) * 65;
         voff[k] = (uint32_t)(c * A_PIX * 4 + r * 16);
     }
-    // IN16: unit uu's image (33,280 contiguous bytes) -> ring slot; 32.5 1-KiB wave-instructions
-    auto issue_img = [&](int uu, char* dstp) {
-        const char* src = reinterpret_cast<const char*>(act16) + (size_t)uu * X3F_BUF;
-        const uint32_t dst = lds_u32(dstp);
-#pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const int piece = wave + X3F_WAVES * r;
-            if (piece < X3F_BUF / 1024) {
-                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
-            } else if (piece == X3F_BUF / 1024 && lane < 32) {
-                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
-            }
-        }
-    };
+    // IN16: unit uu's image -> ring slot
+    auto issue_img = [&](int uu, char* dstp) { x3_issue_unit_img(act16, uu, wave, lane, lds_u32(dstp)); };
     if constexpr (IN16) {
         if (u < U) issue_img(u, smem);
         if (u + G < U) issue_img(u + G, smem + X3F_BUF);
@@ -332,11 +344,14 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             if (!IN16 && mt == sph) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
             if (!IN16 && mt == sph && act16) {
                 // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
-                char* dst = reinterpret_cast<char*>(act16) + (size_t)u * X3F_BUF;
+                // (rows 8-9 of a third are rows 0-1 of the next: both units store the same values there)
+                char* dst = reinterpret_cast<char*>(act16) + (size_t)(u / 3) * X3S_SAMPLE + (u - (u / 3) * 3) * X3S_UNIT_OFF;
 #pragma unroll
                 for (int r = 0; r < (X3F_BUF / 16 + X3F_THREADS - 1) / X3F_THREADS; ++r) {
                     const int i = min(tid + r * X3F_THREADS, X3F_BUF / 16 - 1);
-                    *reinterpret_cast<uint4*>(dst + i * 16) = *reinterpret_cast<const uint4*>(cur + i * 16);
+                    const int pl = i >= X3F_PLANE / 16 ? 1 : 0;
+                    *reinterpret_cast<uint4*>(dst + pl * (X3S_PLANE - X3F_PLANE) + i * 16) =
+                        *reinterpret_cast<const uint4*>(cur + i * 16);
                 }
             }
         }
@@ -870,18 +885,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
     // X16 staging: 2,080 16-B pieces per unit, lane-contiguous (the image is stored as it sits in LDS)
     auto issue_x16 = [&](int uu, char* img) {
-        const char* src = reinterpret_cast<const char*>(act16) + (size_t)uu * (2 * X3W_XP);
-        const uint32_t dst = lds_u32(img + 2 * X3W_DYP);
-        const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
-#pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const int piece = wave_ + 8 * r;  // 1 KiB wave-instructions: 32.5 of them
-            if (piece < (2 * X3W_XP) / 1024) {
-                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
-            } else if (piece == (2 * X3W_XP) / 1024 && lane < 32) {
-                glds16_so(src, (uint32_t)(piece * 1024 + lane * 16), dst + piece * 1024);
-            }
-        }
+        x3_issue_unit_img(act16, uu, __builtin_amdgcn_readfirstlane(tid >> 6), lane, lds_u32(img + 2 * X3W_DYP));
     };
     typedef __fp16 hf4 __attribute__((__vector_size__(8)));
     typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
@@ -1050,7 +1054,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 // 2^s, s = x3_exp(max act): bit-identical to the images that kernel writes from the f32 act), and —
 // when act != nullptr — the f32 act too. One workgroup per sample; pass 1 (thread = 4 consecutive
 // pixels, float4 act stores) computes the maximum, pass 2 recomputes (9 FMAs a value) per (pixel,
-// 8-channel chunk) item and splits: rows 8-9 and 16-17 belong to two units and are written twice.
+// 8-channel chunk) item and splits into the per-sample image (each pixel stored once).
 constexpr int C1X_T = 192;
 constexpr int C1X_G = A_PIX / 4;  // 169 active threads
 __global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
@@ -1116,7 +1120,7 @@ __global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __rest
     for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int k = 0; k < 10; ++k) wr[j][k] = ws[(8 * c8 + j) * 10 + k];
-    char* img = reinterpret_cast<char*>(act16) + (size_t)3 * b * X3F_BUF;
+    char* img = reinterpret_cast<char*>(act16) + (size_t)b * X3S_SAMPLE;
 #pragma unroll 2
     for (int i = tid; i < A_PIX * 4; i += C1X_T) {
         const int p = i >> 2;
@@ -1135,17 +1139,9 @@ __global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __rest
         }
         f16x8 hh, ll;
         x3_split8(v, sc, hh, ll);
-        const int slot = (c8 ^ (xx & 2)) * 16;
-        // unit t3 holds rows 8 t3 .. 8 t3 + 9
-#pragma unroll
-        for (int t3 = 0; t3 < 3; ++t3) {
-            const int r = y - 8 * t3;
-            if (r >= 0 && r < X3F_ROWS) {
-                char* o = img + t3 * X3F_BUF + (r * A_HW + xx) * 64 + slot;
-                *reinterpret_cast<f16x8*>(o) = hh;
-                *reinterpret_cast<f16x8*>(o + X3F_PLANE) = ll;
-            }
-        }
+        char* o = img + p * 64 + (c8 ^ (xx & 2)) * 16;
+        *reinterpret_cast<f16x8*>(o) = hh;
+        *reinterpret_cast<f16x8*>(o + X3S_PLANE) = ll;
     }
 }
 
@@ -1166,7 +1162,7 @@ extern "C" int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, c
                        slk_stream(stream), act, act_amax, W2, b2, pooled, code, B, act16);
     return slk_launch_status();
 }
-extern "C" int64_t slk_conv2_act16_bytes(int B) { return B > 0 ? (int64_t)3 * B * X3F_BUF : 0; }
+extern "C" int64_t slk_conv2_act16_bytes(int B) { return B > 0 ? (int64_t)B * X3S_SAMPLE : 0; }
 
 extern "C" int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* W2, const float* b2,
                                      float* pooled, uint8_t* code, int B, void* stream) {

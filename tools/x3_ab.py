@@ -29,6 +29,8 @@ def main():
     act = ClientStage(a, device=dev).forward(x.to(dev)).clone()
     xg = x.to(dev).contiguous()
     W1, b1 = a.conv1.weight.detach().to(dev).contiguous(), a.conv1.bias.detach().to(dev).contiguous()
+    xg = x.to(dev).contiguous()
+    W1, b1 = a.conv1.weight.detach().to(dev).contiguous(), a.conv1.bias.detach().to(dev).contiguous()
     W2, b2 = b.conv2.weight.detach().to(dev).contiguous(), b.conv2.bias.detach().to(dev).contiguous()
     W3, b3 = b.fc1.weight.detach().to(dev).contiguous(), b.fc1.bias.detach().to(dev).contiguous()
     amax = ops.row_amax(act)
@@ -46,16 +48,35 @@ def main():
         for n in ("slk_conv2_fwd_pool_x3s", "slk_conv2_dgrad_x3", "slk_conv2_wgrad_x3s", "slk_conv2_wgrad_x3_nslab"):
             getattr(L, n).restype = ctypes.c_int
         tag = os.path.basename(path).replace(".so", "")
+        # this library's own act16 images (layouts may differ between builds)
+        L.slk_conv2_act16_bytes.restype = ctypes.c_int64
+        L.slk_conv2_act16_bytes.argtypes = [ctypes.c_int]
+        L.slk_conv1_fwd_x3.restype = ctypes.c_int
+        L.slk_conv1_fwd_x3.argtypes = [P] * 6 + [ctypes.c_int, P]
+        a16 = torch.empty(L.slk_conv2_act16_bytes(B), dtype=torch.uint8, device=dev)
+        am1 = torch.empty(B, device=dev)
+        assert L.slk_conv1_fwd_x3(p(xg), p(W1), p(b1), None, p(am1), p(a16), B, st) == 0
+        if "c1x3" in args.ops:
+            i1 = torch.empty_like(a16)
+            cases[f"c1x3 {tag}"] = (lambda L=L, am1=am1, i1=i1: L.slk_conv1_fwd_x3(
+                p(xg), p(W1), p(b1), None, p(am1), p(i1), B, st))
         if "fwd," in args.ops + "," :
             po, co, a16o = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16)
             L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
             cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
                 p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+        if "dgc1" in args.ops:
+            sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
+            L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
+            L.slk_conv2_dgrad_x3_c1w_nslab.restype = ctypes.c_int
+            L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 8 + [ctypes.c_int, P]
+            cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1: L.slk_conv2_dgrad_x3_c1w(
+                p(dp), p(dpa), p(code), p(W2), p(xg), p(W1), p(b1), p(sl), B, st))
         if "fwdi" in args.ops:
             po2, co2 = torch.empty_like(pooled), torch.empty_like(code)
             L.slk_conv2_fwd_pool_x3i.restype = ctypes.c_int
             L.slk_conv2_fwd_pool_x3i.argtypes = [P] * 6 + [ctypes.c_int, P]
-            cases[f"fwdi {tag}"] = (lambda L=L, po=po2, co=co2: L.slk_conv2_fwd_pool_x3i(
+            cases[f"fwdi {tag}"] = (lambda L=L, po=po2, co=co2, a16=a16: L.slk_conv2_fwd_pool_x3i(
                 p(a16), p(amax), p(W2), p(b2), p(po), p(co), B, st))
         if "dgrad" in args.ops:
             g = torch.empty_like(act)
@@ -70,7 +91,7 @@ def main():
         if "wgrad" in args.ops:
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
-            cases[f"wgrad {tag}"] = (lambda L=L, sl=sl: L.slk_conv2_wgrad_x3s(p(a16), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
+            cases[f"wgrad {tag}"] = (lambda L=L, sl=sl, a16=a16: L.slk_conv2_wgrad_x3s(p(a16), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
     times = {k: [] for k in cases}
     for _ in range(3):
         for f in cases.values():
