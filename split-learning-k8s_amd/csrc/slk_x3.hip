@@ -970,7 +970,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     for (; u < U; u += nks, ++k) {
         // X16: this unit's image DMA landed; the 8 dY loads of load_dy, every wave's last memory
         // instructions (issued after its DMA), may stay in flight
-        const bool dfirst = !X16 || (SLK_X3ABL & 64) || tg == 1;
+        const bool dfirst = !X16 || (SLK_X3ABL & 64) || tg == ((SLK_X3ABL & 65536) ? 0 : 1);
         if constexpr (X16) {
             if (SLK_X3ABL & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
