@@ -1057,7 +1057,10 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 // 8-channel chunk) item and splits into the per-sample image (each pixel stored once).
 constexpr int C1X_T = 192;
 constexpr int C1X_G = A_PIX / 4;  // 169 active threads
-__global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
+#ifndef SLK_C1X_WPE
+#define SLK_C1X_WPE 1
+#endif
+__global__ __launch_bounds__(C1X_T, SLK_C1X_WPE) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
                                                              const float* __restrict__ b1, float* __restrict__ act,
                                                              float* __restrict__ act_amax, uint16_t* __restrict__ act16) {
     __shared__ float xs[IN_HW * IN_HW];
