@@ -833,7 +833,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             dv[j] = dpooled[o + j * P_WIN];
             dcb[j] = code[o + j * P_WIN];
         }
-        sb_ld = x3_exp(act_amax[b]);
+        sb_ld = max(x3_exp(act_amax[b]), sx);  // = x3_exp(amax_b) unless amax_b is 0 (zero images: any scale)
     };
     // db[co] = sum of the routed dY = the pooled gradients whose code routes them (code != NONE): summed
     // in f32 from the raw values as they are staged (a thread keeps one (4-co group, window) item)

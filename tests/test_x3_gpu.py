@@ -330,3 +330,32 @@ def test_trainer_fused_client_backward_matches_unfused(gpu):
         out.append((tr.client.params.cpu().numpy() - init[0], tr.server.params.cpu().numpy() - init[1]))
     for u, v in zip(out[0], out[1]):
         assert np.abs(u - v).max() <= 1e-3 * np.abs(v).max(), (np.abs(u - v).max(), np.abs(v).max())
+
+
+def test_x3_zero_samples(gpu):
+    """A sample whose cut is all zeros (amax 0) and one whose pooled gradient is all zeros: every x3
+    kernel stays finite and on the oracle bar (the wgrad's dY compensation must not scale by the zero
+    sample's exponent)."""
+    from oracle.split_step import conv3x3_wgrad, maxpool2_bwd
+    from splitcnn import ops
+    B = 6
+    act, p, y = _inputs(gpu, B, seed=77)
+    act[2] = 0
+    am = ops.row_amax(act)
+    assert float(am[2]) == 0.0
+    a16 = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu)
+    ps, cs = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=am, act16=a16)
+    _, _, _, dp = ops.fc_xent(ps, p["W3"], p["b3"], y, 1.0 / B)
+    dp[4] = 0
+    dpa = ops.row_amax(dp)
+    for s in (ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am, dp_amax=dpa),
+              ops.conv2_wgrad_slabs(None, dp, cs, impl="x3", act_amax=am, dp_amax=dpa, act16=a16)):
+        got = ops.reduce_slabs(s).cpu().numpy()
+        assert np.isfinite(got).all()
+        codes = cs.cpu().numpy().astype(np.int64)
+        dp64 = dp.double().cpu().numpy().reshape(B, 64, 12, 12)
+        dc = maxpool2_bwd(np.where(codes < 4, dp64, 0.0), np.minimum(codes, 3), (B, 64, 24, 24))
+        dW, db = conv3x3_wgrad(act.double().cpu().numpy(), dc)
+        assert rel_err(got[:18432], dW.reshape(-1)) <= 1e-5 and rel_err(got[18432:], db) <= 1e-5
+    g = ops.conv2_dgrad(dp, cs, p["W2"], impl="x3", dp_amax=dpa)
+    assert torch.isfinite(g).all() and float(g[4].abs().max()) == 0.0
