@@ -159,8 +159,9 @@ int slk_conv2_fwd_pool_x3(const float* act, const float* act_amax, const float* 
 int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
                        float* cut_grad, int B, void* stream);
 /* slk_conv2_wgrad on the x3 path: slabs [slk_conv2_wgrad_x3_nslab(B)][18496] = [dW2 | db2] partials
- * (fixed-order sum = the gradient). The operand scales are per launch (max over the batch of act_amax /
- * dp_amax): the reduction spans samples (server_part.py:51). */
+ * (fixed-order sum = the gradient). The reduction spans samples (server_part.py:51), so every product
+ * carries one scale: the input keeps its sample's scale (from act_amax) and that sample's dY is scaled
+ * to compensate (launch maxima of act_amax / dp_amax); db2 is summed in f32. */
 int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
                        const uint8_t* code, float* slabs, int B, void* stream);
 int slk_conv2_wgrad_x3_nslab(int B);
@@ -172,6 +173,8 @@ int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float*
                            uint8_t* code, uint16_t* act16, int B, void* stream);
 int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled, const float* dp_amax,
                         const uint8_t* code, float* slabs, int B, void* stream);
+/* act16 layout: per sample an h plane then an l plane, each [26 x 26 pixels][32 ci] f16 with 64-B pixels
+ * (8-channel chunk c8 at slot c8 ^ (x & 2)): B x 86,528 bytes. */
 int64_t slk_conv2_act16_bytes(int B);
 
 /* The client's conv1 + ReLU (replaces slk_conv1_fwd_amax inside a fused step, src/client_part.py:114)
