@@ -288,7 +288,7 @@ class ServerStage:
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
         W3, b3 = m.fc1.weight.detach(), m.fc1.bias.detach()
         fi, di, wi = self.impl_fwd, self.impl_dgrad, self.impl_wgrad
-        if act16 is not None and (fi, wi) != ("x3", "x3") or act16 is not None and act_amax is None:
+        if act16 is not None and ((fi, wi) != ("x3", "x3") or act_amax is None):
             raise ValueError("act16 input needs the x3 forward and wgrad (conv preset 'x3') and act_amax")
         if act_amax is None and "x3" in (fi, wi):
             with TIMER("act_amax"):
