@@ -173,3 +173,19 @@ def test_custom_op_fake_kernels_shapes():
     for k, shp in want.items():
         assert tuple(got[k].shape) == shp, k
         assert got[k].dtype == (torch.uint8 if k == "code" else torch.float32), k
+
+
+def test_fused_step_preconditions_without_gpu():
+    """The split-image and fused-client-backward paths refuse configurations they cannot serve before
+    touching a kernel: client images need the x3 forward AND wgrad plus act_amax; the wrappers need
+    act16 / act_amax when act is None; conv presets name their kernels."""
+    from splitcnn import ops
+    from splitcnn.engine import CONV_PRESETS, ServerStage
+    assert CONV_PRESETS["x3"] == ("x3", "x3", "x3") and CONV_PRESETS["f32"] == ("wino", "wino", "wino")
+    y = torch.zeros(3, dtype=torch.int64)
+    img = torch.empty(1, dtype=torch.uint8)
+    for conv, amax in (("f32", torch.zeros(3)), ("x3w", torch.zeros(3)), ("x3", None)):
+        with pytest.raises(ValueError, match="act16 input needs"):
+            ServerStage(device="cpu", conv=conv).forward_backward(None, y, 1.0, act_amax=amax, act16=img)
+    with pytest.raises(ValueError, match="act=None needs"):
+        ops.conv2_wgrad_slabs(None, torch.zeros(3, 9216), torch.zeros(3, 64, 12, 12, dtype=torch.uint8), impl="x3")
