@@ -684,7 +684,10 @@ __global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
 // fc1 weight gradient partials. Grid (9 column blocks of 1024, nsplit batch slices). Thread t owns
 // the 4 columns 4*(blockIdx.x*256 + t) .. +3 and sums its slice of the batch in order, 8 samples'
 // float4 rows in flight; db3 comes from column block 0. dlogits are wave-uniform scalar loads.
-constexpr int FCW_MAXSPLIT = 64;
+#ifndef SLK_FCW_MAXSPLIT
+#define SLK_FCW_MAXSPLIT 64
+#endif
+constexpr int FCW_MAXSPLIT = SLK_FCW_MAXSPLIT;
 constexpr int FCW_SLAB = W3_N + NCLS;  // 92170
 __global__ __launch_bounds__(256) void fc_wgrad_kernel(const float* __restrict__ dlogits,
                                                        const float* __restrict__ pooled,
