@@ -1,0 +1,53 @@
+"""Profiling only: K2 SplitTrainer variants (engine attributes) captured as HIP graphs and timed
+interleaved in ONE process, B = 4096. usage: python tools/ab_trainers.py [--rounds 8]
+Variants: base; fcw_early (ServerStage.fc_wgrad_early); wg_first (ServerStage.wgrad_first)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "split-learning-k8s_amd"), ROOT]
+
+import torch  # noqa: E402
+
+from bench import make_pool  # noqa: E402
+from splitcnn.data import init_models  # noqa: E402
+from splitcnn.engine import SplitTrainer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    B = 4096
+    dev = torch.device("cuda:0")
+    X, Y = make_pool(B, 4, dev)
+    variants = {}
+    for name in ("base", "fcw_early", "wg_first"):
+        tr = SplitTrainer(*init_models(seed=0), device=dev, graph=True)
+        if name == "fcw_early":
+            tr.server.fc_wgrad_early = True
+        if name == "wg_first":
+            tr.server.wgrad_first = True
+        for i in range(5):
+            tr.step(X[i % 4], Y[i % 4])
+        variants[name] = tr
+    times = {k: [] for k in variants}
+    for _ in range(args.rounds):
+        for k, tr in variants.items():
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(args.steps):
+                tr.step(X[i % 4], Y[i % 4])
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) / args.steps)
+    for k, v in times.items():
+        v.sort()
+        print(f"{k:10s} median {v[len(v) // 2]:.4f} ms/step  min {v[0]:.4f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
