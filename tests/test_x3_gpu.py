@@ -359,3 +359,48 @@ def test_x3_zero_samples(gpu):
         assert rel_err(got[:18432], dW.reshape(-1)) <= 1e-5 and rel_err(got[18432:], db) <= 1e-5
     g = ops.conv2_dgrad(dp, cs, p["W2"], impl="x3", dp_amax=dpa)
     assert torch.isfinite(g).all() and float(g[4].abs().max()) == 0.0
+
+
+def test_default_fused_path_full_size_vs_direct_f32(gpu):
+    """K2 size (B = 4096: every persistent x3 workgroup runs its full unit stream): the default step's
+    kernels — conv1 images, forward from images, fused dgrad + client backward, wgrad from images —
+    against the independent direct f32-MFMA kernels on the same inputs (themselves checked vs fp64 in
+    test_wino_gpu.py): 1e-5 of max |ref|, routing differences only where the two pooled maxima tie.
+    Run twice: bit-identical (fixed summation orders)."""
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    B = 4096
+    a, b = init_models(seed=51)
+    x, y = SyntheticMNIST(52).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
+    W2, b2 = b.conv2.weight.detach().to(gpu), b.conv2.bias.detach().to(gpu)
+    W3, b3 = b.fc1.weight.detach().to(gpu), b.fc1.bias.detach().to(gpu)
+
+    def fused():
+        am = torch.empty(B, device=gpu)
+        img = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu)
+        ops.conv1_fwd_x3(x, W1, b1, am, img)
+        pooled, code = ops.conv2_fwd_pool_x3i(img, am, W2, b2)
+        dpa = torch.empty(B, device=gpu)
+        _, _, _, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+        c1 = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, code, W2, x, W1, b1, dp_amax=dpa))
+        s2 = ops.reduce_slabs(ops.conv2_wgrad_slabs(None, dp, code, impl="x3", act_amax=am, dp_amax=dpa, act16=img))
+        return pooled, code, dp, c1, s2
+
+    r1, r2 = fused(), fused()
+    for u, v in zip(r1, r2):
+        assert torch.equal(u, v)
+    pooled, code, dp, c1, s2 = r1
+    act = ops.conv1_fwd(x, W1, b1)
+    pd, cd = ops.conv2_fwd_pool(act, W2, b2, impl="direct")
+    same = code == cd
+    assert same.float().mean().item() > 0.9999
+    assert rel_err(pooled[same].cpu().numpy(), pd[same].cpu().numpy()) <= 1e-5
+    # backward references on the SAME routing (the x3 forward's code) through the f32 direct kernels
+    g = ops.conv2_dgrad(dp, code, W2, impl="direct")
+    c1ref = ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, g)).cpu().numpy()
+    s2ref = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, code, impl="direct")).cpu().numpy()
+    c1, s2 = c1.cpu().numpy(), s2.cpu().numpy()
+    for got, ref in ((c1[:288], c1ref[:288]), (c1[288:], c1ref[288:]), (s2[:18432], s2ref[:18432]), (s2[18432:], s2ref[18432:])):
+        assert rel_err(got, ref) <= 1e-5, rel_err(got, ref)
