@@ -237,6 +237,10 @@ def run_single(args, out):
         kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)
         out["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
         out["roofline"] = roofline_from(kern, B, {"conv2_fwd_pool": fi, "conv2_dgrad": di, "conv2_wgrad": wi})
+        if tr2.fuse_client_backward and out["roofline"].get("kernel") == "conv2_dgrad":
+            out["roofline"]["note"] = ("conv2_dgrad here also runs the client's ReLU backward + conv1 wgrad in its "
+                                       "epilogue (slk_conv2_dgrad_x3_c1w); those FLOPs are not counted, its "
+                                       "time is; traffic = the fused launch's PMC bytes")
     if conv == "f32":  # every conv2 FLOP on the f32 MFMA: one peak prices the whole step
         out["step_roofline_frac"] = round(out["value"] * STEP_FLOP_EXECUTED / (FP32_PEAK_TFLOPS * 1e12), 4)
     out["step_direct_equivalent_tflops"] = round(out["value"] * FLOP_PER_SAMPLE / 1e12, 2)
