@@ -741,6 +741,7 @@ constexpr int X3W_NKS = 128;                         // K shares (slabs)
 constexpr int X3W_XITEMS = 260 * 4;                  // (pixel, 8-channel group) input items per unit
 constexpr int X3W_XR = (X3W_XITEMS + X3W_THREADS - 1) / X3W_THREADS;  // 3 (the last partial)
 constexpr int X3W_DYITEMS = 48 * 8;                  // (window, 4-co group) dY items per unit
+static_assert(X3W_DYITEMS % 64 == 0, "whole waves of dY items");
 static_assert(2 * X3W_BUF <= 163840, "LDS");
 
 // X16 = true: the input image of a unit is the f16 image conv2_fwd_pool_x3 wrote (act16, launch-max
@@ -971,8 +972,11 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // X16: this unit's image DMA landed; the 8 dY loads of load_dy, every wave's last memory
         // instructions (issued after its DMA), may stay in flight
         const bool dfirst = !X16 || (SLK_X3ABL & 64) || tg == ((SLK_X3ABL & 65536) ? 0 : 1);
+        // X16: waves 6-7 hold no dY item (384 items = waves 0-5) and skip the routing (no redundant
+        // redo of item 383); their last memory instructions are then the DMA itself
+        const bool dstage = !(X16 && wave >= X3W_DYITEMS / 64) || (SLK_X3ABL & 131072);
         if constexpr (X16) {
-            if (SLK_X3ABL & 32) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((SLK_X3ABL & 32) || !dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
@@ -986,19 +990,19 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // waves after theirs, so the two waves of a SIMD overlap routing with MFMAs. store_dy goes before
         // the DMA issue: the compiler does not count the asm DMAs, so its wait for the dY registers
         // would otherwise also wait for the DMA just issued
-        if (!(SLK_X3ABL & 32) && dfirst) store_dy(nimg, nx < U);
+        if (!(SLK_X3ABL & 32) && dfirst && dstage) store_dy(nimg, nx < U);
         if constexpr (X16) {
             issue_x16(min(nx, U - 1), nimg);
         } else {
             split_x(nimg);
         }
-        if (!(SLK_X3ABL & 32) && dfirst) {
+        if (!(SLK_X3ABL & 32) && dfirst && dstage) {
             if constexpr (!X16) load_x(min(nx2, U - 1));
             load_dy(min(nx2, U - 1));
         }
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
-        if (!(SLK_X3ABL & 32) && !dfirst) {
+        if (!(SLK_X3ABL & 32) && !dfirst && dstage) {
             store_dy(nimg, nx < U);
             load_dy(min(nx2, U - 1));
         }
