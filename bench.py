@@ -72,9 +72,9 @@ def parse():
     ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
     ap.add_argument("--k5-batch", type=int, default=4096)
     ap.add_argument("--conv", default=None, choices=["x3", "x3w", "f32"],
-                    help="K2 conv2 kernels: x3 = f16 MFMA with hi/lo-split fp32 operands (fwd, dgrad) + "
-                         "Winograd wgrad; f32 = Winograd F(2x2,3x3) on the f32 MFMA throughout "
-                         "(default: splitcnn.engine.CONV_DEFAULT)")
+                    help="K2 conv2 kernels: x3 = f16 MFMA with hi/lo-split fp32 operands for the forward, dgrad "
+                         "and wgrad; x3w = x3 forward + dgrad with the Winograd f32 wgrad; f32 = Winograd "
+                         "F(2x2,3x3) on the f32 MFMA throughout (default: splitcnn.engine.CONV_DEFAULT)")
     ap.add_argument("--no-conv-compare", action="store_true",
                     help="skip the short run of the other conv preset reported beside the headline")
     return ap.parse_args()
@@ -162,6 +162,37 @@ def pmc_traffic(name, B):
         return None
 
 
+# Algorithmic HBM bytes per sample of each conv2 launch as the default fused step runs it (the minimum
+# each must move: inputs read once, outputs written once):
+#   fwd (x3i):  act16 images 86,528 read + pooled 36,864 + code 9,216 written
+#   dgrad:      dpooled 36,864 + code 9,216 read (+ x 3,136 read when the client backward is fused into it,
+#               + the cut gradient 86,528 written when it is not)
+#   wgrad (x3s): act16 86,528 + dpooled 36,864 + code 9,216 read
+ALGO_BYTES = {"conv2_fwd_pool": 132_608, "conv2_dgrad": 46_080, "conv2_wgrad": 132_608}
+# kernel symbols in rocprofv3's --stats summary, per (TIMER name, variant)
+ROCPROF_SYMBOL = {("conv2_dgrad", "x3_fused"): "conv2_dgrad_x3_kernel<true>",
+                  ("conv2_dgrad", "x3"): "conv2_dgrad_x3_kernel<false>",
+                  ("conv2_fwd_pool", "x3_images"): "conv2_fwd_pool_x3_kernel<true>",
+                  ("conv2_wgrad", "x3_images"): "conv2_wgrad_x3_kernel<true>"}
+
+
+def rocprof_avg(symbol, pattern="kernel_stats_k2.csv"):
+    """Average duration (ms) of `symbol` in the newest committed rocprofv3 --stats summary under
+    profiles/ (the same bench command under the profiler), or None."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + pattern)), key=os.path.getmtime)
+    files = [f for f in files if os.path.basename(f).startswith("r03")] or files
+    for f in reversed(files):
+        try:
+            for row in csv.DictReader(open(f)):
+                if symbol in row["Name"]:
+                    return round(float(row["AverageNs"]) / 1e6, 4), os.path.relpath(f, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
+
+
 def conv_roofline(name, avg_ms, B, impl):
     """Roofline of one conv2 launch. wino: its transform-domain GEMM FLOPs on the f32 MFMA peak; x3: the
     f16 MFMA FLOPs it executes (3 products per direct-conv multiply-add) on the dense f16 peak."""
@@ -180,13 +211,26 @@ def conv_roofline(name, avg_ms, B, impl):
             "direct_conv_equivalent_tflops": round(direct_eq, 2)}
 
 
-def roofline_from(kern, B, impls=None):
+def roofline_from(kern, B, impls=None, variants=None):
     conv = {k: v for k, v in kern.items() if k.startswith("conv2_")}
     if not conv:
         return None
     impls = impls or {}
     name = max(conv, key=lambda k: conv[k]["avg_ms"])
     r = conv_roofline(name, conv[name]["avg_ms"], B, impls.get(name, "wino"))
+    variant = (variants or {}).get(name)
+    if variant is not None:
+        algo = ALGO_BYTES[name] * B
+        if name == "conv2_dgrad":
+            algo += (3_136 if variant == "x3_fused" else 86_528) * B
+        r["traffic_algorithmic"] = algo
+        r["traffic_ratio"] = round(r["traffic"] / algo, 3) if r.get("traffic") else None
+        sym = ROCPROF_SYMBOL.get((name, variant))
+        if sym:
+            ms, src = rocprof_avg(sym)
+            r["rocprof_avg_ms"] = ms
+            r["rocprof_source"] = src
+            r["hip_event_avg_ms"] = r["avg_ms"]
     r["per_kernel"] = {k: {kk: conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino"))[kk]
                            for kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops")}
                        for k, v in conv.items()}
@@ -223,24 +267,37 @@ def run_single(args, out):
                                    "into f16 hi + lo (3 MFMA products, per-product error <= ~7e-7 relative, "
                                    "checked vs fp64 at the f32 path's bars), 'wino' = Winograd on the f32 MFMA"}
     out["loss_first_last"] = [round(losses[0][1], 5), round(losses[-1][1], 5)] if losses else None
+    if not args.no_kernel_pass:
+        # (before the preset comparison: the headline's roofline must not depend on the other presets)
+        try:
+            tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False, conv=conv)
+            kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)
+            out["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
+            variants = {"conv2_dgrad": ("x3_fused" if tr2.fuse_client_backward else di),
+                        "conv2_fwd_pool": ("x3_images" if tr2.client.emit_act16 else fi),
+                        "conv2_wgrad": ("x3_images" if tr2.client.emit_act16 else wi)}
+            out["roofline"] = roofline_from(kern, B, {"conv2_fwd_pool": fi, "conv2_dgrad": di, "conv2_wgrad": wi},
+                                            variants)
+            if tr2.fuse_client_backward and out["roofline"].get("kernel") == "conv2_dgrad":
+                out["roofline"]["note"] = ("conv2_dgrad here also runs the client's ReLU backward + conv1 wgrad in "
+                                           "its epilogue (slk_conv2_dgrad_x3_c1w); those FLOPs are not counted, its "
+                                           "time is; traffic = the fused launch's PMC bytes (profiles/traffic.json), "
+                                           "traffic_algorithmic = dpooled + code + x read once")
+            del tr2
+        except Exception as e:  # the headline stands on its own
+            out["roofline"] = {"error": repr(e)[:300]}
     if not args.no_conv_compare:
         out["conv_presets"] = {conv: round(out["value"], 1)}
         for other in CONV_PRESETS:
             if other == conv:
                 continue
-            tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
-            dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
-            out["conv_presets"][other] = round(args.steps * B / dto, 1)
-            del tro
-    if not args.no_kernel_pass:
-        tr2 = SplitTrainer(*init_models(seed=0), device=dev, graph=False, conv=conv)
-        kern = kernel_pass(lambda i: tr2.step(X[i % 4], Y[i % 4]), max(3, min(args.steps, 10)), dev)
-        out["kernels"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
-        out["roofline"] = roofline_from(kern, B, {"conv2_fwd_pool": fi, "conv2_dgrad": di, "conv2_wgrad": wi})
-        if tr2.fuse_client_backward and out["roofline"].get("kernel") == "conv2_dgrad":
-            out["roofline"]["note"] = ("conv2_dgrad here also runs the client's ReLU backward + conv1 wgrad in its "
-                                       "epilogue (slk_conv2_dgrad_x3_c1w); those FLOPs are not counted, its "
-                                       "time is; traffic = the fused launch's PMC bytes")
+            try:
+                tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
+                dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
+                out["conv_presets"][other] = round(args.steps * B / dto, 1)
+                del tro
+            except Exception as e:  # reported, never fatal to the headline
+                out["conv_presets"][other] = {"error": repr(e)[:300]}
     if conv == "f32":  # every conv2 FLOP on the f32 MFMA: one peak prices the whole step
         out["step_roofline_frac"] = round(out["value"] * STEP_FLOP_EXECUTED / (FP32_PEAK_TFLOPS * 1e12), 4)
     out["step_direct_equivalent_tflops"] = round(out["value"] * FLOP_PER_SAMPLE / 1e12, 2)

@@ -25,8 +25,13 @@
  *   - Flat parameter blocks (what the fused SGD updates in one launch):
  *       client: [W1 (288) | b1 (32)]                     = SLK_CLIENT_NPARAM floats
  *       server: [W2 (18432) | b2 (64) | W3 (92160) | b3 (10)] = SLK_SERVER_NPARAM floats
- *   - Arithmetic is fp32 throughout (the reference's dtype); weight-gradient reductions use
- *     per-workgroup slabs summed in a fixed order, so every result is run-to-run bit-stable.
+ *   - Tensors, parameters, accumulators and every non-conv2 kernel are fp32 (the reference's dtype).
+ *     conv2's products come in two forms: the f32 MFMA (Winograd slk_conv2_*, direct slk_conv2_*_direct)
+ *     and "x3" (slk_conv2_*_x3*, the default fused step's): each f32 operand is scaled by an exact power
+ *     of two and split into f16 hi + lo, and a product is hi*hi + hi*lo + lo*hi on the f16 MFMA with
+ *     f32 accumulation (per-product error <= ~7e-7 relative; tested against fp64 at the f32 path's bars).
+ *     Weight-gradient reductions use per-workgroup slabs summed in a fixed order, so every result is
+ *     run-to-run bit-stable.
  */
 #ifndef SLK_H
 #define SLK_H

@@ -111,13 +111,16 @@ __global__ __launch_bounds__(256) void cut_move_kernel(uint32_t* __restrict__ x,
     }
 }
 
+// int32 offsets: one micro-batch of at most 2^31 - 1 elements (99,273 reference cut samples)
+constexpr int64_t CUT_NMAX = 2147483647;
+
 static inline int cut_blocks(int64_t n) { return (int)((n + CB - 1) / CB); }
 
-extern "C" int slk_cut_blocks(int64_t n) { return n > 0 ? cut_blocks(n) : 0; }
+extern "C" int slk_cut_blocks(int64_t n) { return n > 0 && n <= CUT_NMAX ? cut_blocks(n) : 0; }
 
 extern "C" int slk_cut_encode(const float* x, int64_t n, uint32_t* mask, int* counts, int* offsets, int* total,
                               float* vals, void* stream) {
-    SLK_CHECK_ARG(n >= 0);
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX);  // offsets, counts and the total are int32
     if (n == 0) return 0;   // empty tensors carry null pointers
     SLK_CHECK_ARG(x && mask && counts && offsets && total && vals);
     const int nb = cut_blocks(n);
@@ -130,7 +133,7 @@ extern "C" int slk_cut_encode(const float* x, int64_t n, uint32_t* mask, int* co
 }
 
 extern "C" int slk_cut_offsets(const uint32_t* mask, int64_t n, int* counts, int* offsets, int* total, void* stream) {
-    SLK_CHECK_ARG(n >= 0);
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX);  // offsets, counts and the total are int32
     if (n == 0) return 0;   // empty tensors carry null pointers
     SLK_CHECK_ARG(mask && counts && offsets && total);
     const int nb = cut_blocks(n);
@@ -141,7 +144,7 @@ extern "C" int slk_cut_offsets(const uint32_t* mask, int64_t n, int* counts, int
 }
 
 extern "C" int slk_cut_pack(const float* x, int64_t n, const uint32_t* mask, const int* offsets, float* vals, void* stream) {
-    SLK_CHECK_ARG(n >= 0);
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX);  // offsets, counts and the total are int32
     if (n == 0) return 0;   // empty tensors carry null pointers
     SLK_CHECK_ARG(x && mask && offsets && vals);
     hipLaunchKernelGGL(cut_move_kernel<true>, dim3(cut_blocks(n)), dim3(256), 0, slk_stream(stream),
@@ -151,7 +154,7 @@ extern "C" int slk_cut_pack(const float* x, int64_t n, const uint32_t* mask, con
 }
 
 extern "C" int slk_cut_unpack(const float* vals, int64_t n, const uint32_t* mask, const int* offsets, float* x, void* stream) {
-    SLK_CHECK_ARG(n >= 0);
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX);  // offsets, counts and the total are int32
     if (n == 0) return 0;   // empty tensors carry null pointers
     SLK_CHECK_ARG(x && mask && offsets && vals);
     hipLaunchKernelGGL(cut_move_kernel<false>, dim3(cut_blocks(n)), dim3(256), 0, slk_stream(stream),

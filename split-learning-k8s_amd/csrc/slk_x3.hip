@@ -23,22 +23,22 @@ using namespace slk;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-#ifndef SLK_X3ABL
-#define SLK_X3ABL 0  // profiling-only ablation bits (wrong results): see the dgrad kernel
-#endif
-#ifndef SLK_X3D_STG
-#define SLK_X3D_STG 0
-#endif
-
 namespace {
 
 // s such that amax * 2^s < 2^14 (amax in [2^13, 2^14) after scaling); 0 for zero / non-finite amax.
+// Clamped to X3_SMAX so that 2^s and 2^-s are both normal floats: a sample whose max is below
+// 2^(14 - X3_SMAX) (~2^-112, e.g. the subnormal dpooled of a confidently-correct sample) lands lower in
+// f16's range instead of being scaled by inf. Every unscale multiplies by 2^-s of each operand in turn
+// (x3_unscale), never by 2^-(s1 + s2), so it stays finite and exact.
+constexpr int X3_SMAX = 126;
 __device__ __forceinline__ int x3_exp(float amax) {
     if (!(amax > 0.f) || !__builtin_isfinite(amax)) return 0;
     int e;
     (void)frexpf(amax, &e);  // amax = m * 2^e, m in [0.5, 1)
-    return 14 - e;
+    return min(14 - e, X3_SMAX);
 }
+// 2^-s1 * 2^-s2 applied as two exact power-of-two multiplies (each factor a normal float)
+__device__ __forceinline__ float x3_unscale(float v, float u1, float u2) { return (v * u1) * u2; }
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     __syncthreads();
     if (!IN16 && u < U) split_unit(u, raw0, smem);
     int k = 0;
-    const int sph = (SLK_X3ABL & 512) ? 7 : (SLK_X3ABL & 256) ? 0 : (wave >= 4 ? 0 : ((SLK_X3ABL & 1024) ? 2 : 1));
+    const int sph = wave >= 4 ? 0 : 1;
 #pragma unroll 1
     for (; u < U; u += G, ++k) {
         const int cb = k & 1;
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         }
         const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
         f32x4 acc[3][X3F_NT];
-        if constexpr (IN16 && !(SLK_X3ABL & 2048)) {
+        if constexpr (IN16) {
             // no staging in the loop: all 27 (M tile, tap) steps in one stream, A fragments read through
             // a 3-slot ring two steps ahead
 #pragma unroll
@@ -316,15 +316,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
                     acc[mt][nt] = mfma_x3(fh[st % 3], fl[st % 3], wh[nt][tap], wl[nt][tap], acc[mt][nt]);
             }
             // (measured: leaving the order to the compiler beats pinning it with sched_group_barrier,
-            // 0.243 vs 0.275 ms, and the pre-ring loop 0.260; SLK_X3ABL & 4096 pins it)
-            if (SLK_X3ABL & 4096) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-                for (int st = 0; st < 27; ++st) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-                    if (st + 2 < 27) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                }
-            }
+            // 0.243 vs 0.275 ms, and the pre-ring loop 0.260)
         } else
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
@@ -357,7 +349,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         }
         // epilogue: unscale (exact), bias, ReLU, 2x2 max-pool, routing code
         const int b = u / 3, t3 = u - (u / 3) * 3;
-        const float us = ldexpf(1.f, -(sexp(b) + sw));
+        const float us1 = ldexpf(1.f, -sexp(b)), us2 = ldexpf(1.f, -sw);
         const int wy = 4 * t3 + wr;
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
@@ -369,7 +361,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
                 int idx = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    float v = acc[mt][nt][q] * us + bias[nt];
+                    float v = x3_unscale(acc[mt][nt][q], us1, us2) + bias[nt];
                     v = v > 0.f ? v : 0.f;
                     if (v > m) { m = v; idx = q; }
                 }
@@ -469,16 +461,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 
     // expansion items of a unit: i = tid + 512 r -> 4-co group c4 = i & 7, window wi = i >> 3 (row-major
     // over the part's image window rows); rows outside 0..11 expand to zeros
-    // SLK_X3D_STG = 1: only waves 4-7 stage (3 items each), waves 0-3 run MFMAs only
-    constexpr int STG = SLK_X3D_STG;
-    constexpr int NR = STG ? 3 : 2, SSTR = STG ? 256 : X3D_THREADS;
+    constexpr int NR = 2, SSTR = X3D_THREADS;
     static_assert(NR * SSTR >= X3D_ITEMS_MAX, "staging items");
-    const int stid = STG ? tid - 256 : tid;
+    const int stid = tid;
     float dv[NR][4];
     uint32_t dcb[NR][4];
     float ld_amax = 0.f;
     auto load_dy = [&](int uu) {
-        if (STG && wave < 4) return;
         const int b = uu / 6, rr = uu - (uu / 6) * 6, pt = rr >> 1, h = rr & 1;
         ld_amax = amax[b];  // used by the store_dy of this unit (one unit later)
         const int wr0 = x3d_ybase(pt) / 2, nwr = x3d_nwr(pt);
@@ -505,7 +494,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         }
     };
     auto store_dy = [&](int uu, char* img) {
-        if (STG && wave < 4) return;
         const int pt = (uu - (uu / 6) * 6) >> 1;
         const int nwr = x3d_nwr(pt);
         const float sc = ldexpf(1.f, x3_exp(ld_amax));
@@ -590,11 +578,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // read pair per 3 dependent MFMAs: waiting on each read left the SIMD half idle)
             const char* abw = img + cbase + ((T0 + g) * 16 + n16) * X3D_REC + kc * 16;
             auto rd = [&](int i, int tap, f16x8& fh, f16x8& fl) {
-                if (SLK_X3ABL & 2) {  // operands from registers (timing only)
-                    fh = wh[1][tap];
-                    fl = wl[1][(tap + i) % 9];
-                    return;
-                }
                 const char* ab = abw + i * 64 * X3D_REC + (54 - 26 * (tap / 3) - tap % 3) * X3D_REC;
                 fh = *reinterpret_cast<const f16x8*>(ab);
                 fl = *reinterpret_cast<const f16x8*>(ab + 64);
@@ -602,9 +585,8 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused).
             // Half the waves stage before their MFMAs, half after, so the two waves of a SIMD overlap
             // one's staging with the other's MFMAs (both staging at once left the SIMD's MFMA idle).
-            const bool sfirst = (SLK_X3ABL & 8) ? (wave & 1) : ((SLK_X3ABL & 16) ? false : wave >= 4);
-            // (SLK_X3D_STG: store_dy/load_dy return at once on waves 0-3)
-            if (!(SLK_X3ABL & 1) && sfirst) {
+            const bool sfirst = wave >= 4;
+            if (sfirst) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
@@ -619,19 +601,17 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 acc[i] = mfma_x3(fh[st & 3], fl[st & 3], wh[h][tap], wl[h][tap], acc[i]);
             }
             // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
-            if (!(SLK_X3ABL & 8192)) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-                for (int st = 0; st < NS; ++st) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-                    if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                }
+            for (int st = 0; st < NS; ++st) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
-            if (!(SLK_X3ABL & 1) && !sfirst) {
+            if (!sfirst) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
-            if (!(SLK_X3ABL & 4) && T0 + g + 12 < T1) {
+            if (T0 + g + 12 < T1) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) rd(3, q, fh[q], fl[q]);
 #pragma unroll
@@ -639,18 +619,16 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     if (tap + 3 < 9) rd(3, tap + 3, fh[(tap + 3) & 3], fl[(tap + 3) & 3]);
                     acc[3] = mfma_x3(fh[tap & 3], fl[tap & 3], wh[h][tap], wl[h][tap], acc[3]);
                 }
-                if (!(SLK_X3ABL & 8192)) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
+                __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
 #pragma unroll
-                    for (int tap = 0; tap < 9; ++tap) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
-                        if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-                    }
+                for (int tap = 0; tap < 9; ++tap) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
+                    if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
                 }
             }
         }
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
-        const float us = ldexpf(1.f, -(x3_exp(amax_b) + sw));
+        const float us1 = ldexpf(1.f, -x3_exp(amax_b)), us2 = ldexpf(1.f, -sw);
         if constexpr (C1W) {
             // client ReLU backward + conv1 wgrad for this lane's ci and pixels (the cut gradient g is the
             // value the store below would write)
@@ -674,7 +652,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 #pragma unroll
                         for (int kk = 0; kk < 9; ++kk) sum = fmaf(xv[kk], wk[kk], sum);
                         sum += wk[9];
-                        const float gm = sum > 0.f ? acc[i][r] * us : 0.f;
+                        const float gm = sum > 0.f ? x3_unscale(acc[i][r], us1, us2) : 0.f;
 #pragma unroll
                         for (int kk = 0; kk < 9; ++kk) c1acc[kk] = fmaf(gm, xv[kk], c1acc[kk]);
                         c1acc[9] += gm;
@@ -687,7 +665,9 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             for (int i = 0; i < X3D_MPW; ++i) {
                 const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
                 if (t < T1 && p < A_PIX)
-                    *reinterpret_cast<float4*>(gb + p) = make_float4(acc[i][0] * us, acc[i][1] * us, acc[i][2] * us, acc[i][3] * us);
+                    *reinterpret_cast<float4*>(gb + p) =
+                        make_float4(x3_unscale(acc[i][0], us1, us2), x3_unscale(acc[i][1], us1, us2),
+                                    x3_unscale(acc[i][2], us1, us2), x3_unscale(acc[i][3], us1, us2));
             }
         }
         ++q;
@@ -744,8 +724,8 @@ constexpr int X3W_DYITEMS = 48 * 8;                  // (window, 4-co group) dY 
 static_assert(X3W_DYITEMS % 64 == 0, "whole waves of dY items");
 static_assert(2 * X3W_BUF <= 163840, "LDS");
 
-// X16 = true: the input image of a unit is the f16 image conv2_fwd_pool_x3 wrote (act16, launch-max
-// scale, chunk slot kc ^ (x & 2), i.e. the 32-B ci-half slot h ^ ((x >> 1) & 1)), moved by LDS-DMA
+// X16 = true: the input image of a unit is the f16 image conv2_fwd_pool_x3 / conv1_fwd_x3 wrote (act16,
+// per-sample scale 2^s_b, dY compensated by 2^(sd + sx - s_b) as above; chunk slot kc ^ (x & 2), i.e. the 32-B ci-half slot h ^ ((x >> 1) & 1)), moved by LDS-DMA
 // one unit ahead straight into the image buffer: no gather loads, no split VALU.
 template <bool X16>
 __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
@@ -940,15 +920,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             for (int mi = 0; mi < 2; ++mi)
                 acc[mi][t] = mfma_x3(Ah[j & 1][mi], Al[j & 1][mi], Bh[n % 3], Bl[n % 3], acc[mi][t]);
         }
-        if (!(SLK_X3ABL & 16384)) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
-            for (int n = 0; n < N; ++n) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-                if (n + 2 < N) {
-                    if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-                    else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                }
+        for (int n = 0; n < N; ++n) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            if (n + 2 < N) {
+                if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
             }
         }
     };
@@ -971,12 +949,12 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     for (; u < U; u += nks, ++k) {
         // X16: this unit's image DMA landed; the 8 dY loads of load_dy, every wave's last memory
         // instructions (issued after its DMA), may stay in flight
-        const bool dfirst = !X16 || (SLK_X3ABL & 64) || tg == ((SLK_X3ABL & 65536) ? 0 : 1);
+        const bool dfirst = !X16 || tg == 1;
         // X16: waves 6-7 hold no dY item (384 items = waves 0-5) and skip the routing (no redundant
         // redo of item 383); their last memory instructions are then the DMA itself
-        const bool dstage = !(X16 && wave >= X3W_DYITEMS / 64) || (SLK_X3ABL & 131072);
+        const bool dstage = !(X16 && wave >= X3W_DYITEMS / 64);
         if constexpr (X16) {
-            if ((SLK_X3ABL & 32) || !dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
@@ -990,19 +968,19 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // waves after theirs, so the two waves of a SIMD overlap routing with MFMAs. store_dy goes before
         // the DMA issue: the compiler does not count the asm DMAs, so its wait for the dY registers
         // would otherwise also wait for the DMA just issued
-        if (!(SLK_X3ABL & 32) && dfirst && dstage) store_dy(nimg, nx < U);
+        if (dfirst && dstage) store_dy(nimg, nx < U);
         if constexpr (X16) {
             issue_x16(min(nx, U - 1), nimg);
         } else {
             split_x(nimg);
         }
-        if (!(SLK_X3ABL & 32) && dfirst && dstage) {
+        if (dfirst && dstage) {
             if constexpr (!X16) load_x(min(nx2, U - 1));
             load_dy(min(nx2, U - 1));
         }
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
-        if (!(SLK_X3ABL & 32) && !dfirst && dstage) {
+        if (!dfirst && dstage) {
             store_dy(nimg, nx < U);
             load_dy(min(nx2, U - 1));
         }
@@ -1033,7 +1011,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         slabs[(size_t)ks * (W2_N + C2) + W2_N + 32 * cohalf + tid] = sum;
     }
     if (kp == 0) {
-        const float us = ldexpf(1.f, -(sx + sd));
+        const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
         float* slab = slabs + (size_t)ks * (W2_N + C2);
         const int ci = 16 * h + (lane & 15);
         const int nt = tg ? 4 : 5;
@@ -1045,7 +1023,8 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int co = 32 * cohalf + 16 * mi + 4 * (lane >> 4) + r;
-                        slab[(co * C1 + ci) * 9 + 5 * tg + t] = (acc[mi][t][r] + xch[((mi * 5 + t) * 4 + r) * 64 + lane]) * us;
+                        slab[(co * C1 + ci) * 9 + 5 * tg + t] =
+                            x3_unscale(acc[mi][t][r] + xch[((mi * 5 + t) * 4 + r) * 64 + lane], us1, us2);
                     }
         }
     }

@@ -259,8 +259,6 @@ class ServerStage:
         self.loss_log = loss_log if loss_log is not None else LossLog(self.device)
         self.err_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.fuse_optim = True  # step_request: SGD of both slab kinds + the loss log in one launch
-        self.fc_wgrad_early = False  # run fc_wgrad right after fc_xent (pooled still cache-resident)
-        self.wgrad_first = False  # conv2 wgrad before the dgrad (launch-order knob; measured in DESIGN)
         self._buf = _Buffers()
 
     def bind_grads(self, view: torch.Tensor):
@@ -312,17 +310,7 @@ class ServerStage:
                 pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
                 loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
                 dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
-        def wgrad():
-            with TIMER("conv2_wgrad"):
-                return ops.conv2_wgrad_slabs(act, dpooled, code,
-                                             slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
-                                             impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
-        if self.wgrad_first:
-            s2 = wgrad()
-        s3 = None
-        if self.fc_wgrad_early:
-            with TIMER("fc_wgrad"):
-                s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+        # launch order dgrad -> wgrad -> fc wgrad (measured fastest: DESIGN.md §3a "Launch order")
         if client_fuse is not None:
             if di != "x3":
                 raise ValueError("client_fuse needs the x3 dgrad (conv preset 'x3' or 'x3w')")
@@ -335,11 +323,12 @@ class ServerStage:
                 cut_grad = self._b("cut_grad", (B, 32, 26, 26))
             with TIMER("conv2_dgrad"):
                 ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
-        if not self.wgrad_first:
-            s2 = wgrad()
-        if s3 is None:
-            with TIMER("fc_wgrad"):
-                s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+        with TIMER("conv2_wgrad"):
+            s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
+                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
+                                       impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
+        with TIMER("fc_wgrad"):
+            s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3
 
     def apply_grad_slabs(self, s2, s3):

@@ -140,7 +140,7 @@ def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = N
         rnd = fed["round"]
         if rnd is None:
             rnd = fed["round"] = {"states": [], "losses": [], "ids": set(), "done": asyncio.Event(),
-                                  "out": None}
+                                  "out": None, "error": None}
         if client_id is not None:
             if client_id in rnd["ids"]:
                 return Response(content=f"Error: client {client_id!r} already posted to this round",
@@ -150,37 +150,46 @@ def make_app(server=None, device: str = "cuda", learning_mode: Optional[str] = N
         rnd["losses"].append((int(step), float(client_loss), float(epoch)))
         if len(rnd["states"]) >= fed_clients:
             fed["round"] = None
-            with lock:
-                if state["full"] is None:
-                    state["full"] = FullModel()
-                m = state["full"]
-                avg = {k: torch.stack([sd[k].float() for sd in rnd["states"]]).mean(0)
-                       for k in rnd["states"][0]}
-                m.load_state_dict(avg)
-                if sink is not None:
-                    # mlflow.log_metric("loss" / "epoch", ..., step=step)  (server_part.py:86-87)
-                    st = max(s for s, _, _ in rnd["losses"])
-                    mean_loss = sum(l for _, l, _ in rnd["losses"]) / len(rnd["losses"])
-                    try:
-                        if hasattr(sink, "log_metric"):
-                            sink.log_metric("loss", mean_loss, st)
-                            sink.log_metric("epoch", max(e for _, _, e in rnd["losses"]), st)
-                        else:
-                            sink(st, mean_loss)
-                        if hasattr(sink, "flush"):
-                            sink.flush()
-                    except Exception as e:
-                        log.warning("metric sink failed (metrics stay buffered in the sink): %r", e)
-                rnd["out"] = pickle.dumps(m.state_dict())
-            rnd["done"].set()
+            try:
+                with lock:
+                    if state["full"] is None:
+                        state["full"] = FullModel()
+                    m = state["full"]
+                    avg = {k: torch.stack([sd[k].float() for sd in rnd["states"]]).mean(0)
+                           for k in rnd["states"][0]}
+                    m.load_state_dict(avg)
+                    if sink is not None:
+                        # mlflow.log_metric("loss" / "epoch", ..., step=step)  (server_part.py:86-87)
+                        st = max(s for s, _, _ in rnd["losses"])
+                        mean_loss = sum(l for _, l, _ in rnd["losses"]) / len(rnd["losses"])
+                        try:
+                            if hasattr(sink, "log_metric"):
+                                sink.log_metric("loss", mean_loss, st)
+                                sink.log_metric("epoch", max(e for _, _, e in rnd["losses"]), st)
+                            else:
+                                sink(st, mean_loss)
+                            if hasattr(sink, "flush"):
+                                sink.flush()
+                        except Exception as e:
+                            log.warning("metric sink failed (metrics stay buffered in the sink): %r", e)
+                    rnd["out"] = pickle.dumps(m.state_dict())
+            except Exception as e:  # every waiter of this round gets the 500 now, not at its timeout
+                rnd["error"] = (500, f"Error: federated aggregation failed ({e!r})")
+            finally:
+                rnd["done"].set()
         else:
             try:
                 await asyncio.wait_for(rnd["done"].wait(), timeout=fed_timeout)
             except asyncio.TimeoutError:
                 if fed["round"] is rnd:
-                    fed["round"] = None   # abandon the partial round
-                return Response(content=f"Error: federated round incomplete after {fed_timeout}s "
-                                        f"({len(rnd['states'])}/{fed_clients} clients)", status_code=504)
+                    fed["round"] = None   # abandon the partial round: release every other waiter at once
+                    rnd["error"] = (504, f"Error: federated round incomplete after {fed_timeout}s "
+                                         f"({len(rnd['states'])}/{fed_clients} clients)")
+                    rnd["done"].set()
+                if rnd["error"] is None:  # completed concurrently with the timeout
+                    return Response(content=rnd["out"], media_type="application/octet-stream")
+        if rnd["error"] is not None:
+            return Response(content=rnd["error"][1], status_code=rnd["error"][0])
         return Response(content=rnd["out"], media_type="application/octet-stream")
 
     @app.get("/health")

@@ -212,6 +212,49 @@ def test_federated_round_refuses_duplicate_client_and_times_out():
     assert rec.seen == [("loss", 2.0, 7), ("epoch", 3.0, 7)]
 
 
+def test_federated_round_abandon_and_failure_release_every_waiter():
+    """A round abandoned by one waiter's timeout releases every other waiter of that round at once
+    (504, not after its own timeout), and an aggregation that raises answers every waiter 500 at once."""
+    import asyncio
+    import time
+
+    import httpx
+    from splitcnn.data import init_models
+    from splitcnn.http_server import make_app
+    sd = init_models(seed=1, full=True).state_dict()
+    body = lambda cid, state=sd: pickle.dumps({"model_state": state, "epoch": 1, "loss": 1.0, "step": 3,  # noqa: E731
+                                               "client_id": cid})
+
+    async def abandon():
+        app = make_app(device="cpu", learning_mode="federated", fed_clients=3, fed_timeout=1.0)
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as c:
+            t0 = time.monotonic()
+            a = asyncio.create_task(c.post("/aggregate_weights", content=body("a")))
+            await asyncio.sleep(0.6)
+            b = asyncio.create_task(c.post("/aggregate_weights", content=body("b")))
+            ra = await a
+            rb = await b
+            return ra, rb, time.monotonic() - t0
+
+    ra, rb, dt = asyncio.run(abandon())
+    assert ra.status_code == 504 and rb.status_code == 504
+    assert dt < 1.5, dt   # b was released with a (t = 1.0), not at its own timeout (t = 1.6)
+
+    async def failing():
+        app = make_app(device="cpu", learning_mode="federated", fed_clients=2, fed_timeout=30.0)
+        bad = {k + "_x": v for k, v in sd.items()}   # keys FullModel does not have: load_state_dict raises
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as c:
+            t0 = time.monotonic()
+            rs = await asyncio.gather(c.post("/aggregate_weights", content=body("a", bad)),
+                                      c.post("/aggregate_weights", content=body("b", bad)))
+            return rs, time.monotonic() - t0
+
+    rs, dt = asyncio.run(failing())
+    assert [r.status_code for r in rs] == [500, 500] and dt < 10, ([r.status_code for r in rs], dt)
+
+
 def test_mlflow_sink_keeps_metrics_until_posted(monkeypatch):
     """MlflowRestSink.flush drops a chunk only after the tracking server accepted it: a failed post
     raises and the next flush re-sends the same metrics."""

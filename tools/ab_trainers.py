@@ -1,6 +1,7 @@
 """Profiling only: K2 SplitTrainer variants (engine attributes) captured as HIP graphs and timed
 interleaved in ONE process, B = 4096. usage: python tools/ab_trainers.py [--rounds 8]
-Variants: base; fcw_early (ServerStage.fc_wgrad_early); wg_first (ServerStage.wgrad_first)."""
+Variants: the conv presets (engine.CONV_PRESETS) and the default without its fusions. (Round 2 also timed
+launch-order knobs here — fc wgrad early, conv2 wgrad first — both slower; removed from the engine.)"""
 import argparse
 import os
 import sys
@@ -24,12 +25,9 @@ def main():
     dev = torch.device("cuda:0")
     X, Y = make_pool(B, 4, dev)
     variants = {}
-    for name in ("base", "fcw_early", "wg_first"):
-        tr = SplitTrainer(*init_models(seed=0), device=dev, graph=True)
-        if name == "fcw_early":
-            tr.server.fc_wgrad_early = True
-        if name == "wg_first":
-            tr.server.wgrad_first = True
+    configs = {"x3": {}, "x3_unfused": {"fuse_client_backward": False}, "x3w": {"conv": "x3w"}, "f32": {"conv": "f32"}}
+    for name, kw in configs.items():
+        tr = SplitTrainer(*init_models(seed=0), device=dev, graph=True, **kw)
         for i in range(5):
             tr.step(X[i % 4], Y[i % 4])
         variants[name] = tr
