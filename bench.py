@@ -181,9 +181,12 @@ def rocprof_avg(symbol, pattern="kernel_stats_k2.csv"):
     profiles/ (the same bench command under the profiler), or None."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + pattern)), key=os.path.getmtime)
+    # profiles/rocprof_<pattern> is the copy of the newest summary that travels to the GPU box (the
+    # per-round files under profiles/ are gpurun-ignored)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*" + pattern)), key=os.path.getmtime)
     files = [f for f in files if os.path.basename(f).startswith("r03")] or files
-    for f in reversed(files):
+    files = [os.path.join(ROOT, "profiles", "rocprof_" + pattern)] + files[::-1]
+    for f in files:
         try:
             for row in csv.DictReader(open(f)):
                 if symbol in row["Name"]:
@@ -363,7 +366,7 @@ def run_distributed(args, out, rank, world, local):
     def build(topology, micro):
         a, b = init_models(seed=0)
         if topology == "replicated":
-            t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev))
+            t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev), graph=not args.no_graph)
             return (lambda i: t.step(X[i % 4], Y[i % 4])), t, world * B
         if topology == "pipeline":
             assert world == 2
@@ -403,7 +406,11 @@ def run_distributed(args, out, rank, world, local):
     dt = timed(fn, args.steps, args.warmup, dev)
     out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
     out["config"] = {"workload": labels[topo], "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
-                     "parallelism": f"{topo}{world}", "graph": False}
+                     "parallelism": f"{topo}{world}", "graph": bool(getattr(t, "graph", False))}
+    if topo == "replicated":
+        out["config"]["replica_step"] = ("fused single-GPU step kernels (x3 conv2, client images, client backward "
+                                         "in the dgrad epilogue) captured in a HIP graph; bucket all-reduce "
+                                         "outside the graph; one launch steps both stages" if t.fused else "unfused")
     out["scaling"] = "weak"
     if topo != "replicated":
         out["config"]["micro_batches"] = args.micro

@@ -235,7 +235,9 @@ int slk_loss_log(const float* values, int n, float scale, float* ring, int capac
  * loss_values != NULL, slk_loss_log(loss_values, loss_n, loss_scale, ring, capacity, counter) —
  * bit-identical to those separate launches. Replaces the server's optimizer.step() + log_metric
  * (src/server_part.py:52,55) and the client's optimizer.step() (src/client_part.py:133) at the end
- * of a fused split step. The pointer/size arrays are host memory. */
+ * of a fused split step. The pointer/size arrays are host memory. A segment with params[s] == NULL
+ * (and grads[s] != NULL) only reduces: grads[s] = sum of its slabs (the data-parallel replica fills
+ * its all-reduce bucket this way: several slk_reduce_slabs in one launch). */
 int slk_sgd_multi_from_slabs(float* const* params, float* const* grads, const float* const* slabs,
                              const int* nslab, const int* n, int nseg, float lr, const float* loss_values,
                              int loss_n, float loss_scale, float* ring, int capacity, int* counter,

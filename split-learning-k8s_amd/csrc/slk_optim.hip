@@ -208,7 +208,8 @@ extern "C" int slk_sgd_multi_from_slabs(float* const* params, float* const* grad
     SgdMulti a{};
     int nblk = 0;
     for (int s = 0; s < nseg; ++s) {
-        SLK_CHECK_ARG(n[s] >= 0 && nslab[s] >= 0 && params[s] && (slabs[s] || nslab[s] == 0));
+        // a segment with no param is a reduce only (grad = sum of slabs): the all-reduce bucket fill
+        SLK_CHECK_ARG(n[s] >= 0 && nslab[s] >= 0 && (params[s] || (grads && grads[s])) && (slabs[s] || nslab[s] == 0));
         a.seg[s] = SgdSeg{params[s], grads ? grads[s] : nullptr, slabs[s], nslab[s], n[s], rs_blocks(n[s], nslab[s])};
         nblk += a.seg[s].nblk;
     }

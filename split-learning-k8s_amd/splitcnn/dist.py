@@ -104,10 +104,33 @@ def _compute(server, client, act, y, scale):
     return server.compute(act, y, scale)
 
 
+def _fused_pair(client, server) -> bool:
+    """Same-device engine stages with every conv2 kernel on x3: the replica can run the single-GPU
+    fused step's kernels (client conv1 writes the server's split images, the client backward runs in
+    the server's dgrad epilogue) — engine.SplitTrainer's launch sequence minus the optimizer."""
+    return (getattr(server, "conv", None) == "x3" and hasattr(client, "emit_act16")
+            and getattr(client, "device", None) is not None and client.device.type == "cuda"
+            and client.device == server.device)
+
+
 class Replicated:
-    def __init__(self, client, server, group=None, device=None):
+    """Data-parallel replicas (SplitFed-V1 on one node). `fused` (default: whenever `_fused_pair`)
+    runs the replica's compute as the single-GPU fused step (captured in one HIP graph per batch size
+    when `graph`), the gradients land in the bucket by one reduce launch, ONE all-reduce of the
+    bucket, then ONE launch steps both stages and logs the loss. At world 1 that is bit-identical to
+    engine.SplitTrainer's step (same kernels, same slab order; the optimizer reads the reduced
+    gradient instead of the slabs)."""
+
+    def __init__(self, client, server, group=None, device=None, fused: Optional[bool] = None,
+                 graph: bool = False):
         self.client, self.server = client, server
-        _pair_amax(client, server)
+        self.fused = _fused_pair(client, server) if fused is None else fused
+        if self.fused:
+            if not _fused_pair(client, server):
+                raise ValueError("Replicated(fused=True) needs same-device engine stages on the x3 conv preset")
+            client.emit_act16 = True
+        else:
+            _pair_amax(client, server)
         self.group = group
         self.world = dist.get_world_size(group)
         dev = device if device is not None else client.grads.device
@@ -117,8 +140,72 @@ class Replicated:
         self.loss_slot = self.bucket[-1:]
         self.global_step = 0
         self.overlap = True   # split the all-reduce so the server's part overlaps the client backward
+        self.graph = graph and self.fused
+        self._graphs = {}
+
+    # ---------------------------------------------------------------- fused replica (x3 stages)
+    def _compute_fused(self, x, y):
+        """Client forward -> server forward/loss/backward with the client backward in the dgrad
+        epilogue -> every gradient slab reduced into the bucket + the scaled loss into its slot."""
+        from . import ops
+        c, s = self.client, self.server
+        B = x.shape[0]
+        scale = 1.0 / (self.world * B)
+        c.forward(x)
+        cslabs = c._buf.get("c1w_slabs", (ops.conv2_dgrad_c1w_nslab(B), ops.CLIENT_NPARAM), torch.float32, c.device)
+        _, loss_i, s2, s3 = s.forward_backward(None, y, scale, act_amax=c._act_amax, act16=c._act16,
+                                               client_fuse=(x, c.W1.detach(), c.b1.detach(), cslabs))
+        k = ops.CONV2_SLAB
+        ops.sgd_multi_from_slabs([(None, c.grads, cslabs), (None, s.grads[:k], s2), (None, s.grads[k:], s3)], 0.0)
+        ops.loss_sum(loss_i, scale, self.loss_slot)
+
+    def _graph_for(self, B):
+        g = self._graphs.get(B)
+        if g is not None:
+            return g
+        dev = self.bucket.device
+        x = torch.zeros((B, 1, 28, 28), dtype=torch.float32, device=dev)
+        y = torch.zeros((B,), dtype=torch.int64, device=dev)
+        # warm up on a side stream (allocations happen here, not during capture); the compute segment
+        # writes only scratch and the bucket, so the warm-up leaves no trace in the parameters
+        st = torch.cuda.Stream(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(st):
+            self._compute_fused(x, y)
+        torch.cuda.current_stream(dev).wait_stream(st)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self._compute_fused(x, y)
+        g = {"graph": graph, "x": x, "y": y}
+        self._graphs[B] = g
+        return g
+
+    def _step_fused(self, x, y):
+        from . import ops
+        if self.graph:
+            g = self._graph_for(x.shape[0])
+            if x.data_ptr() != g["x"].data_ptr():
+                g["x"].copy_(x, non_blocking=True)
+            if y.data_ptr() != g["y"].data_ptr():
+                g["y"].copy_(y, non_blocking=True)
+            g["graph"].replay()
+        else:
+            self._compute_fused(x, y)
+        dist.all_reduce(self.bucket, group=self.group)
+        c, s, C = self.client, self.server, CLIENT_N
+        ring, ctr = s.loss_log.ring, s.loss_log.counter
+        segs = [(c.params, None, self.bucket[:C].view(1, C)), (s.params, None, self.bucket[C:C + SERVER_N].view(1, SERVER_N))]
+        if c.lr == s.lr:
+            ops.sgd_multi_from_slabs(segs, s.lr, loss=(self.loss_slot, 1.0, ring, ctr))
+        else:
+            ops.sgd_multi_from_slabs(segs[:1], c.lr)
+            ops.sgd_multi_from_slabs(segs[1:], s.lr, loss=(self.loss_slot, 1.0, ring, ctr))
+        s.loss_log.note_step(self.global_step)
+        self.global_step += 1
 
     def step(self, x, y):
+        if self.fused:
+            return self._step_fused(x, y)
         B = x.shape[0]
         scale = 1.0 / (self.world * B)
         act = self.client.forward(x)

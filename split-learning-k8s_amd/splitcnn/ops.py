@@ -348,7 +348,8 @@ def sgd_from_slabs(param, grad, slabs, lr):
 def sgd_multi_from_slabs(segments, lr, loss=None):
     """ONE launch for every optimizer step of a split step: for each (param, grad, slabs) in
     `segments` (<= 4) sgd_from_slabs(param, grad, slabs, lr), plus loss_log(*loss) when
-    loss = (values, scale, ring, counter) — bit-identical to the separate launches."""
+    loss = (values, scale, ring, counter) — bit-identical to the separate launches. A segment whose
+    param is None only reduces its slabs into grad (reduce_slabs of several buffers in one launch)."""
     k = len(segments)
     if not 0 <= k <= 4:
         raise ValueError("sgd_multi_from_slabs: at most 4 segments")
@@ -358,11 +359,13 @@ def sgd_multi_from_slabs(segments, lr, loss=None):
     stream_of = None
     for i, (param, grad, sl) in enumerate(segments):
         nsl, n = sl.shape
-        params[i] = _dev(param, "param", (n,))
+        if param is None and grad is None:
+            raise ValueError("sgd_multi_from_slabs: a segment needs a param or a grad")
+        params[i] = _dev(param, "param", (n,)) if param is not None else None
         grads[i] = _dev(grad, "grad", (n,)) if grad is not None else None
         slabs[i] = _dev(sl, "slabs")
         nslab[i], ns[i] = nsl, n
-        stream_of = param if stream_of is None else stream_of
+        stream_of = (param if param is not None else grad) if stream_of is None else stream_of
     lv, ln, lsc, ring, cap, ctr = None, 0, 0.0, None, 0, None
     if loss is not None:
         values, lsc, ring_t, counter = loss

@@ -409,3 +409,32 @@ def test_cut_codec_bit_identical_to_dense(gpu, tmp_path, topo, world, micro, fix
             if k.startswith("bytes_"):
                 moved, full = sparse[r][k]
                 assert dense[r][k][0] == dense[r][k][1] == full and 0 < moved < full, (r, k, moved, full)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_replicated_fused_world1_rccl_bitwise_vs_split_trainer(gpu, graph):
+    """dist.Replicated's fused replica (the single-GPU step's kernels + the bucket all-reduce over RCCL,
+    one rank) takes exactly SplitTrainer's steps: parameters and logged losses bitwise equal over four
+    B = 256 steps, with and without the HIP graph (src/server_part.py:47-55, src/client_part.py:132-133)."""
+    import torch.distributed as dist
+    from splitcnn import dist as sd
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage, SplitTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        data = SyntheticMNIST(5)
+        batches = [tuple(t.to(gpu) for t in data.batch(256)) for _ in range(4)]
+        tr = SplitTrainer(*init_models(seed=3), device=gpu, graph=True)
+        a, b = init_models(seed=3)
+        rep = sd.Replicated(ClientStage(a, device=gpu), ServerStage(b, device=gpu), graph=graph)
+        assert rep.fused and rep.graph == graph
+        for x, y in batches:
+            tr.step(x, y)
+            rep.step(x, y)
+        torch.cuda.synchronize()
+        assert torch.equal(tr.client.params, rep.client.params)
+        assert torch.equal(tr.server.params, rep.server.params)
+        assert tr.loss_log.flush() == rep.server.loss_log.flush()
+    finally:
+        dist.destroy_process_group()
