@@ -77,6 +77,8 @@ def parse():
                          "F(2x2,3x3) on the f32 MFMA throughout (default: splitcnn.engine.CONV_DEFAULT)")
     ap.add_argument("--no-conv-compare", action="store_true",
                     help="skip the short run of the other conv preset reported beside the headline")
+    ap.add_argument("--no-hub-loopback", action="store_true",
+                    help="skip the 1-GPU loopback of the K4 hub server's compute (7 clients x --micro chunks)")
     return ap.parse_args()
 
 
@@ -304,6 +306,73 @@ def run_single(args, out):
     if conv == "f32":  # every conv2 FLOP on the f32 MFMA: one peak prices the whole step
         out["step_roofline_frac"] = round(out["value"] * STEP_FLOP_EXECUTED / (FP32_PEAK_TFLOPS * 1e12), 4)
     out["step_direct_equivalent_tflops"] = round(out["value"] * FLOP_PER_SAMPLE / 1e12, 2)
+
+
+def run_hub_loopback(args, nc=7):
+    """K4's bottleneck measured on ONE GPU: the hub server's step for nc clients x B samples (the chunked,
+    graph-captured sequence dist.Hub.server_step runs: per micro-batch chunk of nc*B/m samples codec
+    unpack -> forward / loss / backward -> codec pack; then one SGD step), with the chunks' inputs already
+    in the server's receive buffers (no transport). Compared with the fused 1-GPU step minus the client's
+    conv1 (which a hub server does not run), the server's rate bounds BASELINE config 4's throughput."""
+    import torch
+
+    from splitcnn import dist as sd
+    from splitcnn.codec import CutCodec
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    dev = torch.device("cuda:0")
+    B, m = args.batch, args.micro
+    b, G = B // m, nc * B
+    a, srv = init_models(seed=0)
+    hub = sd.Hub(ServerStage(srv, device=dev), rank=nc, world=nc + 1, micro=m, compress=not args.dense_exchange,
+                 graph=not args.no_graph)
+    codec = hub._use_codec(dev)
+    hub._prepare(B, dev, codec)  # the chunk graphs (their warm-up zeroes the receive buffers)
+    cl = ClientStage(a, device=dev)
+    cl.emit_amax = True
+    n = b * 32 * 26 * 26
+    acts = hub._buf("acts", (G, 32, 26, 26), torch.float32, dev)
+    labels = hub._buf("labels", (G,), torch.int64, dev)
+    amx = hub._buf("amax", (G,), torch.float32, dev)
+    hub._buf("cuts", (G, 32, 26, 26), torch.float32, dev)
+    hub._buf("loss_parts", (m,), torch.float32, dev)
+    data = SyntheticMNIST(7)
+    for k in range(m):
+        for ci in range(nc):
+            sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
+            x, y = data.batch(b)
+            cl.forward(x.to(dev), out=acts[sl])
+            amx[sl].copy_(cl._act_amax)
+            labels[sl].copy_(y.to(dev))
+            if codec is not None:
+                codec.encode(acts[sl], codec.buffers(("s", ci, k), n, dev))
+    return hub, cl, codec, data, nc
+
+
+def hub_loopback_rate(args, ref_value, conv1_ms):
+    import torch
+    hub, cl, codec, data, nc = run_hub_loopback(args)
+    dev = torch.device("cuda:0")
+    B, m = args.batch, args.micro
+    b = B // m
+    s = hub.stage
+    parts = hub._bufs["loss_parts"]
+
+    def step(i):
+        for k in range(m):
+            hub._run_chunk(k, B, dev, codec)
+        s.step()
+        s.log_loss(parts, scale=1.0)
+    K = max(3, min(args.steps, 10))
+    dt = timed(step, K, 2, dev)
+    rate = K * nc * B / dt
+    fused_minus_conv1 = B / (B / ref_value - conv1_ms * 1e-3) if ref_value and conv1_ms else None
+    return {"workload": f"K4 hub server compute, {nc} clients x {B} samples in {m} chunks of {nc * b} "
+                        f"(codec unpack/pack {'on' if codec is not None else 'off'}, HIP graph per chunk), "
+                        "inputs already in the receive buffers: the 1-GPU bound of BASELINE config 4",
+            "samples_per_s": round(rate, 1), "ms_per_step": round(dt / K * 1e3, 3), "global_batch": nc * B,
+            "fused_1gpu_minus_conv1_samples_per_s": round(fused_minus_conv1, 1) if fused_minus_conv1 else None,
+            "ratio": round(rate / fused_minus_conv1, 3) if fused_minus_conv1 else None}
 
 
 def run_wide(args, B, steps, warmup, kernel_pass_on=True):
@@ -534,6 +603,11 @@ def main():
         out["data"] = "synthetic CIFAR-shape batches (class prototypes + noise), random-init weights (seed 0)"
     else:
         run_single(args, out)
+        if not args.no_hub_loopback:
+            try:
+                out["k4_server_loopback"] = hub_loopback_rate(args, out["value"], (out.get("kernels") or {}).get("conv1_fwd"))
+            except Exception as e:  # the headline stands on its own
+                out["k4_server_loopback"] = {"error": repr(e)[:300]}
         if not args.no_k5:
             try:
                 out["widened"] = run_wide(args, args.k5_batch, max(5, min(args.steps, 20)), 3,

@@ -186,18 +186,21 @@ int64_t slk_conv2_act16_bytes(int B);
  * writing the x3 server operand directly: act_amax and the act16 images (bit-identical to those
  * slk_conv2_fwd_pool_x3s writes), plus the f32 act when act != NULL. The server forward then reads the
  * images (slk_conv2_fwd_pool_x3i: same pooled / code as slk_conv2_fwd_pool_x3 on the f32 act, bitwise)
- * and so does the wgrad (slk_conv2_wgrad_x3s). */
+ * and so does the wgrad (slk_conv2_wgrad_x3s). relu_bits (optional, slk_relu_bits_bytes(B) bytes, 16-byte
+ * aligned): the ReLU mask act > 0 of every cut element, 1 bit each (per sample [4 channel groups cg][169]
+ * u32, bit 4 (c & 7) + u of word (c >> 3, t) = act[c][4 t + u] > 0), which slk_conv2_dgrad_x3_c1w consumes. */
 int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1, float* act, float* act_amax, uint16_t* act16,
-                     int B, void* stream);
+                     uint32_t* relu_bits, int B, void* stream);
+int64_t slk_relu_bits_bytes(int B);
 int slk_conv2_fwd_pool_x3i(const uint16_t* act16, const float* act_amax, const float* W2, const float* b2,
                            float* pooled, uint8_t* code, int B, void* stream);
 
 /* The x3 dgrad with the client's backward fused (src/server_part.py:51 -> src/client_part.py:132 in one
  * launch, for the single-GPU step): the cut gradient is not written; each workgroup applies the client's
- * ReLU mask (recomputed from x, W1, b1) and writes one slab [dW1 c*9+tap (288) | db1 c (32)] of the
+ * ReLU mask (relu_bits from slk_conv1_fwd_x3) and writes one slab [dW1 c*9+tap (288) | db1 c (32)] of the
  * client gradient (slk_conv2_dgrad_x3_c1w_nslab(B) slabs, reduced by slk_sgd_from_slabs). */
 int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
-                           const float* x, const float* W1, const float* b1, float* client_slabs, int B, void* stream);
+                           const float* x, const uint32_t* relu_bits, float* client_slabs, int B, void* stream);
 int slk_conv2_dgrad_x3_c1w_nslab(int B);
 
 /* ---------------------------------------------------------------- reductions / optimizer */

@@ -390,6 +390,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 // bytes); one barrier per unit. 8 waves: wave = (ci tile nt, tile group g: tiles T0 + g + 4i); its weight
 // fragments for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its <= 4 accumulators live
 // across the part's two co halves.
+// ReLU bitmap of the cut (written by conv1_fwd_x3_kernel, layout there): u32 words per (ci, u), per sample
+constexpr int RB_SAMPLE = 4 * (A_PIX / 4);  // 676 u32 = 2,704 B per sample: [channel group 4][169]
 constexpr int X3D_THREADS = 512;
 constexpr int X3D_REC = 160;                       // bytes per image pixel: h 64 | l 64 | pad 32
 constexpr int X3D_NRMAX = 14;                      // image rows (dY rows) of the largest part
@@ -405,20 +407,34 @@ __device__ __forceinline__ int x3d_t0(int pt) { return pt == 0 ? 0 : (pt == 1 ? 
 __device__ __forceinline__ int x3d_ybase(int pt) { return pt == 0 ? -2 : (pt == 1 ? 6 : 14); }
 __device__ __forceinline__ int x3d_nwr(int pt) { return pt == 2 ? 7 : 6; }  // image window rows
 
+// Accumulation: per (tile, unit) the hi*hi products go into the tile's accumulator and the two cross
+// products (hi*lo, lo*hi) into a separate chain started from zero, added to the accumulator by one f32
+// add at the end of the tile's 9 taps. The f16 MFMA's internal alignment truncates (toward -inf) at the
+// unit of its largest addend; cross products added straight onto the large accumulator lost their low
+// bits there, a bias of ~-1.5e-8 of sum |a b| per output that the client gradient (a sum over 2.8 M cut
+// elements) turned into ~1e-6 of db1 (tools/ubench/x3_bias.hip: 17x less bias this way).
 // C1W = true (the fused single-GPU step): the cut gradient is not stored; the epilogue applies the
-// client's ReLU mask (recomputed from x, W1, b1 with conv1's exact FMA order, as slk_conv1_wgrad_remask
-// does) and accumulates the conv1 weight gradient dW1[ci][tap] += g * x, db1[ci] += g in registers (a
-// lane owns one ci); each workgroup writes one 320-float client slab (src/client_part.py:132 — the
-// client's act.backward(cut_grad) without the cut gradient ever reaching HBM). x of the next pair is
-// loaded a unit ahead and kept in LDS (2 x 3,136 B).
+// client's ReLU mask (the 1-bit map conv1_fwd_x3 wrote) and accumulates the conv1 weight gradient
+// dW1[ci][tap] = sum_p g[ci][p] x[p + tap], db1[ci] = sum_p g[ci][p] as a GEMM on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32, an exact fmaf chain): A = the masked, unscaled accumulators as they sit in
+// the lanes (row = ci, k = the lane's 4-pixel group), B = x at each lane's (pixel, tap) (col = tap 0-8,
+// 9 = bias -> 1.0), one 16 ci x 16 col accumulator per wave for the whole launch; each workgroup writes
+// one 320-float client slab (src/client_part.py:132 — the client's act.backward(cut_grad) without the
+// cut gradient ever reaching HBM). x and the bit map of the next pair are loaded a unit ahead into LDS.
 template <bool C1W>
 __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ dpooled, const float* __restrict__ amax, const uint8_t* __restrict__ code,
     const float* __restrict__ W2, float* __restrict__ cut_grad, int B, const float* __restrict__ xin = nullptr,
-    const float* __restrict__ W1 = nullptr, const float* __restrict__ b1 = nullptr, float* __restrict__ c1slabs = nullptr) {
+    const uint32_t* __restrict__ relu_bits = nullptr, float* __restrict__ c1slabs = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
-    __shared__ float xsm[C1W ? 2 : 1][C1W ? IN_HW * IN_HW : 1];
-    __shared__ float w1s[C1W ? C1 * 10 : 1];  // [c][9 taps | bias]
+    // C1W: per pair, x (3,136 B) then its ReLU bits (2,704 B), double-buffered, moved by LDS-DMA
+    constexpr int XB_X = IN_HW * IN_HW * 4, XB_BYTES = XB_X + RB_SAMPLE * 4;
+    static_assert(XB_X > 3072 && XB_X <= 4096 && XB_X % 16 == 0 && RB_SAMPLE * 4 > 2048 && RB_SAMPLE * 4 <= 3072 &&
+                  RB_SAMPLE % 4 == 0, "DMA pieces of issue_xb");
+    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 : 1][C1W ? XB_BYTES : 16];
+    // C1W: each wave's conv1-gradient accumulator D1[ci 16 nt + 4 (lane >> 4) + r][col lane & 15] (col =
+    // tap 0-8, 9 = bias), kept here between epilogues (not in the MFMA loop's registers)
+    __shared__ __attribute__((aligned(16))) f32x4 d1s[C1W ? X3D_THREADS : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
@@ -534,16 +550,22 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     // (pair = (sample, part))
     const int P = 3 * B;  // pairs
     int pr = blockIdx.x;
-    // C1W: per-lane conv1 gradient accumulators for ci = 16 nt + n16 (9 taps + bias) and x staging
-    float c1acc[C1W ? 10 : 1];
-#pragma unroll
-    for (int j = 0; j < (C1W ? 10 : 1); ++j) c1acc[j] = 0.f;
-    float2 xr = make_float2(0.f, 0.f);
-    const bool xthr = C1W && tid < IN_HW * IN_HW / 2;
+    // pair pp's x and bits -> xbm[buf]: waves 0-3 move x (3 x 1 KiB + 64 B), waves 4-6 the bits (2 x
+    // 1 KiB + 656 B), one 16-B piece per lane (retired by the s_waitcnt before the barrier that opens the next pair)
+    auto issue_xb = [&](int pp, int buf) {
+        const size_t b = (size_t)(pp / 3);
+        if (wave < 4) {
+            if (wave < 3 || lane < (XB_X % 1024) / 16)
+                glds16_so(reinterpret_cast<const char*>(xin + b * IN_HW * IN_HW) + wave * 1024, (uint32_t)lane * 16,
+                          lds_u32(xbm[buf]) + wave * 1024);
+        } else if (wave < 6 || (wave == 6 && lane < (RB_SAMPLE * 4 - 2048) / 16)) {
+            glds16_so(reinterpret_cast<const char*>(relu_bits + b * RB_SAMPLE) + (wave - 4) * 1024, (uint32_t)lane * 16,
+                      lds_u32(xbm[buf]) + XB_X + (wave - 4) * 1024);
+        }
+    };
     if constexpr (C1W) {
-        if (tid < C1 * 9) w1s[(tid / 9) * 10 + tid % 9] = W1[tid];
-        if (tid < C1) w1s[tid * 10 + 9] = b1[tid];
-        if (pr < P && xthr) reinterpret_cast<float2*>(xsm[0])[tid] = reinterpret_cast<const float2*>(xin + (size_t)(pr / 3) * IN_HW * IN_HW)[tid];
+        d1s[tid] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pr < P) issue_xb(pr, 0);
     }
     if (pr < P) {
         load_dy(2 * pr);
@@ -563,13 +585,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         for (int i = 0; i < X3D_MPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int h = 0; h < 2; ++h, ++k) {
+            // C1W: this pair's x / bits DMA (issued during the previous pair) retired before the barrier
+            if (C1W && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
-            if constexpr (C1W) {
-                // x of the next pair: loaded at its h = 0 unit, into LDS at h = 1 (the other buffer)
-                const int np = min(pr + G, P - 1);
-                if (h == 0 && xthr) xr = reinterpret_cast<const float2*>(xin + (size_t)(np / 3) * IN_HW * IN_HW)[tid];
-                if (h == 1 && xthr) reinterpret_cast<float2*>(xsm[(q + 1) & 1])[tid] = xr;
-            }
+            // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue)
+            if (C1W && h == 0) issue_xb(min(pr + G, P - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
             const int unx = min(h ? 2 * (pr + G) : 2 * pr + 1, U - 1);   // the unit after this one
@@ -591,6 +611,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 load_dy(unx2);
             }
             f16x8 fh[4], fl[4];
+            f32x4 ct;  // cross products of the current tile (see the accumulation note above)
             constexpr int NS = 27;  // tiles 0..2 exist for every wave and part
 #pragma unroll
             for (int q = 0; q < 3; ++q) rd(q / 9, q % 9, fh[q], fl[q]);
@@ -598,7 +619,10 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             for (int st = 0; st < NS; ++st) {
                 if (st + 3 < NS) rd((st + 3) / 9, (st + 3) % 9, fh[(st + 3) & 3], fl[(st + 3) & 3]);
                 const int i = st / 9, tap = st % 9;
-                acc[i] = mfma_x3(fh[st & 3], fl[st & 3], wh[h][tap], wl[h][tap], acc[i]);
+                acc[i] = mfma_f16(fh[st & 3], wh[h][tap], acc[i]);
+                ct = mfma_f16(fh[st & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
+                ct = mfma_f16(fl[st & 3], wh[h][tap], ct);
+                if (tap == 8) acc[i] += ct;
             }
             // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
             __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
@@ -617,8 +641,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {
                     if (tap + 3 < 9) rd(3, tap + 3, fh[(tap + 3) & 3], fl[(tap + 3) & 3]);
-                    acc[3] = mfma_x3(fh[tap & 3], fl[tap & 3], wh[h][tap], wl[h][tap], acc[3]);
+                    acc[3] = mfma_f16(fh[tap & 3], wh[h][tap], acc[3]);
+                    ct = mfma_f16(fh[tap & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
+                    ct = mfma_f16(fl[tap & 3], wh[h][tap], ct);
                 }
+                acc[3] += ct;
                 __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {
@@ -630,35 +657,33 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
         const float us1 = ldexpf(1.f, -x3_exp(amax_b)), us2 = ldexpf(1.f, -sw);
         if constexpr (C1W) {
-            // client ReLU backward + conv1 wgrad for this lane's ci and pixels (the cut gradient g is the
-            // value the store below would write)
+            // client ReLU backward + conv1 wgrad (the cut gradient g is the value the store below would
+            // write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels 16 t + 4 kc + r
             const int ci = 16 * nt + n16;
-            const float* xs = xsm[q & 1];
-            float wk[10];
-#pragma unroll
-            for (int j = 0; j < 10; ++j) wk[j] = w1s[ci * 10 + j];
+            const float* xs = reinterpret_cast<const float*>(xbm[q & 1]);
+            const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbm[q & 1] + XB_X);
+            f32x4 d1 = d1s[tid];
+            // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff
+            const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
 #pragma unroll
             for (int i = 0; i < X3D_MPW; ++i) {
                 const int t = T0 + g + 4 * i;
+                if (t < T1) {  // wave-uniform
+                    const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
+                    // (pixels past 675: no conv1 thread, mask 0, so A = 0 there)
+                    const uint32_t mw = tq < A_PIX / 4 ? bs[(ci >> 3) * (A_PIX / 4) + tq] >> (4 * (ci & 7)) : 0u;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int p = 16 * t + 4 * kc + r;
-                    if (t < T1 && p < A_PIX) {
-                        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
-                        float xv[9];
-#pragma unroll
-                        for (int kk = 0; kk < 9; ++kk) xv[kk] = xs[(y + kk / 3) * IN_HW + xx + kk % 3];
-                        float sum = 0.f;
-#pragma unroll
-                        for (int kk = 0; kk < 9; ++kk) sum = fmaf(xv[kk], wk[kk], sum);
-                        sum += wk[9];
-                        const float gm = sum > 0.f ? x3_unscale(acc[i][r], us1, us2) : 0.f;
-#pragma unroll
-                        for (int kk = 0; kk < 9; ++kk) c1acc[kk] = fmaf(gm, xv[kk], c1acc[kk]);
-                        c1acc[9] += gm;
+                    for (int r = 0; r < 4; ++r) {
+                        const float gm = ((mw >> r) & 1u) ? x3_unscale(acc[i][r], us1, us2) : 0.f;
+                        const int p = min(16 * t + 4 * kc + r, A_PIX - 1);
+                        const int y = p / A_HW;
+                        const float xv = xs[p + 2 * y + toff];
+                        const float bv = n16 < 9 ? xv : (n16 == 9 ? 1.f : 0.f);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, bv, d1, 0, 0, 0);
                     }
                 }
             }
+            d1s[tid] = d1;
         } else {
             float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
@@ -673,18 +698,15 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         ++q;
     }
     if constexpr (C1W) {
-        // slab of this workgroup: ci's 16 partials (4 kc lanes x 4 tile groups) summed in a fixed order
+        // slab of this workgroup: D1 of the 4 tile-group waves of each ci tile, summed in wave order
         __syncthreads();
-        float* part = reinterpret_cast<float*>(smem);  // [wave][lane][10]
-#pragma unroll
-        for (int j = 0; j < 10; ++j) part[(wave * 64 + lane) * 10 + j] = c1acc[j];
-        __syncthreads();
+        const float* part = reinterpret_cast<const float*>(d1s);  // [wave][lane][4]
         if (tid < C1 * 10) {
             const int ci = tid / 10, j = tid - (tid / 10) * 10;
-            const int ntc = ci >> 4, n = ci & 15;
+            const int ntc = ci >> 4, cl = ci & 15;  // D1 row cl = 4 (lane >> 4) + r, col j = lane & 15
+            const int src = ((cl >> 2) * 16 + j) * 4 + (cl & 3);
             float sum = 0.f;
-            for (int gg = 0; gg < 4; ++gg)
-                for (int kq = 0; kq < 4; ++kq) sum += part[((ntc + 2 * gg) * 64 + kq * 16 + n) * 10 + j];
+            for (int gg = 0; gg < 4; ++gg) sum += part[(ntc + 2 * gg) * 256 + src];
             c1slabs[(size_t)blockIdx.x * (C1 * 10) + (j < 9 ? ci * 9 + j : C1 * 9 + ci)] = sum;
         }
     }
@@ -1038,14 +1060,19 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 // when act != nullptr — the f32 act too. One workgroup per sample; pass 1 (thread = 4 consecutive
 // pixels, float4 act stores) computes the maximum, pass 2 recomputes (9 FMAs a value) per (pixel,
 // 8-channel chunk) item and splits into the per-sample image (each pixel stored once).
+// BITS: also the ReLU mask act > 0 of every cut element, 1 bit each, for the fused client backward in
+// conv2_dgrad_x3_kernel<true> (which then reads 2.7 KB a sample instead of recomputing conv1): per
+// sample [4 channel groups cg][169 threads t] u32, bit 4 (c & 7) + u of (cg = c >> 3, t) = (act[c][4t + u]
+// > 0) — pass 1's thread t packs its own 4 pixels of 8 channels into one word (act >= 0, so its bit
+// pattern is nonzero iff act > 0: min(bits, 1) is the mask bit) and writes 4 coalesced words.
 constexpr int C1X_T = 192;
 constexpr int C1X_G = A_PIX / 4;  // 169 active threads
-#ifndef SLK_C1X_WPE
-#define SLK_C1X_WPE 1
-#endif
-__global__ __launch_bounds__(C1X_T, SLK_C1X_WPE) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
+static_assert(RB_SAMPLE == 4 * C1X_G, "bit map layout");
+template <bool BITS>
+__global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
                                                              const float* __restrict__ b1, float* __restrict__ act,
-                                                             float* __restrict__ act_amax, uint16_t* __restrict__ act16) {
+                                                             float* __restrict__ act_amax, uint16_t* __restrict__ act16,
+                                                             uint32_t* __restrict__ relu_bits) {
     __shared__ float xs[IN_HW * IN_HW];
     __shared__ float amx[C1X_T / 64];
     __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
@@ -1083,12 +1110,22 @@ __global__ __launch_bounds__(C1X_T, SLK_C1X_WPE) void conv1_fwd_x3_kernel(const 
     float am = 0.f;
     if (active) {
         float4* out = act ? reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid : nullptr;
+#pragma unroll
+        for (int cg = 0; cg < 4; ++cg) {
+            uint32_t bw = 0;
 #pragma unroll 4
-        for (int c = 0; c < C1; ++c) {
-            float o[4];
-            conv(c, o);
-            if (act) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
-            am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+            for (int cc = 0; cc < 8; ++cc) {
+                const int c = 8 * cg + cc;
+                float o[4];
+                conv(c, o);
+                if (act) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
+                am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+                if constexpr (BITS) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) bw |= min(__float_as_uint(o[u]), 1u) << (4 * cc + u);
+                }
+            }
+            if constexpr (BITS) relu_bits[(size_t)b * RB_SAMPLE + cg * C1X_G + tid] = bw;
         }
     }
     am = wave_max(am);
@@ -1171,13 +1208,18 @@ extern "C" int slk_conv2_fwd_pool_x3i(const uint16_t* act16, const float* act_am
 }
 
 extern "C" int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1, float* act, float* act_amax,
-                                uint16_t* act16, int B, void* stream) {
+                                uint16_t* act16, uint32_t* relu_bits, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && (B == 0 || (x && W1 && b1 && act_amax && act16)));
     if (B == 0) return 0;
-    hipLaunchKernelGGL(conv1_fwd_x3_kernel, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act, act_amax,
-                       act16);
+    if (relu_bits)
+        hipLaunchKernelGGL(conv1_fwd_x3_kernel<true>, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act,
+                           act_amax, act16, relu_bits);
+    else
+        hipLaunchKernelGGL(conv1_fwd_x3_kernel<false>, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act,
+                           act_amax, act16, relu_bits);
     return slk_launch_status();
 }
+extern "C" int64_t slk_relu_bits_bytes(int B) { return B > 0 ? (int64_t)B * RB_SAMPLE * 4 : 0; }
 
 extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
                                   float* cut_grad, int B, void* stream) {
@@ -1185,20 +1227,20 @@ extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, co
     if (B == 0) return 0;
     const int P = 3 * B;
     hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
-                       slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B, nullptr, nullptr, nullptr, nullptr);
+                       slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B, nullptr, nullptr, nullptr);
     return slk_launch_status();
 }
 
 extern "C" int slk_conv2_dgrad_x3_c1w_nslab(int B) { return B <= 0 ? 0 : (3 * B < X3D_GRID ? 3 * B : X3D_GRID); }
 
 extern "C" int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
-                                      const float* x, const float* W1, const float* b1, float* client_slabs, int B,
+                                      const float* x, const uint32_t* relu_bits, float* client_slabs, int B,
                                       void* stream) {
-    SLK_CHECK_ARG(B >= 0 && (B == 0 || (dpooled && dp_amax && code && W2 && x && W1 && b1 && client_slabs)));
+    SLK_CHECK_ARG(B >= 0 && (B == 0 || (dpooled && dp_amax && code && W2 && x && relu_bits && client_slabs)));
     if (B == 0) return 0;
     const int P = 3 * B;
     hipLaunchKernelGGL(conv2_dgrad_x3_kernel<true>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
-                       slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, x, W1, b1, client_slabs);
+                       slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, x, relu_bits, client_slabs);
     return slk_launch_status();
 }
 

@@ -59,9 +59,10 @@ _SIGS = {
     "slk_conv2_fwd_pool_x3s": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_wgrad_x3s": [_P, _P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_act16_bytes": [_I],
-    "slk_conv1_fwd_x3": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv1_fwd_x3": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_relu_bits_bytes": [_I],
     "slk_conv2_fwd_pool_x3i": [_P, _P, _P, _P, _P, _P, _I, _P],
-    "slk_conv2_dgrad_x3_c1w": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_dgrad_x3_c1w": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
     "slk_conv2_dgrad_x3_c1w_nslab": [_I],
     "slk_reduce_slabs": [_P, _I, _I, _P, _I, _P],
     "slk_sgd_from_slabs": [_P, _P, _P, _I, _I, _F, _P],
@@ -93,7 +94,8 @@ _SIGS = {
     "slk_wide_fc_shadow": [_P, _P, _P],
     "slk_tick": [_P, _P],
 }
-_RESTYPES = {"slk_error_string": ctypes.c_char_p, "slk_build_id": ctypes.c_char_p, "slk_conv2_act16_bytes": ctypes.c_int64}
+_RESTYPES = {"slk_error_string": ctypes.c_char_p, "slk_build_id": ctypes.c_char_p, "slk_conv2_act16_bytes": ctypes.c_int64,
+             "slk_relu_bits_bytes": ctypes.c_int64}
 
 SYMBOLS = tuple(_SIGS)
 

@@ -154,7 +154,7 @@ class Replicated:
         c.forward(x)
         cslabs = c._buf.get("c1w_slabs", (ops.conv2_dgrad_c1w_nslab(B), ops.CLIENT_NPARAM), torch.float32, c.device)
         _, loss_i, s2, s3 = s.forward_backward(None, y, scale, act_amax=c._act_amax, act16=c._act16,
-                                               client_fuse=(x, c.W1.detach(), c.b1.detach(), cslabs))
+                                               client_fuse=(x, c._relu_bits, cslabs))
         k = ops.CONV2_SLAB
         ops.sgd_multi_from_slabs([(None, c.grads, cslabs), (None, s.grads[:k], s2), (None, s.grads[k:], s3)], 0.0)
         ops.loss_sum(loss_i, scale, self.loss_slot)
@@ -227,24 +227,51 @@ class Replicated:
         self.global_step += 1
 
 
-class Pipeline:
-    """2-rank client/server pipeline with m micro-batches. `role` is "client" or "server".
+class Hub:
+    """N-1 client ranks (0..N-2) feed one server rank (N-1) — SplitFed, BASELINE config 4; with one
+    client it is the 2-GPU client/server pipeline (config 3, `Pipeline`). Each client cuts its batch
+    into `micro` micro-batches and sends micro-batch k's cut (+ labels, + its per-sample max on GPUs,
+    so the server's x3 kernels need not re-read the cut for their scales) while computing k+1.
 
-    compress (default on for CUDA tensors): the cut and its gradient travel through the lossless
-    sparse codec (codec.py): per step one int32 header with the m micro-batches' nonzero counts, then
-    per micro-batch the bit mask + the nonzero activations out and the gradient at those positions back.
-    Results are bit-identical to the dense exchange; `exchange_bytes` counts what actually moved and
-    `dense_bytes` what the dense exchange would have moved."""
+    Server: its buffers are laid out [micro-batch k][client c][b] so that micro-batch k of EVERY client
+    is one contiguous chunk of nc*b samples: the server runs one forward/loss/backward per chunk (not
+    one per (client, micro-batch) part), captured once per chunk in a HIP graph (`graph`, default on
+    GPUs; the exchange stays outside the graphs), accumulates its gradient across chunks, returns each
+    part's cut gradient as soon as its chunk is done, and steps once: exactly the reference's step at
+    the concatenated batch nc*B (src/server_part.py:47-52; the mean-loss scale 1/(nc*B) is applied in
+    the cross-entropy kernel). Clients all-reduce their 320-float gradient and step.
 
-    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None, compress: bool = True):
-        assert role in ("client", "server")
-        self.stage, self.role, self.peer, self.micro, self.group = stage, role, peer, micro, group
+    compress (default on for CUDA tensors): the cut and its gradient travel through the lossless sparse
+    codec (codec.py): per micro-batch a 4-byte count, the bit mask and the nonzero activations out, the
+    gradient at those positions back. The sizes RCCL's point-to-point calls need are learned per
+    micro-batch (the client waits only for micro-batch k's encode before sending it, on a side stream,
+    while k+1 computes; the server posts micro-batch k's receives once its count has landed), so no
+    step-wide host sync holds the first send back. Results are bit-identical to the dense exchange.
+    `exchange_bytes` counts what moved on this rank's link(s), `dense_bytes` what the dense exchange
+    would have moved."""
+
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress: bool = True,
+                 group=None, server_rank: Optional[int] = None, client_ranks=None, graph: bool = True):
+        self.stage, self.rank, self.world = stage, rank, world
+        self.server_rank = world - 1 if server_rank is None else server_rank
+        self.client_ranks = list(range(world - 1)) if client_ranks is None else list(client_ranks)
+        self.nclients = len(self.client_ranks)
+        self.client_group = client_group
+        self.group = group
+        self.micro = micro
         self.compress = compress
+        self.graph = graph
         self.global_step = 0
         self._bufs = {}
+        self._graphs = {}
+        self._side = None
         self.exchange_bytes = 0
         self.dense_bytes = 0
         self._codec = None
+
+    @property
+    def is_server(self):
+        return self.rank == self.server_rank
 
     def _use_codec(self, device):
         if not (self.compress and torch.device(device).type == "cuda"):
@@ -254,328 +281,267 @@ class Pipeline:
             self._codec = CutCodec()
         return self._codec
 
-    def _buf(self, name, shape, dtype, device):
+    @staticmethod
+    def _ship_amax(device) -> bool:
+        """GPU stages exchange the cut's per-sample max with the cut (both sides decide alike)."""
+        return torch.device(device).type == "cuda"
+
+    def _buf(self, name, shape, dtype, device, pin=False):
         t = self._bufs.get(name)
-        if t is None or tuple(t.shape) != tuple(shape) or t.device != device:
-            t = torch.empty(shape, dtype=dtype, device=device)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or (not pin and t.device != device):
+            t = torch.empty(shape, dtype=dtype, pin_memory=True) if pin else torch.empty(shape, dtype=dtype, device=device)
             self._bufs[name] = t
         return t
 
+    def _side_stream(self, device):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device)
+        return self._side
+
+    def _p2p(self, op, t, peer, side=None):
+        """isend / irecv on `side` (a CUDA stream: RCCL then orders the transfer after that stream's
+        work only, not after everything queued on the current stream)."""
+        if side is None:
+            return op(t, peer, group=self.group)
+        with torch.cuda.stream(side):
+            return op(t, peer, group=self.group)
+
+    def _recv_count(self, head, src, slot, pinned):
+        """Receive a 1-element int32 count from `src` and return it on the host, without waiting for
+        the compute queued on the current stream (side stream + pinned copy)."""
+        dev = head.device
+        if _host_staged(head, self.group):
+            h = torch.empty(1, dtype=torch.int32)
+            dist.irecv(h, src, group=self.group).wait()
+            head.copy_(h)
+            return int(h.item())
+        side = self._side_stream(dev)
+        w = self._p2p(dist.irecv, head, src, side)
+        with torch.cuda.stream(side):
+            w.wait()
+            pinned[slot:slot + 1].copy_(head, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        ev.synchronize()
+        return int(pinned[slot].item())
+
+    # ------------------------------------------------------------------------------ client
     def client_step(self, x, y):
-        B = x.shape[0]
-        m = self.micro
-        assert B % m == 0, "batch must be divisible by the micro-batch count"
-        mb = B // m
-        c = self.stage
-        dev = x.device
-        acts = self._buf("acts", (B, 32, 26, 26), torch.float32, dev)
-        cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, dev)
-        codec = self._use_codec(dev)
-        if codec is not None:
-            return self._client_step_codec(codec, x, y, acts, cuts, m, mb)
-        sends, recvs = [], []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            c.forward(x[sl], out=acts[sl])
-            sends.append(isend(acts[sl], self.peer, group=self.group))
-            sends.append(isend(y[sl], self.peer, group=self.group))
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            recvs.append(irecv(cuts[sl], self.peer, group=self.group))
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            recvs[k].wait()
-            c.backward(cuts[sl], x=x[sl], act=acts[sl], accumulate=k > 0)
-        for w in sends:
-            w.wait()
-        c.step()
-        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + y.numel() * 8
-        self.global_step += 1
-
-    def _client_step_codec(self, codec, x, y, acts, cuts, m, mb):
-        c = self.stage
-        n = mb * 32 * 26 * 26
-        bufs = []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            c.forward(x[sl], out=acts[sl])
-            b = codec.buffers(("c", k), n, x.device)
-            codec.encode(acts[sl], b)
-            bufs.append(b)
-        head = self._buf("head", (m,), torch.int32, x.device)
-        for k in range(m):
-            head[k:k + 1].copy_(bufs[k][3])
-        totals = head.tolist()            # the one host sync of the step: sizes of the sparse payloads
-        sends = [isend(head, self.peer, group=self.group)]
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            sends.append(isend(bufs[k][0], self.peer, group=self.group))
-            sends.append(isend(y[sl], self.peer, group=self.group))
-            if totals[k]:
-                sends.append(isend(bufs[k][4][:totals[k]], self.peer, group=self.group))
-        gv = [self._buf(("gvals", k), (n,), torch.float32, x.device) for k in range(m)]
-        recvs = [irecv(gv[k][:totals[k]], self.peer, group=self.group) if totals[k] else None for k in range(m)]
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            if recvs[k] is not None:
-                recvs[k].wait()
-            codec.unpack(cuts[sl], bufs[k], vals=gv[k])
-            c.backward(cuts[sl], x=x[sl], act=acts[sl], accumulate=k > 0)
-        for w in sends:
-            w.wait()
-        c.step()
-        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + y.numel() * 8
-        self.dense_bytes = 2 * acts.numel() * 4 + y.numel() * 8
-        self.global_step += 1
-
-    def server_step(self, B: int, device):
-        m = self.micro
-        mb = B // m
-        s = self.stage
-        acts = self._buf("acts", (B, 32, 26, 26), torch.float32, device)
-        labels = self._buf("labels", (B,), torch.int64, device)
-        cuts = self._buf("cuts", (B, 32, 26, 26), torch.float32, device)
-        parts = self._buf("loss_parts", (m,), torch.float32, device)
-        codec = self._use_codec(device)
-        if codec is not None:
-            return self._server_step_codec(codec, B, device, acts, labels, cuts, parts, m, mb)
-        recvs = []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            recvs.append((irecv(acts[sl], self.peer, group=self.group),
-                          irecv(labels[sl], self.peer, group=self.group)))
-        sends = []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            recvs[k][0].wait()
-            recvs[k][1].wait()
-            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / B, accumulate=k > 0, cut_grad=cuts[sl])
-            _loss_sum(loss_i, 1.0 / B, parts[k:k + 1])
-            sends.append(isend(cuts[sl], self.peer, group=self.group))
-        s.step()
-        s.log_loss(parts, scale=1.0, step=self.global_step)
-        for w in sends:
-            w.wait()
-        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
-        self.global_step += 1
-
-    def _server_step_codec(self, codec, B, device, acts, labels, cuts, parts, m, mb):
-        s = self.stage
-        n = mb * 32 * 26 * 26
-        head = self._buf("head", (m,), torch.int32, device)
-        irecv(head, self.peer, group=self.group).wait()
-        totals = head.tolist()            # the one host sync of the step: sizes of the sparse payloads
-        bufs, recvs = [], []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            b = codec.buffers(("s", k), n, device)
-            bufs.append(b)
-            rk = [irecv(b[0], self.peer, group=self.group), irecv(labels[sl], self.peer, group=self.group)]
-            if totals[k]:
-                rk.append(irecv(b[4][:totals[k]], self.peer, group=self.group))
-            recvs.append(rk)
-        sends = []
-        for k in range(m):
-            sl = slice(k * mb, (k + 1) * mb)
-            for r in recvs[k]:
-                r.wait()
-            codec.offsets(n, bufs[k])
-            codec.unpack(acts[sl], bufs[k])
-            _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / B, accumulate=k > 0, cut_grad=cuts[sl])
-            _loss_sum(loss_i, 1.0 / B, parts[k:k + 1])
-            gv = self._buf(("gvals", k), (n,), torch.float32, device)
-            codec.pack(cuts[sl], bufs[k], vals=gv)
-            if totals[k]:
-                sends.append(isend(gv[:totals[k]], self.peer, group=self.group))
-        s.step()
-        s.log_loss(parts, scale=1.0, step=self.global_step)
-        for w in sends:
-            w.wait()
-        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + labels.numel() * 8
-        self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
-        self.global_step += 1
-
-
-class Hub:
-    """N-1 client ranks (0..N-2) feed one server rank (N-1). `compress` as for Pipeline: per client
-    and step one int32 header of the micro-batch nonzero counts, then mask + values each way."""
-
-    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress: bool = True):
-        self.stage, self.rank, self.world = stage, rank, world
-        self.server_rank = world - 1
-        self.nclients = world - 1
-        self.client_group = client_group
-        self.micro = micro
-        self.compress = compress
-        self.global_step = 0
-        self._bufs = {}
-        self.exchange_bytes = 0
-        self.dense_bytes = 0
-        self._codec = None
-
-    _use_codec = Pipeline._use_codec
-
-    @property
-    def is_server(self):
-        return self.rank == self.server_rank
-
-    def _buf(self, name, shape, dtype, device):
-        t = self._bufs.get(name)
-        if t is None or tuple(t.shape) != tuple(shape) or t.device != device:
-            t = torch.empty(shape, dtype=dtype, device=device)
-            self._bufs[name] = t
-        return t
-
-    def client_step(self, x, y):
-        """Client k: forward each of `micro` micro-batches and send it (+ labels) while computing the
-        next; back-propagate each returned cut-gradient slice as it lands; all-reduce; SGD."""
+        """Forward each micro-batch and send it while computing the next; back-propagate each returned
+        cut-gradient slice as it lands; all-reduce the client gradient over the client ranks; SGD."""
         c = self.stage
         B, m = x.shape[0], self.micro
         assert B % m == 0, "batch must be divisible by the micro-batch count"
         b = B // m
-        act = self._buf("act", (B, 32, 26, 26), torch.float32, x.device)
-        cut = self._buf("cut", (B, 32, 26, 26), torch.float32, x.device)
-        codec = self._use_codec(x.device)
-        if codec is not None:
-            return self._client_step_codec(codec, x, y, act, cut, m, b)
-        sends, recvs = [], []
-        for k in range(m):
-            sl = slice(k * b, (k + 1) * b)
-            c.forward(x[sl], out=act[sl])
-            sends.append(isend(act[sl], self.server_rank))
-            sends.append(isend(y[sl], self.server_rank))
-        for k in range(m):
-            recvs.append(irecv(cut[k * b:(k + 1) * b], self.server_rank))
-        for k in range(m):
-            sl = slice(k * b, (k + 1) * b)
-            recvs[k].wait()
-            c.backward(cut[sl], x=x[sl], act=act[sl], accumulate=k > 0)
-        for w in sends:
-            w.wait()
-        if self.nclients > 1:
-            dist.all_reduce(c.grads, group=self.client_group)
-        c.step()
-        self.exchange_bytes = self.dense_bytes = 2 * act.numel() * 4 + y.numel() * 8
-        self.global_step += 1
-
-    def _client_step_codec(self, codec, x, y, act, cut, m, b):
-        c = self.stage
+        dev = x.device
+        srv = self.server_rank
+        act = self._buf("act", (B, 32, 26, 26), torch.float32, dev)
+        cut = self._buf("cut", (B, 32, 26, 26), torch.float32, dev)
+        ship = self._ship_amax(dev)
+        if ship:
+            c.emit_amax = True
+            amx = self._buf("amax", (B,), torch.float32, dev)
+        codec = self._use_codec(dev)
         n = b * 32 * 26 * 26
-        bufs = []
+        sends, bufs, evs = [], [], []
+        counts = self._buf("counts_host", (m,), torch.int32, dev, pin=True) if codec is not None else None
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             c.forward(x[sl], out=act[sl])
-            bk = codec.buffers(("c", k), n, x.device)
+            if ship:
+                amx[sl].copy_(c._act_amax)
+            if codec is None:
+                sends += [isend(act[sl], srv, self.group), isend(y[sl], srv, self.group)]
+                if ship:
+                    sends.append(isend(amx[sl], srv, self.group))
+                continue
+            bk = codec.buffers(("c", k), n, dev)
             codec.encode(act[sl], bk)
             bufs.append(bk)
-        head = self._buf("head", (m,), torch.int32, x.device)
-        for k in range(m):
-            head[k:k + 1].copy_(bufs[k][3])
-        totals = head.tolist()
-        sends = [isend(head, self.server_rank)]
-        for k in range(m):
-            sl = slice(k * b, (k + 1) * b)
-            sends.append(isend(bufs[k][0], self.server_rank))
-            sends.append(isend(y[sl], self.server_rank))
-            if totals[k]:
-                sends.append(isend(bufs[k][4][:totals[k]], self.server_rank))
-        gv = [self._buf(("gvals", k), (n,), torch.float32, x.device) for k in range(m)]
-        recvs = [irecv(gv[k][:totals[k]], self.server_rank) if totals[k] else None for k in range(m)]
+            counts[k:k + 1].copy_(bk[3], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            evs.append(ev)
+        totals = []
+        if codec is not None:
+            side = self._side_stream(dev)
+            for k in range(m):
+                sl = slice(k * b, (k + 1) * b)
+                evs[k].synchronize()          # micro-batch k's encode only: k+1.. keep computing
+                t = int(counts[k].item())
+                totals.append(t)
+                side.wait_event(evs[k])
+                seq = [bufs[k][3], bufs[k][0], y[sl]] + ([amx[sl]] if ship else []) + ([bufs[k][4][:t]] if t else [])
+                sends += [self._p2p(isend, u, srv, side) for u in seq]
+            gv = [self._buf(("gvals", k), (n,), torch.float32, dev) for k in range(m)]
+            recvs = [self._p2p(irecv, gv[k][:totals[k]], srv, side) if totals[k] else None for k in range(m)]
+        else:
+            side = self._side_stream(dev) if dev.type == "cuda" else None
+            recvs = [self._p2p(irecv, cut[k * b:(k + 1) * b], srv, side) for k in range(m)]
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             if recvs[k] is not None:
                 recvs[k].wait()
-            codec.unpack(cut[sl], bufs[k], vals=gv[k])
+            if codec is not None:
+                codec.unpack(cut[sl], bufs[k], vals=gv[k])
             c.backward(cut[sl], x=x[sl], act=act[sl], accumulate=k > 0)
         for w in sends:
             w.wait()
         if self.nclients > 1:
             dist.all_reduce(c.grads, group=self.client_group)
         c.step()
-        self.exchange_bytes = m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + y.numel() * 8
-        self.dense_bytes = 2 * act.numel() * 4 + y.numel() * 8
+        extra = y.numel() * 8 + (B * 4 if ship else 0)
+        self.dense_bytes = 2 * act.numel() * 4 + extra
+        self.exchange_bytes = (self.dense_bytes if codec is None else
+                               m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + extra)
         self.global_step += 1
 
-    def server_step(self, B: int, device):
-        """B = per-client batch; the server step covers (N-1)*B samples, consumed part by part in
-        (micro-batch, client) order as they arrive, gradient accumulated, ONE SGD step."""
+    # ------------------------------------------------------------------------------ server
+    def _chunk(self, k, B, device, codec):
+        """Micro-batch k of every client as ONE server step part: [unpack] -> forward / loss / backward
+        with the gradient accumulated over chunks -> scaled loss into its slot -> [pack]."""
         s = self.stage
         m, nc = self.micro, self.nclients
         b, G = B // m, nc * B
+        CH = nc * b
+        n = b * 32 * 26 * 26
         acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
-        parts = self._buf("loss_parts", (m * nc,), torch.float32, device)
-        codec = self._use_codec(device)
+        parts = self._buf("loss_parts", (m,), torch.float32, device)
+        ch = slice(k * CH, (k + 1) * CH)
         if codec is not None:
-            return self._server_step_codec(codec, B, device, acts, labels, cuts, parts)
-        reqs = {}
-        for c in range(nc):
-            for k in range(m):
-                sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                reqs[c, k] = (irecv(acts[sl], c), irecv(labels[sl], c))
-        sends, part = [], 0
-        for k in range(m):
-            for c in range(nc):
-                sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                for r in reqs[c, k]:
-                    r.wait()
-                _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=part > 0, cut_grad=cuts[sl])
-                _loss_sum(loss_i, 1.0 / G, parts[part:part + 1])
-                sends.append(isend(cuts[sl], c))
-                part += 1
-        s.step()
-        s.log_loss(parts, scale=1.0, step=self.global_step)
-        for w in sends:
-            w.wait()
-        self.exchange_bytes = self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
-        self.global_step += 1
+            for ci in range(nc):
+                bk = codec.buffers(("s", ci, k), n, device)
+                codec.offsets(n, bk)
+                codec.unpack(acts[k * CH + ci * b:k * CH + (ci + 1) * b], bk)
+        kw = {}
+        if self._ship_amax(device):
+            kw["act_amax"] = self._buf("amax", (G,), torch.float32, device)[ch]
+        _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
+        _loss_sum(loss_i, 1.0 / G, parts[k:k + 1])
+        if codec is not None:
+            for ci in range(nc):
+                bk = codec.buffers(("s", ci, k), n, device)
+                codec.pack(cuts[k * CH + ci * b:k * CH + (ci + 1) * b], bk,
+                           vals=self._buf(("gvals", ci, k), (n,), torch.float32, device))
 
-    def _server_step_codec(self, codec, B, device, acts, labels, cuts, parts):
+    def _graphed(self, device) -> bool:
+        return self.graph and torch.device(device).type == "cuda"
+
+    def _prepare(self, B, device, codec):
+        """Capture one HIP graph per chunk (first step at this batch size), BEFORE any receive is posted:
+        the warm-up runs on zeroed inputs in the very buffers the receives fill later."""
+        if not self._graphed(device) or all((k, B, codec is not None) in self._graphs for k in range(self.micro)):
+            return
+        G = self.nclients * B
+        self._buf("acts", (G, 32, 26, 26), torch.float32, device).zero_()
+        self._buf("labels", (G,), torch.int64, device).zero_()
+        if self._ship_amax(device):
+            self._buf("amax", (G,), torch.float32, device).zero_()
+        n = (B // self.micro) * 32 * 26 * 26
+        st = torch.cuda.Stream(device)
+        for k in range(self.micro):
+            if codec is not None:
+                for ci in range(self.nclients):
+                    codec.buffers(("s", ci, k), n, device)[0].zero_()
+            st.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(st):
+                self._chunk(k, B, device, codec)
+            torch.cuda.current_stream(device).wait_stream(st)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._chunk(k, B, device, codec)
+            self._graphs[k, B, codec is not None] = g
+        torch.cuda.current_stream(device).synchronize()
+
+    def _run_chunk(self, k, B, device, codec):
+        if self._graphed(device):
+            self._graphs[k, B, codec is not None].replay()
+        else:
+            self._chunk(k, B, device, codec)
+
+    def server_step(self, B: int, device):
+        """B = per-client batch; the server step covers nc*B samples in `micro` chunks, ONE SGD step."""
         s = self.stage
         m, nc = self.micro, self.nclients
+        assert B % m == 0, "batch must be divisible by the micro-batch count"
         b, G = B // m, nc * B
+        CH = nc * b
         n = b * 32 * 26 * 26
-        heads = [self._buf(("head", c), (m,), torch.int32, device) for c in range(nc)]
-        hreq = [irecv(heads[c], c) for c in range(nc)]
+        ship = self._ship_amax(device)
+        acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
+        labels = self._buf("labels", (G,), torch.int64, device)
+        cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
+        amx = self._buf("amax", (G,), torch.float32, device) if ship else None
+        parts = self._buf("loss_parts", (m,), torch.float32, device)
+        codec = self._use_codec(device)
+        self._prepare(B, device, codec)
+        part = lambda k, ci: slice(k * CH + ci * b, k * CH + (ci + 1) * b)  # noqa: E731
+        reqs = {}
+        if codec is None:
+            for ci, cr in enumerate(self.client_ranks):
+                for k in range(m):
+                    sl = part(k, ci)
+                    reqs[ci, k] = [irecv(acts[sl], cr, self.group), irecv(labels[sl], cr, self.group)]
+                    if ship:
+                        reqs[ci, k].append(irecv(amx[sl], cr, self.group))
+        else:
+            pinned = self._buf("counts_host", (m * nc,), torch.int32, device, pin=True)
         totals = {}
-        for c in range(nc):
-            hreq[c].wait()
-            for k, t in enumerate(heads[c].tolist()):
-                totals[c, k] = t
-        reqs, bufs = {}, {}
-        for c in range(nc):
-            for k in range(m):
-                sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                bk = codec.buffers(("s", c, k), n, device)
-                bufs[c, k] = bk
-                rk = [irecv(bk[0], c), irecv(labels[sl], c)]
-                if totals[c, k]:
-                    rk.append(irecv(bk[4][:totals[c, k]], c))
-                reqs[c, k] = rk
-        sends, part = [], 0
+        sends = []
         for k in range(m):
-            for c in range(nc):
-                sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                for r in reqs[c, k]:
+            if codec is not None:
+                # per client, in its send order: the count, then mask / labels / max / values
+                for ci, cr in enumerate(self.client_ranks):
+                    sl = part(k, ci)
+                    bk = codec.buffers(("s", ci, k), n, device)
+                    t = self._recv_count(self._buf(("head", ci, k), (1,), torch.int32, device), cr, k * nc + ci, pinned)
+                    totals[ci, k] = t
+                    seq = [bk[0], labels[sl]] + ([amx[sl]] if ship else []) + ([bk[4][:t]] if t else [])
+                    # on the side stream: the transfer need not wait for chunk k-1's compute
+                    reqs[ci, k] = [self._p2p(irecv, u, cr, self._side_stream(device)) for u in seq]
+            for ci in range(nc):
+                for r in reqs[ci, k]:
                     r.wait()
-                codec.offsets(n, bufs[c, k])
-                codec.unpack(acts[sl], bufs[c, k])
-                _, loss_i = s.compute(acts[sl], labels[sl], 1.0 / G, accumulate=part > 0, cut_grad=cuts[sl])
-                _loss_sum(loss_i, 1.0 / G, parts[part:part + 1])
-                gv = self._buf(("gvals", c, k), (n,), torch.float32, device)
-                codec.pack(cuts[sl], bufs[c, k], vals=gv)
-                if totals[c, k]:
-                    sends.append(isend(gv[:totals[c, k]], c))
-                part += 1
+            self._run_chunk(k, B, device, codec)
+            for ci, cr in enumerate(self.client_ranks):
+                if codec is None:
+                    sends.append(isend(cuts[part(k, ci)], cr, self.group))
+                elif totals[ci, k]:
+                    gv = self._buf(("gvals", ci, k), (n,), torch.float32, device)
+                    sends.append(isend(gv[:totals[ci, k]], cr, self.group))
         s.step()
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:
             w.wait()
-        self.exchange_bytes = (nc * m * 4 + sum(bufs[key][0].numel() * 4 + 2 * t * 4 for key, t in totals.items())
-                               + labels.numel() * 8)
-        self.dense_bytes = 2 * acts.numel() * 4 + labels.numel() * 8
+        extra = labels.numel() * 8 + (G * 4 if ship else 0)
+        self.dense_bytes = 2 * acts.numel() * 4 + extra
+        self.exchange_bytes = (self.dense_bytes if codec is None else
+                               nc * m * 4 + sum(codec.buffers(("s", ci, k), n, device)[0].numel() * 4 + 2 * t * 4
+                                                for (ci, k), t in totals.items()) + extra)
         self.global_step += 1
+
+    def cuts_by_client(self, B: int) -> torch.Tensor:
+        """The last step's cut gradient in client order [client][B] (the server keeps [k][client][b])."""
+        m, nc = self.micro, self.nclients
+        cuts = self._bufs["cuts"]
+        return cuts.view(m, nc, B // m, *cuts.shape[1:]).transpose(0, 1).reshape(nc * B, *cuts.shape[1:])
+
+
+class Pipeline(Hub):
+    """2-rank client/server pipeline (BASELINE config 3) with m micro-batches: the hub with one client.
+    `role` is "client" or "server", `peer` the other rank. Both sides accumulate their gradient over
+    the micro-batches and step once per batch (= the reference step at batch B)."""
+
+    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None, compress: bool = True,
+                 graph: bool = True):
+        assert role in ("client", "server")
+        me = dist.get_rank()
+        super().__init__(stage, me, dist.get_world_size(), None, micro, compress, group=group,
+                         server_rank=peer if role == "client" else me,
+                         client_ranks=[me] if role == "client" else [peer], graph=graph)
+        self.role, self.peer = role, peer
 
 
 class FedAvg:

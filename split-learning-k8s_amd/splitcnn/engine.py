@@ -168,6 +168,7 @@ class ClientStage:
         self._act = None
         self._act_amax = None
         self._act16 = None
+        self._relu_bits = None
         self.emit_amax = False  # forward also writes the per-sample max of act (x3 server kernels)
         # forward writes the x3 server operand (act16 images + act_amax) instead of the f32 act: the
         # fused single-GPU step, where the cut never leaves the device (forward then returns None)
@@ -194,9 +195,10 @@ class ClientStage:
         if self.emit_act16:
             amax = self._buf.get("act_amax", (B,), torch.float32, self.device)
             a16 = self._buf.get("act16", (ops.conv2_act16_bytes(B),), torch.uint8, self.device)
+            bits = self._buf.get("relu_bits", (B, ops.RELU_BITS_WORDS), torch.int32, self.device)
             with TIMER("conv1_fwd"):
-                act = ops.conv1_fwd_x3(x, self.W1.detach(), self.b1.detach(), amax, a16, act=out)
-            self._x, self._act, self._act_amax, self._act16 = x, act, amax, a16
+                act = ops.conv1_fwd_x3(x, self.W1.detach(), self.b1.detach(), amax, a16, act=out, relu_bits=bits)
+            self._x, self._act, self._act_amax, self._act16, self._relu_bits = x, act, amax, a16, bits
             return act
         act = out if out is not None else self._buf.get("act", (B, 32, 26, 26), torch.float32, self.device)
         amax = self._buf.get("act_amax", (B,), torch.float32, self.device) if self.emit_amax else None
@@ -280,7 +282,7 @@ class ServerStage:
         conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
         of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise.
         act16 (with act_amax, x3 forward + wgrad only): the client's split input images
-        (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, W1, b1,
+        (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, relu_bits,
         slabs) (x3 dgrad only, single-GPU step): the dgrad also runs the client's ReLU backward +
         conv1 wgrad into `slabs` and the cut gradient is not materialised (returned as None)."""
         B = labels.shape[0]
@@ -314,9 +316,9 @@ class ServerStage:
         if client_fuse is not None:
             if di != "x3":
                 raise ValueError("client_fuse needs the x3 dgrad (conv preset 'x3' or 'x3w')")
-            cx, cW1, cb1, cslabs = client_fuse
+            cx, cbits, cslabs = client_fuse
             with TIMER("conv2_dgrad"):
-                ops.conv2_dgrad_client_slabs(dpooled, code, W2, cx, cW1, cb1, dp_amax=dp_amax, slabs=cslabs)
+                ops.conv2_dgrad_client_slabs(dpooled, code, W2, cx, cbits, dp_amax=dp_amax, slabs=cslabs)
             cut_grad = None
         else:
             if cut_grad is None:
@@ -408,7 +410,8 @@ class SplitTrainer:
         self.client.emit_amax = "x3" in (self.server.impl_fwd, self.server.impl_wgrad)
         self.client.emit_act16 = (self.server.impl_fwd, self.server.impl_wgrad) == ("x3", "x3") and act16
         # the x3 dgrad also runs the client's ReLU backward + conv1 wgrad (no cut gradient in HBM)
-        self.fuse_client_backward = self.server.impl_dgrad == "x3" and fuse_client_backward
+        # (the client's ReLU mask comes from the bit map conv1_fwd_x3 writes next to the images)
+        self.fuse_client_backward = self.server.impl_dgrad == "x3" and self.client.emit_act16 and fuse_client_backward
         self.graph = graph
         self._graphs = {}
         self.global_step = 0
@@ -425,7 +428,7 @@ class SplitTrainer:
             slabs = c._buf.get("c1w_slabs", (ops.conv2_dgrad_c1w_nslab(x.shape[0]), ops.CLIENT_NPARAM),
                                torch.float32, self.device)
             self.server.step_request(act, y, act_amax=c._act_amax, act16=a16,
-                                     client_fuse=(x, c.W1.detach(), c.b1.detach(), slabs))
+                                     client_fuse=(x, c._relu_bits, slabs))
             c.step_from_slabs(slabs)
             return
         cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax, act16=a16)

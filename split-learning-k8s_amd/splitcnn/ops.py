@@ -69,13 +69,22 @@ def conv1_fwd(x, W1, b1, out=None, act_amax=None):
     return act
 
 
-def conv1_fwd_x3(x, W1, b1, act_amax, act16, act=None):
+RELU_BITS_WORDS = 676  # int32 words of the cut's ReLU bit map per sample (slk_relu_bits_bytes / 4)
+
+
+def relu_bits_buffer(B: int, device) -> torch.Tensor:
+    return torch.empty((B, RELU_BITS_WORDS), dtype=torch.int32, device=device)
+
+
+def conv1_fwd_x3(x, W1, b1, act_amax, act16, act=None, relu_bits=None):
     """conv1 + ReLU writing the x3 server operand: act_amax [B] and the act16 images
-    (conv2_act16_bytes(B) uint8), plus the f32 act when `act` is given. Returns act (or None)."""
+    (conv2_act16_bytes(B) uint8), plus the f32 act when `act` is given and the cut's ReLU bit map
+    (int32 [B, RELU_BITS_WORDS], the fused client backward's mask) when `relu_bits` is. Returns act (or None)."""
     B = batch_of(x, (1, 28, 28), "x")
     ap = _dev(act, "act", (B, 32, 26, 26)) if act is not None else None
+    bp = _dev(relu_bits, "relu_bits", (B, RELU_BITS_WORDS), torch.int32) if relu_bits is not None else None
     _lib.call("slk_conv1_fwd_x3", _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)), _dev(b1, "conv1.bias", (32,)),
-              ap, _dev(act_amax, "act_amax", (B,)), _act16(act16, B), B, _stream(x))
+              ap, _dev(act_amax, "act_amax", (B,)), _act16(act16, B), bp, B, _stream(x))
     return act
 
 
@@ -95,10 +104,10 @@ def conv2_dgrad_c1w_nslab(B: int) -> int:
     return _lib.query("slk_conv2_dgrad_x3_c1w_nslab", B)
 
 
-def conv2_dgrad_client_slabs(dpooled, code, W2, x, W1, b1, dp_amax=None, slabs=None):
+def conv2_dgrad_client_slabs(dpooled, code, W2, x, relu_bits, dp_amax=None, slabs=None):
     """x3 dgrad fused with the client's ReLU backward + conv1 wgrad: returns the client's gradient
     slabs [conv2_dgrad_c1w_nslab(B), 320] (conv1_wgrad_slabs' layout); the cut gradient is not
-    materialised. W1 / b1 must be the weights of the forward that produced the cut."""
+    materialised. relu_bits: the ReLU bit map conv1_fwd_x3 wrote for this cut."""
     B = _pooled_batch(dpooled)
     batch_of(x, (1, 28, 28), "x")
     if x.shape[0] != B:
@@ -107,7 +116,7 @@ def conv2_dgrad_client_slabs(dpooled, code, W2, x, W1, b1, dp_amax=None, slabs=N
     slabs = _out(slabs, (conv2_dgrad_c1w_nslab(B), CLIENT_NPARAM), x, name="slabs")
     _lib.call("slk_conv2_dgrad_x3_c1w", _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
               _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
-              _dev(x, "x"), _dev(W1, "conv1.weight", (32, 1, 3, 3)), _dev(b1, "conv1.bias", (32,)),
+              _dev(x, "x"), _dev(relu_bits, "relu_bits", (B, RELU_BITS_WORDS), torch.int32),
               _dev(slabs, "slabs"), B, _stream(x))
     return slabs
 

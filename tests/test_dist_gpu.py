@@ -241,13 +241,13 @@ def _worker(rank, world, port, topo, fixture, micro, outdir, compress=True):
                 y = torch.from_numpy(fx[f"y_{s}"]).to(dev)
                 if rank == 0:
                     t.client_step(x, y)
-                    res[f"act_{s}"] = t._bufs["acts"].cpu().numpy()
+                    res[f"act_{s}"] = t._bufs["act"].cpu().numpy()
                     res[f"params_{s}"] = t.stage.params.cpu().numpy()
                     res[f"grads_{s}"] = t.stage.grads.cpu().numpy()
                     res[f"bytes_{s}"] = np.array([t.exchange_bytes, t.dense_bytes])
                 else:
                     t.server_step(x.shape[0], dev)
-                    res[f"cut_{s}"] = t._bufs["cuts"].cpu().numpy()
+                    res[f"cut_{s}"] = t.cuts_by_client(x.shape[0]).cpu().numpy()
                     res[f"params_{s}"] = t.stage.params.cpu().numpy()
                     res[f"grads_{s}"] = t.stage.grads.cpu().numpy()
             if rank == 1:
@@ -267,7 +267,7 @@ def _worker(rank, world, port, topo, fixture, micro, outdir, compress=True):
             else:
                 t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=compress)
                 t.server_step(B, dev)
-                res["cut_1"] = t._bufs["cuts"].cpu().numpy()
+                res["cut_1"] = t.cuts_by_client(B).cpu().numpy()
                 torch.cuda.synchronize()
                 res["losses"] = np.array([l for _, l in t.stage.loss_log.flush()])
             res["params_1"] = t.stage.params.cpu().numpy()

@@ -240,8 +240,11 @@ def test_conv1_x3_images_and_forward_from_images_bitwise(gpu, B):
     am1, i1 = torch.empty(B, device=gpu), torch.full((nb,), 7, dtype=torch.uint8, device=gpu)
     act1 = ops.conv1_fwd_x3(x, W1, b1, am1, i1, act=torch.empty_like(act0))
     am2, i2 = torch.empty(B, device=gpu), torch.full((nb,), 9, dtype=torch.uint8, device=gpu)
-    assert ops.conv1_fwd_x3(x, W1, b1, am2, i2) is None
+    bits = torch.full((B, ops.RELU_BITS_WORDS), -1, dtype=torch.int32, device=gpu)
+    assert ops.conv1_fwd_x3(x, W1, b1, am2, i2, relu_bits=bits) is None
     assert torch.equal(act1, act0) and torch.equal(am1, am0) and torch.equal(am2, am0)
+    # the ReLU bit map is exactly act > 0 (every bit; the padding bits past pixel 675 are zero)
+    assert np.array_equal(_decode_bits(bits), (act0 > 0).reshape(B, 32, 676).cpu().numpy())
     i0 = torch.empty(nb, dtype=torch.uint8, device=gpu)
     p0, c0 = ops.conv2_fwd_pool(act0, W2, b2, impl="x3", act_amax=am0, act16=i0)
     assert torch.equal(i1, i0) and torch.equal(i2, i0)
@@ -255,13 +258,14 @@ def test_conv1_x3_images_and_forward_from_images_bitwise(gpu, B):
 
 def test_trainer_client_images_bitwise(gpu):
     """SplitTrainer with the client writing the x3 images (no f32 cut) and with the f32 cut + the
-    forward writing them: identical parameters and losses after three steps, bit for bit."""
+    forward writing them: identical parameters and losses after three steps, bit for bit (both with the
+    separate client backward: the fused one needs the client's images and bit map)."""
     from splitcnn.data import SyntheticMNIST, init_models
     from splitcnn.engine import SplitTrainer
     out = []
     for img in (True, False):
         a, b = init_models(seed=21)
-        tr = SplitTrainer(a, b, device=gpu, graph=True, conv="x3", act16=img)
+        tr = SplitTrainer(a, b, device=gpu, graph=True, conv="x3", act16=img, fuse_client_backward=False)
         assert tr.client.emit_act16 == img
         data = SyntheticMNIST(22)
         for _ in range(3):
@@ -290,7 +294,7 @@ def test_dgrad_with_fused_client_backward(gpu, B):
     pooled, code = ops.conv2_fwd_pool(act, W2, b2, impl="x3")
     dpa = torch.empty(B, device=gpu)
     _, _, _, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
-    slabs = ops.conv2_dgrad_client_slabs(dp, code, W2, x, W1, b1, dp_amax=dpa)
+    slabs = ops.conv2_dgrad_client_slabs(dp, code, W2, x, _relu_bits(x, W1, b1), dp_amax=dpa)
     assert slabs.shape == (min(3 * B, 256), 320)
     fused = ops.reduce_slabs(slabs).cpu().numpy()
     g = ops.conv2_dgrad(dp, code, W2, impl="x3", dp_amax=dpa)
@@ -299,6 +303,25 @@ def test_dgrad_with_fused_client_backward(gpu, B):
     for sl in (slice(0, 288), slice(288, 320)):
         assert rel_err(fused[sl], sep[sl]) <= 1e-5
         assert rel_err(fused[sl], ref[sl]) <= 1e-5
+
+
+def _relu_bits(x, W1, b1):
+    """The cut's ReLU bit map as the fused step gets it (conv1_fwd_x3 writes it next to the images)."""
+    from splitcnn import ops
+    B = x.shape[0]
+    bits = ops.relu_bits_buffer(B, x.device)
+    ops.conv1_fwd_x3(x, W1, b1, torch.empty(B, device=x.device),
+                     torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=x.device), relu_bits=bits)
+    return bits
+
+
+def _decode_bits(bits):
+    """[B, 676] int32 -> bool [B, 32, 676]: bit 4 (c & 7) + u of word (c >> 3, t) = pixel 4 t + u of channel c."""
+    w = bits.cpu().numpy().view(np.uint32).reshape(-1, 4, 169)
+    c = np.arange(32)
+    sh = (4 * (c & 7))[:, None, None] + np.arange(4)[None, None, :]          # c, 1, u
+    b = (w[:, c >> 3, :, None] >> sh[None].astype(np.uint32)) & 1            # B, c, t, u
+    return b.reshape(-1, 32, 676).astype(bool)
 
 
 def _c1_ref64(x, W1, b1, g):
@@ -386,7 +409,7 @@ def test_default_fused_path_full_size_vs_direct_f32(gpu):
         pooled, code = ops.conv2_fwd_pool_x3i(img, am, W2, b2)
         dpa = torch.empty(B, device=gpu)
         _, _, _, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
-        c1 = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, code, W2, x, W1, b1, dp_amax=dpa))
+        c1 = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, code, W2, x, _relu_bits(x, W1, b1), dp_amax=dpa))
         s2 = ops.reduce_slabs(ops.conv2_wgrad_slabs(None, dp, code, impl="x3", act_amax=am, dp_amax=dpa, act16=img))
         return pooled, code, dp, c1, s2
 
@@ -451,7 +474,7 @@ def test_full_size_x3_error_within_2x_of_f32(gpu):
     dW64, db64 = wgrad64(act, dc)
     checks["dW2"] = errs(sx[:18432], sd[:18432], dW64.reshape(-1))
     checks["db2"] = errs(sx[18432:], sd[18432:], db64)
-    c1x = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cx, W2, x, W1, b1, dp_amax=dpa))
+    c1x = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cx, W2, x, _relu_bits(x, W1, b1), dp_amax=dpa))
     c1d = ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, ops.conv2_dgrad(dp, cx, W2, impl="direct")))
     c164 = torch.from_numpy(_c1_ref64(x, W1, b1, g64)).to(gpu)
     checks["dW1"] = errs(c1x[:288], c1d[:288], c164[:288])
@@ -491,12 +514,12 @@ def test_x3_tiny_sample_maxima_stay_finite(gpu, tiny):
         assert np.isfinite(got).all()
         assert rel_err(got[:18432], dW64.reshape(-1).cpu().numpy()) <= 1e-5
         assert rel_err(got[18432:], db64.cpu().numpy()) <= 1e-5
-    # the fused client backward on the same tiny-dpooled sample (x chosen freely: its mask is recomputed)
+    # the fused client backward on the same tiny-dpooled sample (x chosen freely, with its own ReLU bits)
     from splitcnn.data import SyntheticMNIST, init_models
     a, _ = init_models(seed=79)
     x = SyntheticMNIST(80).batch(B)[0].to(gpu)
     W1, b1 = a.conv1.weight.detach().to(gpu), a.conv1.bias.detach().to(gpu)
-    c1 = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cs, p["W2"], x, W1, b1, dp_amax=dpa)).cpu().numpy()
+    c1 = ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cs, p["W2"], x, _relu_bits(x, W1, b1), dp_amax=dpa)).cpu().numpy()
     assert np.isfinite(c1).all()
     ref = _c1_ref64(x, W1, b1, dgrad64(dc, p["W2"]))
     assert rel_err(c1[:288], ref[:288]) <= 1e-5 and rel_err(c1[288:], ref[288:]) <= 1e-5

@@ -10,7 +10,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "split-learning-k8s_amd"), ROOT, os.path.join(ROOT, "tests")]
 from ref64 import conv_relu64, dgrad64, route64  # noqa: E402
-from test_x3_gpu import _c1_ref64, _inputs  # noqa: E402
+from test_x3_gpu import _c1_ref64, _inputs, _relu_bits  # noqa: E402
 
 from splitcnn import ops  # noqa: E402
 from splitcnn.data import SyntheticMNIST, init_models  # noqa: E402
@@ -67,7 +67,7 @@ _, _, _, dp = ops.fc_xent(px, W3, b3, y, 1.0 / B, dp_amax=dpa)
 g64 = dgrad64(route64(dp, cx), W2)
 ref = torch.from_numpy(_c1_ref64(x, W1, b1, g64))
 paths = {
-    "fused_x3": ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cx, W2, x, W1, b1, dp_amax=dpa)),
+    "fused_x3": ops.reduce_slabs(ops.conv2_dgrad_client_slabs(dp, cx, W2, x, _relu_bits(x, W1, b1), dp_amax=dpa)),
     "x3_then_remask": ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, ops.conv2_dgrad(dp, cx, W2, impl="x3", dp_amax=dpa))),
     "direct_then_remask": ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, ops.conv2_dgrad(dp, cx, W2, impl="direct"))),
     "wino_then_remask": ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x, W1, b1, ops.conv2_dgrad(dp, cx, W2, impl="wino"))),

@@ -51,27 +51,26 @@ def main():
         # this library's own act16 images (layouts may differ between builds)
         L.slk_conv2_act16_bytes.restype = ctypes.c_int64
         L.slk_conv2_act16_bytes.argtypes = [ctypes.c_int]
+        # ABI 2 (round 3): conv1_fwd_x3 also writes the ReLU bit map, the fused dgrad reads it instead of
+        # W1 / b1; older builds (ABI 1) are driven with their own argument lists
+        abi2 = hasattr(L, "slk_relu_bits_bytes")
         L.slk_conv1_fwd_x3.restype = ctypes.c_int
-        L.slk_conv1_fwd_x3.argtypes = [P] * 6 + [ctypes.c_int, P]
+        L.slk_conv1_fwd_x3.argtypes = [P] * (7 if abi2 else 6) + [ctypes.c_int, P]
         a16 = torch.empty(L.slk_conv2_act16_bytes(B), dtype=torch.uint8, device=dev)
         am1 = torch.empty(B, device=dev)
-        assert L.slk_conv1_fwd_x3(p(xg), p(W1), p(b1), None, p(am1), p(a16), B, st) == 0
+        bits = torch.empty(B, 768, dtype=torch.int32, device=dev)
+        c1x = (lambda L, am, img: L.slk_conv1_fwd_x3(p(xg), p(W1), p(b1), None, p(am), p(img), p(bits), B, st)) if abi2 \
+            else (lambda L, am, img: L.slk_conv1_fwd_x3(p(xg), p(W1), p(b1), None, p(am), p(img), B, st))
+        assert c1x(L, am1, a16) == 0
         if "c1x3" in args.ops:
             i1 = torch.empty_like(a16)
-            cases[f"c1x3 {tag}"] = (lambda L=L, am1=am1, i1=i1: L.slk_conv1_fwd_x3(
-                p(xg), p(W1), p(b1), None, p(am1), p(i1), B, st))
+            cases[f"c1x3 {tag}"] = (lambda L=L, am1=am1, i1=i1, f=c1x: f(L, am1, i1))
+        dgc1_args = (lambda: (p(xg), p(bits))) if abi2 else (lambda: (p(xg), p(W1), p(b1)))
         if "fwd," in args.ops + "," :
             po, co, a16o = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16)
             L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
             cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
                 p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
-        if "dgc1" in args.ops:
-            sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
-            L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
-            L.slk_conv2_dgrad_x3_c1w_nslab.restype = ctypes.c_int
-            L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 8 + [ctypes.c_int, P]
-            cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1: L.slk_conv2_dgrad_x3_c1w(
-                p(dp), p(dpa), p(code), p(W2), p(xg), p(W1), p(b1), p(sl), B, st))
         if "fwdi" in args.ops:
             po2, co2 = torch.empty_like(pooled), torch.empty_like(code)
             L.slk_conv2_fwd_pool_x3i.restype = ctypes.c_int
@@ -85,9 +84,10 @@ def main():
         if "dgc1" in args.ops:
             sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
             L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
-            L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 8 + [ctypes.c_int, P]
-            cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1: L.slk_conv2_dgrad_x3_c1w(
-                p(dp), p(dpa), p(code), p(W2), p(xg), p(W1), p(b1), p(sl), B, st))
+            L.slk_conv2_dgrad_x3_c1w_nslab.restype = ctypes.c_int
+            L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * (7 if abi2 else 8) + [ctypes.c_int, P]
+            cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1, xa=dgc1_args(): L.slk_conv2_dgrad_x3_c1w(
+                p(dp), p(dpa), p(code), p(W2), *xa, p(sl), B, st))
         if "wgrad" in args.ops:
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
