@@ -719,9 +719,10 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 // channels contiguous and are read with ds_read_b64_tr_b16 (one 4-pixel x 16-channel block per 16-lane
 // group, delivered column-major): dY image [192 q = 24 y_l + x][32 co], input image [260 px][32 ci], f16
 // (h, l) planes. Unit = (sample, third): output rows 8t..8t+7 (K = 192 = 6 K-steps, no padding);
-// K-chunk c of 8 pixels = row c / 3, columns 8 (c % 3) .. +7, so the input pixel of tap (ky, kx) is a
-// per-(K-step, lane) base + an immediate. dY pixel rows keep the two 32-B co tiles swapped on odd
-// 8-pixel groups (the two 16-lane groups of a half-wave then hit disjoint banks).
+// a K-chunk of 8 pixels = one 8-column segment of one output row (the two 16-lane groups of a half-wave
+// on adjacent rows, see abase below), so the input pixel of tap (ky, kx) is a per-(K-step, lane) base +
+// an immediate. dY pixel rows keep the two 32-B co tiles swapped on odd 8-pixel groups (the two 16-lane
+// groups of a half-wave then hit disjoint banks).
 // A workgroup owns one co half (M = 32) and a K share (units ks, ks + nks, ...); the two co halves
 // of a share run on different workgroups, each splitting the same input rows. A K sum spans samples,
 // so every product must carry ONE scale: the input keeps its sample's 2^s_b (the act16 images' scale)
@@ -870,22 +871,28 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
     };
 
-    // transposed-read bases: group g4 = lane >> 4 (K-chunk), lane 4qq + pp of the group
+    // transposed-read bases: group g4 = lane >> 4 (K-chunk), lane 4qq + pp of the group. K-chunk (K-step
+    // s, g4) = 8 output pixels: segment seg of row orow, with the two 16-lane groups of a half-wave on the
+    // same segment of two adjacent rows (idx = 2 s + (g4 >> 1): orow = 2 (idx / 3) + (g4 & 1), seg =
+    // idx % 3): their input pixels are then 26 apart, 2 mod 4, and the images' (x >> 1) slot swizzle puts
+    // them on disjoint banks (chunks 8 pixels apart in one row were 2-way: tools/lds_banks.py)
     const int g4 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-    int abase[2];  // dY: pixel 8c + qq (+4), co tile mi in slot mi ^ (g4 & 1)
+    int abase[3][2];  // dY: pixel q = 24 orow + 8 seg + qq (+4), co tile mi in slot mi ^ ((q >> 3) & 1)
+    int xbase[3][3];  // input per (this wave's K-step j, kx); X16 images keep ci half h in slot h ^ ((x >> 1) & 1)
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) abase[mi] = (8 * g4 + qq) * 64 + ((mi ^ (g4 & 1)) * 32) + pp * 8;
-    // input bases per (this wave's K-step j, kx); X16 images keep ci half h in slot h ^ ((x >> 1) & 1)
-    int xbase[3][3];
+    for (int j = 0; j < 3; ++j) {
+        const int idx = 2 * (kp + 2 * j) + (g4 >> 1);
+        const int orow = 2 * (idx / 3) + (g4 & 1), seg = idx % 3;
+        const int q0 = 24 * orow + 8 * seg;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+        for (int mi = 0; mi < 2; ++mi) abase[j][mi] = (q0 + qq) * 64 + ((mi ^ ((q0 >> 3) & 1)) * 32) + pp * 8;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-            const int c = 4 * (kp + 2 * j) + g4;
-            const int x = 8 * (c % 3) + qq + kx;
+            const int x = 8 * seg + qq + kx;
             const int slot = X16 ? (h ^ ((x >> 1) & 1)) : h;
-            xbase[j][kx] = 2 * X3W_DYP + (((c / 3) * A_HW + x) * 64) + slot * 32 + pp * 8;
+            xbase[j][kx] = 2 * X3W_DYP + ((orow * A_HW + x) * 64) + slot * 32 + pp * 8;
         }
+    }
     // X16 staging: 2,080 16-B pieces per unit, lane-contiguous (the image is stored as it sits in LDS)
     auto issue_x16 = [&](int uu, char* img) {
         x3_issue_unit_img(act16, uu, __builtin_amdgcn_readfirstlane(tid >> 6), lane, lds_u32(img + 2 * X3W_DYP));
@@ -915,11 +922,10 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         constexpr int N = 3 * NT;
         f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
         auto rdA = [&](int j, int slot) {
-            const int s = kp + 2 * j;
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi) {
-                Ah[slot][mi] = trr(img + abase[mi] + s * 2048);
-                Al[slot][mi] = trr(img + X3W_DYP + abase[mi] + s * 2048);
+                Ah[slot][mi] = trr(img + abase[j][mi]);
+                Al[slot][mi] = trr(img + X3W_DYP + abase[j][mi]);
             }
         };
         auto rdB = [&](int n, int slot) {
