@@ -1,0 +1,63 @@
+"""The fused server head (slk_fc_xent / slk_fc_xent_amax: fc1 forward, cross-entropy forward + backward,
+fc1 input gradient — src/model_def.py:28, src/server_part.py:49-51) against float64 and against the
+separate launches (slk_fc_fwd -> slk_fc_dgrad), over ragged batch sizes (a workgroup holds 4 samples)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref64(pooled, W3, b3, y, scale):
+    p, W, b = (t.double().cpu().numpy() for t in (pooled, W3, b3))
+    z = p.reshape(p.shape[0], -1) @ W.T + b
+    m = z.max(axis=1, keepdims=True)
+    e = np.exp(z - m)
+    sm = e / e.sum(axis=1, keepdims=True)
+    yy = y.cpu().numpy()
+    loss = (m[:, 0] + np.log(e.sum(axis=1))) - z[np.arange(len(yy)), yy]
+    dz = (sm - np.eye(10)[yy]) * scale
+    return z, loss, dz, (dz @ W).reshape(pooled.shape)
+
+
+@pytest.mark.parametrize("B", [1, 7, 16, 17, 100, 4096])
+def test_fc_xent_mfma_vs_float64_and_separate_kernels(gpu, B):
+    from splitcnn import ops
+    g = torch.Generator().manual_seed(B)
+    pooled = torch.relu(torch.randn(B, 64, 12, 12, generator=g)).to(gpu)
+    W3 = (torch.randn(10, 9216, generator=g) * 0.01).to(gpu)
+    b3 = (torch.randn(10, generator=g) * 0.1).to(gpu)
+    y = torch.randint(0, 10, (B,), generator=g).to(gpu)
+    dpa = torch.empty(B, device=gpu)
+    logits, loss_i, dlogits, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+    z64, l64, dz64, dp64 = _ref64(pooled, W3, b3, y, 1.0 / B)
+    assert rel_err(logits.cpu().numpy(), z64) <= 1e-5
+    assert rel_err(loss_i.cpu().numpy(), l64) <= 1e-5
+    assert rel_err(dlogits.cpu().numpy(), dz64) <= 1e-5
+    assert rel_err(dp.cpu().numpy(), dp64) <= 1e-5
+    assert torch.equal(dpa, dp.reshape(B, -1).abs().amax(dim=1))
+    # the separate launches run the same per-phase code: bit-identical logits and input gradient
+    lg2 = ops.fc_fwd(pooled, W3, b3)
+    assert torch.equal(lg2, logits)
+    dp2 = ops.fc_dgrad(dlogits, W3)
+    assert torch.equal(dp2.reshape(dp.shape), dp)
+    # without dp_amax: the same outputs bit for bit
+    r2 = ops.fc_xent(pooled, W3, b3, y, 1.0 / B)
+    assert all(torch.equal(u, v) for u, v in zip(r2, (logits, loss_i, dlogits, dp)))
+
+
+def test_fc_xent_bad_label_sets_flag(gpu):
+    from splitcnn import ops
+    B = 20
+    pooled = torch.rand(B, 64, 12, 12, device=gpu)
+    W3 = torch.randn(10, 9216, device=gpu) * 0.01
+    b3 = torch.zeros(10, device=gpu)
+    y = torch.randint(0, 10, (B,), device=gpu)
+    y[17] = 10
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, loss_i, dlogits, _ = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, err_flag=flag)
+    assert int(flag.item()) == 1
+    assert torch.isnan(loss_i[17]) and torch.isnan(dlogits[17]).all()
+    assert torch.isfinite(loss_i[:17]).all() and torch.isfinite(loss_i[18:]).all()

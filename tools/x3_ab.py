@@ -88,6 +88,14 @@ def main():
             L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * (7 if abi2 else 8) + [ctypes.c_int, P]
             cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1, xa=dgc1_args(): L.slk_conv2_dgrad_x3_c1w(
                 p(dp), p(dpa), p(code), p(W2), *xa, p(sl), B, st))
+        if "fc" in args.ops.split(","):
+            lg, li, dlg, dpo, dpam = (torch.empty(B, 10, device=dev), torch.empty(B, device=dev),
+                                     torch.empty(B, 10, device=dev), torch.empty_like(dp), torch.empty(B, device=dev))
+            yl = y.to(dev)
+            L.slk_fc_xent_amax.restype = ctypes.c_int
+            L.slk_fc_xent_amax.argtypes = [P] * 9 + [ctypes.c_float, P, ctypes.c_int, P]
+            cases[f"fc {tag}"] = (lambda L=L, lg=lg, li=li, dlg=dlg, dpo=dpo, dpam=dpam, yl=yl: L.slk_fc_xent_amax(
+                p(pooled), p(W3), p(b3), p(yl), p(lg), p(li), p(dlg), p(dpo), p(dpam), 1.0 / B, None, B, st))
         if "wgrad" in args.ops:
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
