@@ -605,9 +605,18 @@ def main():
         run_single(args, out)
         if not args.no_hub_loopback:
             try:
-                out["k4_server_loopback"] = hub_loopback_rate(args, out["value"], (out.get("kernels") or {}).get("conv1_fwd"))
+                c1 = (out.get("kernels") or {}).get("conv1_fwd")
+                out["k4_server_loopback"] = hub_loopback_rate(args, out["value"], c1)
+                # the same server step with the dense exchange (no codec kernels on the server; the link
+                # then carries 2x the bytes): which one K4 should run depends on the link rate
+                import torch
+                torch.cuda.empty_cache()
+                out["k4_server_loopback"]["dense_exchange"] = {
+                    k: v for k, v in hub_loopback_rate(argparse.Namespace(**{**vars(args), "dense_exchange": True}),
+                                                       out["value"], c1).items()
+                    if k in ("samples_per_s", "ms_per_step", "ratio")}
             except Exception as e:  # the headline stands on its own
-                out["k4_server_loopback"] = {"error": repr(e)[:300]}
+                out.setdefault("k4_server_loopback", {})["error"] = repr(e)[:300]
         if not args.no_k5:
             try:
                 out["widened"] = run_wide(args, args.k5_batch, max(5, min(args.steps, 20)), 3,
