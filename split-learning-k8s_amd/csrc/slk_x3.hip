@@ -606,6 +606,44 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     }
     int k = 0, q = 0;
     (void)u;
+    // C1W epilogue of one pair: client ReLU backward + conv1 wgrad (the cut gradient g is the value the
+    // C1W = false store would write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels
+    // 16 t + 4 kc + r
+    auto c1w_epi = [&](int T0e, int T1e, float us1e, int qe) {
+        const int ci = 16 * nt + n16;
+        const float* xs = reinterpret_cast<const float*>(xbm[qe & 1]);
+        const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbm[qe & 1] + XB_X);
+        f32x4 d1 = d1s[tid];
+        // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff
+        // (every lane reads a valid pixel; cols 10-15 and the bias col 9 select their constant after)
+        const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
+        const float bsel = n16 == 9 ? 1.f : 0.f;
+        // a tile's reads first (unconditional, clamped), then its 4 MFMAs: no exec-masked block between
+        // each read and its MFMA (which exposed every ds_read's latency, all eight waves at once)
+#pragma unroll
+        for (int i = 0; i < X3D_MPW; ++i) {
+            const int t = T0e + g + 4 * i;
+            if (i < 3 || t < T1e) {  // wave-uniform (tiles 0-2 exist for every wave and part)
+                const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
+                const uint32_t mraw = bs[(ci >> 3) * (A_PIX / 4) + min(tq, A_PIX / 4 - 1)];
+                float xv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int p = min(16 * t + 4 * kc + r, A_PIX - 1);
+                    xv[r] = xs[p + 2 * (p / A_HW) + toff];
+                }
+                // (pixels past 675: no conv1 thread, mask 0, so A = 0 there)
+                const uint32_t mw = tq < A_PIX / 4 ? mraw >> (4 * (ci & 7)) : 0u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    // g * 2^sw: the weight scale's 2^-sw is applied once to the slab (exact either way)
+                    const float gm = ((mw >> r) & 1u) ? acc[i][r] * us1e : 0.f;
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, n16 < 9 ? xv[r] : bsel, d1, 0, 0, 0);
+                }
+            }
+        }
+        d1s[tid] = d1;
+    };
 #pragma unroll 1
     for (; pr < P; pr += G) {
         const int b = pr / 3, pt = pr - (pr / 3) * 3;
@@ -688,33 +726,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
         const float us1 = ldexpf(1.f, -x3_exp(amax_b)), us2 = ldexpf(1.f, -sw);
         if constexpr (C1W) {
-            // client ReLU backward + conv1 wgrad (the cut gradient g is the value the store below would
-            // write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels 16 t + 4 kc + r
-            const int ci = 16 * nt + n16;
-            const float* xs = reinterpret_cast<const float*>(xbm[q & 1]);
-            const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbm[q & 1] + XB_X);
-            f32x4 d1 = d1s[tid];
-            // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff
-            const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
-#pragma unroll
-            for (int i = 0; i < X3D_MPW; ++i) {
-                const int t = T0 + g + 4 * i;
-                if (t < T1) {  // wave-uniform
-                    const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
-                    // (pixels past 675: no conv1 thread, mask 0, so A = 0 there)
-                    const uint32_t mw = tq < A_PIX / 4 ? bs[(ci >> 3) * (A_PIX / 4) + tq] >> (4 * (ci & 7)) : 0u;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float gm = ((mw >> r) & 1u) ? x3_unscale(acc[i][r], us1, us2) : 0.f;
-                        const int p = min(16 * t + 4 * kc + r, A_PIX - 1);
-                        const int y = p / A_HW;
-                        const float xv = xs[p + 2 * y + toff];
-                        const float bv = n16 < 9 ? xv : (n16 == 9 ? 1.f : 0.f);
-                        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, bv, d1, 0, 0, 0);
-                    }
-                }
-            }
-            d1s[tid] = d1;
+            c1w_epi(T0, T1, us1, q);
         } else {
             float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
@@ -738,7 +750,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             const int src = ((cl >> 2) * 16 + j) * 4 + (cl & 3);
             float sum = 0.f;
             for (int gg = 0; gg < 4; ++gg) sum += part[(ntc + 2 * gg) * 256 + src];
-            c1slabs[(size_t)blockIdx.x * (C1 * 10) + (j < 9 ? ci * 9 + j : C1 * 9 + ci)] = sum;
+            c1slabs[(size_t)blockIdx.x * (C1 * 10) + (j < 9 ? ci * 9 + j : C1 * 9 + ci)] = sum * ldexpf(1.f, -sw);
         }
     }
 }

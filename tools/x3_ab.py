@@ -43,6 +43,7 @@ def main():
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     cases = {}
+    outs = {}  # case -> output tensor (compared across libraries after the timing)
     for li, path in enumerate(args.libs):
         L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_DEEPBIND)  # own symbols first
         for n in ("slk_conv2_fwd_pool_x3s", "slk_conv2_dgrad_x3", "slk_conv2_wgrad_x3s", "slk_conv2_wgrad_x3_nslab"):
@@ -77,10 +78,12 @@ def main():
             L.slk_conv2_fwd_pool_x3i.argtypes = [P] * 6 + [ctypes.c_int, P]
             cases[f"fwdi {tag}"] = (lambda L=L, po=po2, co=co2, a16=a16: L.slk_conv2_fwd_pool_x3i(
                 p(a16), p(amax), p(W2), p(b2), p(po), p(co), B, st))
+            outs[f"fwdi {tag}"] = po2
         if "dgrad" in args.ops:
             g = torch.empty_like(act)
             L.slk_conv2_dgrad_x3.argtypes = [P] * 5 + [ctypes.c_int, P]
             cases[f"dgrad {tag}"] = (lambda L=L, g=g: L.slk_conv2_dgrad_x3(p(dp), p(dpa), p(code), p(W2), p(g), B, st))
+            outs[f"dgrad {tag}"] = g
         if "dgc1" in args.ops:
             sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
             L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
@@ -88,6 +91,7 @@ def main():
             L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * (7 if abi2 else 8) + [ctypes.c_int, P]
             cases[f"dgc1 {tag}"] = (lambda L=L, sl=sl1, xa=dgc1_args(): L.slk_conv2_dgrad_x3_c1w(
                 p(dp), p(dpa), p(code), p(W2), *xa, p(sl), B, st))
+            outs[f"dgc1 {tag}"] = sl1
         if "fc" in args.ops.split(","):
             lg, li, dlg, dpo, dpam = (torch.empty(B, 10, device=dev), torch.empty(B, device=dev),
                                      torch.empty(B, 10, device=dev), torch.empty_like(dp), torch.empty(B, device=dev))
@@ -116,6 +120,16 @@ def main():
     for k, v in sorted(times.items()):
         v.sort()
         print(f"{k:24s} median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)
+    first = {}
+    for k, t in outs.items():  # each library's output vs the first library's (same op)
+        op = k.split()[0]
+        if op not in first:
+            first[op] = t
+            continue
+        r = first[op]
+        red = (lambda z: z.sum(0)) if op == "dgc1" else (lambda z: z)
+        a, b_ = red(t.double()), red(r.double())
+        print(f"check {k:18s} max|diff|/max|ref| {((a - b_).abs().max() / b_.abs().max()).item():.3e}", flush=True)
 
 
 if __name__ == "__main__":
