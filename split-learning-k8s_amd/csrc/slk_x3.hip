@@ -1117,7 +1117,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
 constexpr int C1X_T = 192;
 constexpr int C1X_G = A_PIX / 4;  // 169 active threads
 static_assert(RB_SAMPLE == 4 * C1X_G, "bit map layout");
-template <bool BITS>
+template <bool BITS, bool ACT>
 __global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
                                                              const float* __restrict__ b1, float* __restrict__ act,
                                                              float* __restrict__ act_amax, uint16_t* __restrict__ act16,
@@ -1142,32 +1142,31 @@ __global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __r
 #pragma unroll
         for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
     }
-    auto conv = [&](int c, float o[4]) {
-        const float* w = ws + c * 10;
-        float wk[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) wk[k] = w[k];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float sum = 0.f;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) sum = fmaf(xv[u][k], wk[k], sum);
-            sum += wk[9];
-            o[u] = sum > 0.f ? sum : 0.f;
-        }
-    };
     float am = 0.f;
     if (active) {
-        float4* out = act ? reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid : nullptr;
+        float4* out = ACT ? reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid : nullptr;
 #pragma unroll
         for (int cg = 0; cg < 4; ++cg) {
             uint32_t bw = 0;
-#pragma unroll 4
+#pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
                 const int c = 8 * cg + cc;
+                // the channel's weights are wave-uniform: scalar loads issued ahead, no LDS round trip
+                // (and no wait on one) per channel
+                float wk[10];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) wk[k] = W1[c * 9 + k];
+                wk[9] = b1[c];
                 float o[4];
-                conv(c, o);
-                if (act) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float sum = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) sum = fmaf(xv[u][k], wk[k], sum);
+                    sum += wk[9];
+                    o[u] = sum > 0.f ? sum : 0.f;
+                }
+                if constexpr (ACT) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
                 am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
                 if constexpr (BITS) {
 #pragma unroll
@@ -1260,12 +1259,15 @@ extern "C" int slk_conv1_fwd_x3(const float* x, const float* W1, const float* b1
                                 uint16_t* act16, uint32_t* relu_bits, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && (B == 0 || (x && W1 && b1 && act_amax && act16)));
     if (B == 0) return 0;
-    if (relu_bits)
-        hipLaunchKernelGGL(conv1_fwd_x3_kernel<true>, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act,
-                           act_amax, act16, relu_bits);
+    const dim3 g(B), t(C1X_T);
+    if (relu_bits && act)
+        hipLaunchKernelGGL((conv1_fwd_x3_kernel<true, true>), g, t, 0, slk_stream(stream), x, W1, b1, act, act_amax, act16, relu_bits);
+    else if (relu_bits)
+        hipLaunchKernelGGL((conv1_fwd_x3_kernel<true, false>), g, t, 0, slk_stream(stream), x, W1, b1, act, act_amax, act16, relu_bits);
+    else if (act)
+        hipLaunchKernelGGL((conv1_fwd_x3_kernel<false, true>), g, t, 0, slk_stream(stream), x, W1, b1, act, act_amax, act16, relu_bits);
     else
-        hipLaunchKernelGGL(conv1_fwd_x3_kernel<false>, dim3(B), dim3(C1X_T), 0, slk_stream(stream), x, W1, b1, act,
-                           act_amax, act16, relu_bits);
+        hipLaunchKernelGGL((conv1_fwd_x3_kernel<false, false>), g, t, 0, slk_stream(stream), x, W1, b1, act, act_amax, act16, relu_bits);
     return slk_launch_status();
 }
 extern "C" int64_t slk_relu_bits_bytes(int B) { return B > 0 ? (int64_t)B * RB_SAMPLE * 4 : 0; }
