@@ -365,9 +365,11 @@ class ServerStage:
 
     def step_request(self, act: Optional[torch.Tensor], labels: torch.Tensor, step: Optional[int] = None,
                      cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
-                     act16: Optional[torch.Tensor] = None, client_fuse=None):
+                     act16: Optional[torch.Tensor] = None, client_fuse=None, extra_segments=()):
         """One /forward_pass request (server_part.py:38-58): returns (cut_grad, loss_i). The mean
-        loss for `step` lands in the device loss log."""
+        loss for `step` lands in the device loss log. `extra_segments`: further (param, grad, slabs)
+        reduce+SGD segments at this stage's lr run in the same optimizer launch (the fused trainer's
+        client update, whose slabs the dgrad wrote)."""
         B = labels.shape[0]
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, 1.0 / B, cut_grad=cut_grad,
                                                          act_amax=act_amax, act16=act16, client_fuse=client_fuse)
@@ -377,13 +379,16 @@ class ServerStage:
             # after its wgrad: moving that wgrad ahead of the server's update measured +25-35 us.
             k = ops.CONV2_SLAB
             with TIMER("sgd_server"):
-                ops.sgd_multi_from_slabs([(self.params[:k], self.grads[:k], s2), (self.params[k:], self.grads[k:], s3)],
+                ops.sgd_multi_from_slabs([(self.params[:k], self.grads[:k], s2), (self.params[k:], self.grads[k:], s3),
+                                          *extra_segments],
                                          self.lr, loss=(loss_i, 1.0 / B, self.loss_log.ring, self.loss_log.counter))
             if step is not None:
                 self.loss_log.note_step(step)
         else:
             self.apply_grad_slabs(s2, s3)
             self.log_loss(loss_i, step=step)
+            for prm, grd, sl in extra_segments:
+                ops.sgd_from_slabs(prm, grd, sl, self.lr)
         return cut_grad, loss_i
 
     def check_labels(self):
@@ -427,9 +432,14 @@ class SplitTrainer:
             c = self.client
             slabs = c._buf.get("c1w_slabs", (ops.conv2_dgrad_c1w_nslab(x.shape[0]), ops.CLIENT_NPARAM),
                                torch.float32, self.device)
+            # the client's update joins the server's optimizer launch (its slabs are complete once the
+            # dgrad has run; bit-identical to step_from_slabs) when both stages step at one lr
+            one = c.lr == self.server.lr
             self.server.step_request(act, y, act_amax=c._act_amax, act16=a16,
-                                     client_fuse=(x, c._relu_bits, slabs))
-            c.step_from_slabs(slabs)
+                                     client_fuse=(x, c._relu_bits, slabs),
+                                     extra_segments=[(c.params, c.grads, slabs)] if one else ())
+            if not one:
+                c.step_from_slabs(slabs)
             return
         cut_grad, _ = self.server.step_request(act, y, act_amax=self.client._act_amax, act16=a16)
         self.client.backward_step(cut_grad)
