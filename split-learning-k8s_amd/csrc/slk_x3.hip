@@ -185,7 +185,11 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 
     const int U = 3 * B;
     const int G = gridDim.x;
-    int u = blockIdx.x;
+    // a contiguous range of units per workgroup: the three thirds of a sample run back to back on one
+    // CU, so the 2 halo rows each shares with the next come from that XCD's L2, not HBM
+    const int per = (U + G - 1) / G;
+    const int u0 = min((int)blockIdx.x * per, U), u1 = min(u0 + per, U);
+    int u = u0;
     // DMA source offsets (bytes within a unit): piece g = 64k' + lane -> channel g / 65, 16-B run g % 65
     uint32_t voff[X3F_WPIECES];
 #pragma unroll
@@ -197,11 +201,11 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     // IN16: unit uu's image -> ring slot
     auto issue_img = [&](int uu, char* dstp) { x3_issue_unit_img(act16, uu, wave, lane, lds_u32(dstp)); };
     if constexpr (IN16) {
-        if (u < U) issue_img(u, smem);
-        if (u + G < U) issue_img(u + G, smem + X3F_BUF);
+        if (u < u1) issue_img(u, smem);
+        if (u + 1 < u1) issue_img(u + 1, smem + X3F_BUF);
     } else {
-        if (u < U) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
-        if (u + G < U) x3f_issue_raw(act, u + G, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
+        if (u < u1) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
+        if (u + 1 < u1) x3f_issue_raw(act, u + 1, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
     }
 
     // weight scale: max |W2| over the whole tensor
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     // prologue: unit u's raw rows landed -> split into f16 buffer 0 (IN16: its image is there)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!IN16 && u < U) split_unit(u, raw0, smem);
+    if (!IN16 && u < u1) split_unit(u, raw0, smem);
     int k = 0;
     const int sph = wave >= 4 ? 0 : 1;
     // Epilogue of one (M tile, co tile) window group: the first max of the raw accumulators (the unscale
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         code[o] = (uint8_t)(m > 0.f ? idx : CODE_NONE);
     };
 #pragma unroll 1
-    for (; u < U; u += G, ++k) {
+    for (; u < u1; ++u, ++k) {
         const int cb = k & 1;
         // unit u+G's raw rows (issued one unit ago) have landed; the previous epilogue's stores may stay
         // IN16: unit u's image (issued two units ago) has landed; unit u+G's DMA (at most 5 wave-
@@ -307,9 +311,9 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         __syncthreads();
         const int kr = k % 3;  // IN16 ring slot of unit u
         if constexpr (IN16) {
-            if (u + 2 * G < U) issue_img(u + 2 * G, smem + (kr == 0 ? 2 : kr - 1) * X3F_BUF);
+            if (u + 2 < u1) issue_img(u + 2, smem + (kr == 0 ? 2 : kr - 1) * X3F_BUF);
         } else {
-            if (u + 2 * G < U) x3f_issue_raw(act, u + 2 * G, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
+            if (u + 2 < u1) x3f_issue_raw(act, u + 2, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
         }
         const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
         f32x4 acc[3][X3F_NT];
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             // staging after M tile 0 on waves 4-7 and after M tile 1 on waves 0-3 (waves w and w + 4
             // share a SIMD; measured: 0/1 beats 0/0 and 0/2). Past the last unit this splits a clamped
             // unit's stale raw rows into a buffer nobody reads
-            if (!IN16 && mt == sph) split_unit(min(u + G, U - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
+            if (!IN16 && mt == sph) split_unit(min(u + 1, u1 - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
             if (!IN16 && mt == sph && act16) {
                 // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
                 // (rows 8-9 of a third are rows 0-1 of the next: both units store the same values there)
@@ -576,11 +580,15 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 
     f32x4 acc[X3D_MPW];
     int u = blockIdx.x;
-    // units of a workgroup: u, u + G, ... — the two co halves of a part must be consecutive for the
-    // accumulators, so a workgroup walks PAIRS: unit index = 2 * (pair) + h with pairs strided by G
-    // (pair = (sample, part))
+    // a workgroup walks PAIRS (pair = (sample, part); unit index = 2 * pair + h: the two co halves of a
+    // part are consecutive for the accumulators) over a CONTIGUOUS range, so the three parts of a sample
+    // run back to back on one CU: the dpooled window rows that neighbouring parts share (19 rows read
+    // per 12) and the sample's x / bit map come from that XCD's L2 the second time (a stride of G put
+    // them on different XCDs: HBM re-reads)
     const int P = 3 * B;  // pairs
-    int pr = blockIdx.x;
+    const int per = (P + G - 1) / G;
+    const int p0 = min((int)blockIdx.x * per, P), p1 = min(p0 + per, P);
+    int pr = p0;
     // pair pp's x and bits -> xbm[buf]: waves 0-3 move x (3 x 1 KiB + 64 B), waves 4-6 the bits (2 x
     // 1 KiB + 656 B), one 16-B piece per lane (retired by the s_waitcnt before the barrier that opens the next pair)
     auto issue_xb = [&](int pp, int buf) {
@@ -596,9 +604,9 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     };
     if constexpr (C1W) {
         d1s[tid] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pr < P) issue_xb(pr, 0);
+        if (pr < p1) issue_xb(pr, 0);
     }
-    if (pr < P) {
+    if (pr < p1) {
         load_dy(2 * pr);
         __syncthreads();  // zeroing / red restore done before the first expansion
         store_dy(2 * pr, smem);
@@ -645,7 +653,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         d1s[tid] = d1;
     };
 #pragma unroll 1
-    for (; pr < P; pr += G) {
+    for (; pr < p1; ++pr) {
         const int b = pr / 3, pt = pr - (pr / 3) * 3;
         const int T0 = x3d_t0(pt), T1 = pt == 2 ? X3D_MT : x3d_t0(pt + 1);
         const float amax_b = amax[b];  // for the epilogue, loaded early
@@ -658,11 +666,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             if (C1W && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
             // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue)
-            if (C1W && h == 0) issue_xb(min(pr + G, P - 1), (q + 1) & 1);
+            if (C1W && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
-            const int unx = min(h ? 2 * (pr + G) : 2 * pr + 1, U - 1);   // the unit after this one
-            const int unx2 = min(h ? 2 * (pr + G) + 1 : 2 * (pr + G), U - 1);  // and the one after that
+            const int unx = min(h ? 2 * (pr + 1) : 2 * pr + 1, 2 * p1 - 1);   // the unit after this one
+            const int unx2 = min(h ? 2 * (pr + 1) + 1 : 2 * (pr + 1), 2 * p1 - 1);  // and the one after that
             // A fragments of (tile i, tap) through a 4-slot ring, read 3 steps ahead of their MFMAs (one
             // read pair per 3 dependent MFMAs: waiting on each read left the SIMD half idle)
             const char* abw = img + cbase + ((T0 + g) * 16 + n16) * X3D_REC + kc * 16;
@@ -766,7 +774,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 // on adjacent rows, see abase below), so the input pixel of tap (ky, kx) is a per-(K-step, lane) base +
 // an immediate. dY pixel rows keep the two 32-B co tiles swapped on odd 8-pixel groups (the two 16-lane
 // groups of a half-wave then hit disjoint banks).
-// A workgroup owns one co half (M = 32) and a K share (units ks, ks + nks, ...); the two co halves
+// A workgroup owns one co half (M = 32) and a K share (a contiguous range of units); the two co halves
 // of a share run on different workgroups, each splitting the same input rows. A K sum spans samples,
 // so every product must carry ONE scale: the input keeps its sample's 2^s_b (the act16 images' scale)
 // and the sample's dY takes 2^(sd + sx - s_b) (sx, sd: the launch scales from the maxima of the
@@ -1002,8 +1010,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         }
     };
 
-    int u = ks;
-    if (u < U) {
+    // a contiguous range of units per K share: the three thirds of a sample run back to back, so the
+    // 2 halo rows each shares with the next come from L2 (both co-half workgroups of the share sit on
+    // one XCD and read the same images)
+    const int per = (U + nks - 1) / nks;
+    const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
+    int u = u0;
+    if (u < u1) {
         if constexpr (X16) {
             issue_x16(u, smem);
         } else {
@@ -1012,12 +1025,12 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         load_dy(u);
         if constexpr (!X16) split_x(smem);
         store_dy(smem, true);
-        if constexpr (!X16) load_x(min(u + nks, U - 1));
-        load_dy(min(u + nks, U - 1));
+        if constexpr (!X16) load_x(min(u + 1, u1 - 1));
+        load_dy(min(u + 1, u1 - 1));
     }
     int k = 0;
 #pragma unroll 1
-    for (; u < U; u += nks, ++k) {
+    for (; u < u1; ++u, ++k) {
         // X16: this unit's image DMA landed; the 8 dY loads of load_dy, every wave's last memory
         // instructions (issued after its DMA), may stay in flight
         const bool dfirst = !X16 || tg == 1;
@@ -1029,7 +1042,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
-        const int nx = u + nks, nx2 = u + 2 * nks;
+        const int nx = u + 1, nx2 = u + 2;
         const char* img = smem + (k & 1) * X3W_BUF;
         char* nimg = smem + ((k & 1) ^ 1) * X3W_BUF;
         // unit u+1's rows and dY were requested a whole unit ago. No branch around the staging (past the
@@ -1039,21 +1052,21 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // waves after theirs, so the two waves of a SIMD overlap routing with MFMAs. store_dy goes before
         // the DMA issue: the compiler does not count the asm DMAs, so its wait for the dY registers
         // would otherwise also wait for the DMA just issued
-        if (dfirst && dstage) store_dy(nimg, nx < U);
+        if (dfirst && dstage) store_dy(nimg, nx < u1);
         if constexpr (X16) {
-            issue_x16(min(nx, U - 1), nimg);
+            issue_x16(min(nx, u1 - 1), nimg);
         } else {
             split_x(nimg);
         }
         if (dfirst && dstage) {
-            if constexpr (!X16) load_x(min(nx2, U - 1));
-            load_dy(min(nx2, U - 1));
+            if constexpr (!X16) load_x(min(nx2, u1 - 1));
+            load_dy(min(nx2, u1 - 1));
         }
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
         if (!dfirst && dstage) {
-            store_dy(nimg, nx < U);
-            load_dy(min(nx2, U - 1));
+            store_dy(nimg, nx < u1);
+            load_dy(min(nx2, u1 - 1));
         }
     }
     __syncthreads();
