@@ -23,6 +23,10 @@ using namespace slk;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef SLK_X3W_SPREAD
+#define SLK_X3W_SPREAD 0
+#endif
+
 namespace {
 
 // s such that amax * 2^s < 2^14 (amax in [2^13, 2^14) after scaling); 0 for zero / non-finite amax.
@@ -148,6 +152,20 @@ __device__ __forceinline__ void x3_issue_unit_img(const uint16_t* act16, int uu,
             if (pp < PP - 1 || lane < 16) glds16_so(src, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3F_PLANE + pp * 1024);
         }
     }
+}
+
+// the same image as separate pieces for issue inside the MFMA stream: full piece r (0-3) of wave w is
+// piece w + 8r of the 32 full 1-KiB pieces (plane = piece >> 4); the two 256-B quarters go to waves 0-1
+__device__ __forceinline__ const char* x3_unit_img_src(const uint16_t* act16, int uu) {
+    const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+    return reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t3 * X3S_UNIT_OFF;
+}
+__device__ __forceinline__ void x3_issue_img_full(const char* srch, int wave, int lane, uint32_t lds, int r) {
+    const int piece = wave + 8 * r, pl = piece >> 4, pp = piece & 15;
+    glds16_so(srch + pl * X3S_PLANE, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3F_PLANE + pp * 1024);
+}
+__device__ __forceinline__ void x3_issue_img_quarter(const char* srch, int wave, int lane, uint32_t lds) {
+    if (lane < 16) glds16_so(srch + wave * X3S_PLANE, (uint32_t)(16 * 1024 + lane * 16), lds + wave * X3F_PLANE + 16 * 1024);
 }
 
 __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave, int lane, const uint32_t* voff,
@@ -310,9 +328,13 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES) : "memory");
         __syncthreads();
         const int kr = k % 3;  // IN16 ring slot of unit u
-        if constexpr (IN16) {
-            if (u + 2 < u1) issue_img(u + 2, smem + (kr == 0 ? 2 : kr - 1) * X3F_BUF);
-        } else {
+        // IN16: unit u+2's image (past the range: a clamped unit into the free slot, never read) — the
+        // quarters now, the 4 full pieces of each wave spread over the first MFMA steps (one burst here
+        // measured 0.2456 vs 0.2336 ms, interleaved A/B)
+        const char* nsrc = x3_unit_img_src(act16, min(u + 2, u1 - 1));
+        const uint32_t nlds = lds_u32(smem + (kr == 0 ? 2 : kr - 1) * X3F_BUF);
+        if (IN16 && wave < 2) x3_issue_img_quarter(nsrc, wave, lane, nlds);
+        if constexpr (!IN16) {
             if (u + 2 < u1) x3f_issue_raw(act, u + 2, wave, lane, voff, lds_u32(raw0 + cb * X3F_RAW));
         }
         const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
@@ -344,6 +366,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             }
 #pragma unroll
             for (int st = 0; st < 27; ++st) {
+                if (st < 8 && (st & 1) == 0) x3_issue_img_full(nsrc, wave, lane, nlds, st >> 1);
                 if (st + 2 < 27) rdA(st + 2);
                 const int mt = st / 9, tap = st % 9;
 #pragma unroll
@@ -406,6 +429,7 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 #pragma unroll
         for (int nt = 0; nt < X3F_NT; ++nt) epi_piece(pend[nt], p_pre, p_us, bias[nt], p_o + nt * 16 * P_WIN);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 
 // ============================================================================ conv2 dgrad (cut gradient)
@@ -968,6 +992,9 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     // a unit's work for this wave: K-steps kp, kp + 2, kp + 4 x its taps; B fragments (4 transposed reads)
     // run 2 steps ahead through a 3-slot ring, A fragments (8 reads) one K-step ahead; the
     // sched_group_barriers keep that order (hipcc otherwise sinks every read next to its MFMAs)
+    // (SLK_X3W_SPREAD: the next unit's 4 full image pieces of this wave go out between the first MFMA steps)
+    const char* dsrc = nullptr;
+    uint32_t dlds = 0;
     auto unit_mfma = [&](const char* img, auto TG) {
         constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
         constexpr int N = 3 * NT;
@@ -990,6 +1017,9 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         rdB(1, 1);
 #pragma unroll
         for (int n = 0; n < N; ++n) {
+#if SLK_X3W_SPREAD
+            if (X16 && n < 8 && (n & 1) == 0) x3_issue_img_full(dsrc, wave, lane, dlds, n >> 1);
+#endif
             if (n + 2 < N) {
                 rdB(n + 2, (n + 2) % 3);
                 if ((n + 2) % NT == 0) rdA((n + 2) / NT, ((n + 2) / NT) & 1);
@@ -1038,7 +1068,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // redo of item 383); their last memory instructions are then the DMA itself
         const bool dstage = !(X16 && wave >= X3W_DYITEMS / 64);
         if constexpr (X16) {
-            if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!dstage || (SLK_X3W_SPREAD && dfirst)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         }
         __syncthreads();  // image k&1 complete; image (k+1)&1 free
@@ -1054,7 +1084,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         // would otherwise also wait for the DMA just issued
         if (dfirst && dstage) store_dy(nimg, nx < u1);
         if constexpr (X16) {
+#if SLK_X3W_SPREAD
+            dsrc = x3_unit_img_src(act16, min(nx, u1 - 1));
+            dlds = lds_u32(nimg + 2 * X3W_DYP);
+            if (wave < 2) x3_issue_img_quarter(dsrc, wave, lane, dlds);
+#else
             issue_x16(min(nx, u1 - 1), nimg);
+#endif
         } else {
             split_x(nimg);
         }
@@ -1069,6 +1105,9 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
             load_dy(min(nx2, u1 - 1));
         }
     }
+#if SLK_X3W_SPREAD
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA into the image buffers reused below
+#endif
     __syncthreads();
     // K parities: kp = 1 waves hand their sums to kp = 0 through LDS (region per (h, tg))
     constexpr int XN = 2 * 5 * 4;  // floats per lane
