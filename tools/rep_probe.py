@@ -28,7 +28,7 @@ rep = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev))
 a2, b2 = init_models(seed=0)
 tr = SplitTrainer(a2, b2, device=dev, graph=True)
 res = {}
-for name, fn in (("replicated_eager", lambda i: rep.step(X[i % 4], Y[i % 4])),
+for name, fn in (("replicated_graph", lambda i: rep.step(X[i % 4], Y[i % 4])),
                  ("trainer_graph", lambda i: tr.step(X[i % 4], Y[i % 4]))) * 2:
     for i in range(5):
         fn(i)
