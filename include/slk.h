@@ -53,7 +53,7 @@ extern "C" {
 
 int slk_abi_version(void);
 const char* slk_error_string(int err);
-/* Hex sha256 of the sources this library was compiled from (csrc/*.hip, csrc/*.h, include/slk.h);
+/* Hex sha256 of the sources this library was compiled from (the csrc .hip and .h files, include/slk.h);
  * splitcnn/_lib.py refuses a library whose id differs from the tree's. */
 const char* slk_build_id(void);
 

@@ -495,7 +495,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const int nt = wave & 1, g = wave >> 1;
     const int n16 = lane & 15, kc = lane >> 4;
     const int G = gridDim.x;
-    const int U = 6 * B;
 
     // zero both images once: the leading pixels and columns 24-25 are never written again
     for (int o = tid * 16; o < 2 * X3D_IMG; o += X3D_THREADS * 16) *reinterpret_cast<uint4*>(smem + o) = make_uint4(0, 0, 0, 0);
@@ -599,7 +598,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     };
 
     f32x4 acc[X3D_MPW];
-    int u = blockIdx.x;
     // a workgroup walks PAIRS (pair = (sample, part); unit index = 2 * pair + h: the two co halves of a
     // part are consecutive for the accumulators) over a CONTIGUOUS range, so the three parts of a sample
     // run back to back on one CU: the dpooled window rows that neighbouring parts share (19 rows read
@@ -633,7 +631,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         load_dy(2 * pr + 1);
     }
     int k = 0, q = 0;
-    (void)u;
     // C1W epilogue of one pair: client ReLU backward + conv1 wgrad (the cut gradient g is the value the
     // C1W = false store would write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels
     // 16 t + 4 kc + r
