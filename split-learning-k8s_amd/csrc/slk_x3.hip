@@ -336,20 +336,22 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         const char* cur = smem + (IN16 ? kr : cb) * X3F_BUF;
         f32x4 acc[3][X3F_NT];
         if constexpr (IN16) {
-            // no staging in the loop: all 27 (M tile, tap) steps in one stream, A fragments read through
-            // a 3-slot ring two steps ahead
+            // no staging in the loop: all 27 (M tile, tap) steps in one stream
 #pragma unroll
             for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < X3F_NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            f16x8 fh[3], fl[3];
+            // A fragments read RA steps ahead through a ring of RA + 1 (interleaved A/B: RA = 1 0.2287 ms,
+            // 2 0.2333, 3 0.2339 — the epilogue pieces and DMA pieces now fill the gaps the deeper ring hid)
+            constexpr int RA = 1;
+            f16x8 fh[RA + 1], fl[RA + 1];
             auto rdA = [&](int st) {
                 const int mt = st / 9, tap = st % 9, ky = tap / 3, kx = tap % 3;
-                fh[st % 3] = *reinterpret_cast<const f16x8*>(cur + abase[mt][kx] + ky * A_HW * 64);
-                fl[st % 3] = *reinterpret_cast<const f16x8*>(cur + X3F_PLANE + abase[mt][kx] + ky * A_HW * 64);
+                fh[st % (RA + 1)] = *reinterpret_cast<const f16x8*>(cur + abase[mt][kx] + ky * A_HW * 64);
+                fl[st % (RA + 1)] = *reinterpret_cast<const f16x8*>(cur + X3F_PLANE + abase[mt][kx] + ky * A_HW * 64);
             };
-            rdA(0);
-            rdA(1);
+#pragma unroll
+            for (int q = 0; q < RA; ++q) rdA(q);
             // this unit's scales and output offsets (for the pieces of its epilogue issued in-stream)
             const int b_ = u / 3, t3_ = u - (u / 3) * 3, se_ = sexp(b_) + sw;
             const float pre_ = ldexpf(1.f, min(126 - se_, 0)), us_ = ldexpf(1.f, -min(se_, 126));
@@ -363,11 +365,11 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 #pragma unroll
             for (int st = 0; st < 27; ++st) {
                 if (st < 8 && (st & 1) == 0) x3_issue_img_full(nsrc, wave, lane, nlds, st >> 1);
-                if (st + 2 < 27) rdA(st + 2);
+                if (st + RA < 27) rdA(st + RA);
                 const int mt = st / 9, tap = st % 9;
 #pragma unroll
                 for (int nt = 0; nt < X3F_NT; ++nt)
-                    acc[mt][nt] = mfma_x3(fh[st % 3], fl[st % 3], wh[nt][tap], wl[nt][tap], acc[mt][nt]);
+                    acc[mt][nt] = mfma_x3(fh[st % (RA + 1)], fl[st % (RA + 1)], wh[nt][tap], wl[nt][tap], acc[mt][nt]);
                 if (tap == 3 || tap == 6) {
                     const int nt = tap == 3 ? 0 : 1;
                     if (mt == 0) epi_piece(pend[nt], p_pre, p_us, bias[nt], p_o + nt * 16 * P_WIN);
