@@ -8,14 +8,14 @@ fp32, the whole step (client fwd -> cut hand-off -> server fwd/CE/bwd/SGD -> cli
 replayed as one HIP graph. Inputs are resident in HBM before the timed region (a pool of batches,
 copied into the graph's static input buffers inside each step).
 
-N > 1: `value` is --topology replicated (default: data-parallel SplitFed-V1 replicas, each rank one
-client + one server replica, one 444 KB gradient all-reduce per step, weak scaling — NOT one of
-BASELINE.json's configs, and labelled so). The BASELINE topologies follow as labelled objects:
-"k3_pipeline" (N = 2: client GPU <-> server GPU, micro-batched RCCL send/recv), "k4_hub" (N >= 3:
-N-1 client GPUs -> 1 server GPU on the reference cut) and "k5_splitfed" (the widened model's
-client-heavy cut on the same hub topology), each with its cut-exchange GB/s per link and direction
-against a measured RCCL p2p peak ("p2p_peak_GBps_measured") and the vendor link figure.
---topology pipeline / hub makes that topology the headline instead.
+N > 1: `value` is BASELINE's topology for that N: N = 2 -> config 3 ("K3", client GPU <-> server GPU,
+micro-batched RCCL send/recv); N >= 3 -> config 4 ("K4", SplitFed: N-1 client GPUs feeding one server
+GPU on the reference cut, client-gradient all-reduce). The RCCL p2p rate is measured first, the cut
+exchange (dense fp32 or the lossless sparse codec) predicted from it and decided by a short trial of
+both; "exchange" reports the choice and the cut-exchange GB/s per link and direction against the
+measured p2p peak and the vendor link figure. Side objects: "replicated_dp" (data-parallel SplitFed-V1
+replicas of the fused K2 step — NOT a BASELINE config) and "k5_splitfed" (config 5's widened model on
+the hub topology). --topology replicated makes the replicas the headline instead.
 
 One JSON line on rank 0 with the driver's contract plus "roofline" (dominant kernel, measured live
 with HIP events on the launch stream in an eager pass after the timed region) and "cpu_baseline"
@@ -59,14 +59,16 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU (per-client) batch")
     ap.add_argument("--topology", default="auto", choices=["auto", "replicated", "pipeline", "hub"])
     ap.add_argument("--micro", type=int, default=4, help="micro-batches of the pipeline / hub topologies")
-    ap.add_argument("--dense-exchange", action="store_true",
-                    help="pipeline / hub: ship the dense cut + gradient instead of the lossless sparse codec")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "dense", "codec"],
+                    help="pipeline / hub cut exchange: auto = measure the link, then the faster of a short trial "
+                         "of each; dense = fp32 cut + gradient; codec = the lossless sparse codec")
+    ap.add_argument("--dense-exchange", action="store_true", help="= --exchange dense")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-pass", action="store_true")
     ap.add_argument("--no-exchange-phase", action="store_true")
-    ap.add_argument("--exchange-steps", type=int, default=10)
+    ap.add_argument("--exchange-steps", type=int, default=10, help="steps of the N > 1 side objects")
     ap.add_argument("--config", default="k2", choices=["k2", "k5"],
                     help="k2 = reference split CNN fp32 (headline); k5 = widened bf16 split CNN")
     ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
@@ -97,16 +99,18 @@ def cpu_baseline(seconds: float):
     except Exception:
         model = "?"
     aff = d.get("affinity_cpus") or d.get("nproc")
+    st, ct = d.get("server_threads"), d.get("client_threads")
     return {"value": round(d["value"], 1), "unit": "samples/s",
-            # cores = the CPUs this job may run on (its affinity mask: what torch's threads share);
-            # the machine's nproc is larger and not available to it
-            "cores": aff,
+            # cores = the torch threads that actually compute: the client blocks on the server's reply and
+            # the server on the client's request, so the two processes alternate and at most max(server,
+            # client) threads run at once (torch's default thread count, i.e. OMP_NUM_THREADS where set)
+            "cores": max(t for t in (st, ct) if t) if (st or ct) else aff,
             "kind": "port",
             "sample": f"{d['steps']} steps x B=64 in {d['seconds']:.1f}s: torch-CPU client+server processes "
                       f"over FastAPI/uvicorn + requests + pickle on localhost (src/client_part.py:103-138 <-> "
-                      f"src/server_part.py:25-58, MLflow omitted), both processes on the job's {aff} CPUs "
-                      f"(affinity mask) with torch threads server={d.get('server_threads')} "
-                      f"client={d.get('client_threads')}; machine nproc={d.get('nproc')} ({model})"}
+                      f"src/server_part.py:25-58, MLflow omitted) at torch's default thread count: server={st} "
+                      f"client={ct} threads (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
+                      f"which alternate; affinity mask {aff} CPUs, machine nproc={d.get('nproc')} ({model})"}
 
 
 def make_pool(B, n, device, seed=42):
@@ -179,23 +183,29 @@ ROCPROF_SYMBOL = {("conv2_dgrad", "x3_fused"): "conv2_dgrad_x3_kernel<true>",
 
 
 def rocprof_avg(symbol, pattern="kernel_stats_k2.csv"):
-    """Average duration (ms) of `symbol` in the newest committed rocprofv3 --stats summary under
-    profiles/ (the same bench command under the profiler), or None."""
+    """Average duration (ms) of `symbol` in the committed rocprofv3 --stats summary of the same bench
+    command, profiles/rocprof_<pattern>, with the slk_build_id of the library it profiled (the
+    `.build_id` file written next to it by tools/gpu_profile_all.sh). Returns (ms, source, build id,
+    whether that id is the loaded library's) or Nones."""
     import csv
-    import glob
-    # profiles/rocprof_<pattern> is the copy of the newest summary that travels to the GPU box (the
-    # per-round files under profiles/ are gpurun-ignored)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*" + pattern)), key=os.path.getmtime)
-    files = [f for f in files if os.path.basename(f).startswith("r03")] or files
-    files = [os.path.join(ROOT, "profiles", "rocprof_" + pattern)] + files[::-1]
-    for f in files:
-        try:
-            for row in csv.DictReader(open(f)):
-                if symbol in row["Name"]:
-                    return round(float(row["AverageNs"]) / 1e6, 4), os.path.relpath(f, ROOT)
-        except (OSError, KeyError, ValueError):
-            continue
-    return None, None
+    f = os.path.join(ROOT, "profiles", "rocprof_" + pattern)
+    try:
+        bid = open(os.path.splitext(f)[0] + ".build_id").read().strip()
+    except OSError:
+        bid = None
+    try:
+        from splitcnn import _lib
+        current = _lib.build_id()
+    except Exception:  # noqa: BLE001
+        current = None
+    try:
+        for row in csv.DictReader(open(f)):
+            if symbol in row["Name"]:
+                return (round(float(row["AverageNs"]) / 1e6, 4), os.path.relpath(f, ROOT), bid,
+                        bid is not None and bid == current)
+    except (OSError, KeyError, ValueError):
+        pass
+    return None, None, None, False
 
 
 def conv_roofline(name, avg_ms, B, impl):
@@ -232,9 +242,11 @@ def roofline_from(kern, B, impls=None, variants=None):
         r["traffic_ratio"] = round(r["traffic"] / algo, 3) if r.get("traffic") else None
         sym = ROCPROF_SYMBOL.get((name, variant))
         if sym:
-            ms, src = rocprof_avg(sym)
-            r["rocprof_avg_ms"] = ms
+            ms, src, bid, same = rocprof_avg(sym)
+            # only a profile of THIS library build counts as the cross-check; an older one is labelled
+            r["rocprof_avg_ms" if same else "rocprof_avg_ms_historical"] = ms
             r["rocprof_source"] = src
+            r["rocprof_build_id"] = bid[:16] if bid else None
             r["hip_event_avg_ms"] = r["avg_ms"]
     r["per_kernel"] = {k: {kk: conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino"))[kk]
                            for kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops")}
@@ -409,14 +421,34 @@ def run_wide(args, B, steps, warmup, kernel_pass_on=True):
 
 
 XGMI_LINK_GBPS = 153.6   # vendor per-link xGMI figure (task brief: 7 links x ~153 GB/s per GPU); convention unstated
+# Server-side rates of the hub step on one GPU (bench k4_server_loopback; samples/s at B = 4096 per
+# client): with the dense exchange the server runs the plain stage kernels, with the codec it also unpacks
+# and packs. Used only for the exchange PREDICTION reported next to the measured trial that decides.
+HUB_SERVER_RATE = {"dense": 4.4e6, "codec": 3.4e6}
+CODEC_WIRE_FRACTION = 0.456   # wire bytes / dense bytes of the codec on the synthetic data
+
+
+def predict_exchange(nc, B, p2p_gbps):
+    """Predicted step time of the hub per exchange: max(server compute of nc*B samples, one client link's
+    cut bytes in one direction at the measured p2p rate) — the micro-batches overlap the two. Dense wins
+    once the link sustains about 354 MB / (7 x 4096 / 4.4 M/s) = 55 GB/s per direction at nc = 7."""
+    out = {}
+    for ex, frac in (("dense", 1.0), ("codec", CODEC_WIRE_FRACTION)):
+        server = nc * B / HUB_SERVER_RATE[ex]
+        link = frac * B * CUT_BYTES / (p2p_gbps * 1e9) if p2p_gbps else float("inf")
+        out[ex] = round(max(server, link) * 1e3, 3)
+    return out
 
 
 def run_distributed(args, out, rank, world, local):
-    """N > 1. Headline `value`: data-parallel SplitFed-V1 replicas of the K2 step (linear weak scaling
-    by construction; NOT one of BASELINE.json's configs — labelled so). Then the BASELINE topologies,
-    each as its own labelled object: K3 = Pipeline (N = 2), K4 = Hub (N >= 3: N-1 client GPUs -> 1
-    server GPU), K5-SplitFed = WideHub (the widened, client-heavy cut), with cut-exchange GB/s per
-    direction against a measured RCCL p2p peak and the vendor link figure."""
+    """N > 1, BASELINE's own topologies. Headline `value`: N = 2 -> K3 (client GPU <-> server GPU,
+    micro-batched RCCL send/recv, dist.Pipeline); N >= 3 -> K4 (SplitFed: N-1 client GPUs feeding 1
+    server GPU, client all-reduce, dist.Hub). Before timing: the RCCL p2p rate client 0 -> server is
+    measured, the exchange (dense fp32 or the lossless sparse codec) is predicted from it, and a short
+    trial of both on the real topology decides. Side objects: "replicated_dp" (data-parallel
+    SplitFed-V1 replicas of the fused K2 step — NOT a BASELINE config) and "k5_splitfed" (config 5's
+    widened model on the hub topology), with cut-exchange GB/s against the measured p2p peak and the
+    vendor link figure."""
     import torch
     import torch.distributed as dist
 
@@ -426,13 +458,13 @@ def run_distributed(args, out, rank, world, local):
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     B = args.batch
-    topo = args.topology if args.topology != "auto" else "replicated"
+    topo = args.topology if args.topology != "auto" else ("pipeline" if world == 2 else "hub")
     X, Y = make_pool(B, 4, dev, seed=42 + rank)
     grp = sd.client_group_for(world)   # every rank creates it (collective), used by hub topologies
+    groups = sd.exchange_groups()      # one process group per exchange direction (see its docstring)
+    nc = world - 1
 
-    codec = not args.dense_exchange
-
-    def build(topology, micro):
+    def build(topology, micro, codec):
         a, b = init_models(seed=0)
         if topology == "replicated":
             t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev), graph=not args.no_graph)
@@ -440,28 +472,32 @@ def run_distributed(args, out, rank, world, local):
         if topology == "pipeline":
             assert world == 2
             if rank == 0:
-                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=codec)
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=codec, groups=groups,
+                                graph=not args.no_graph)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
-            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec)
+            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec, groups=groups,
+                            graph=not args.no_graph)
             return (lambda i: t.server_step(B, dev)), t, B
         if topology == "hub":
             if rank < world - 1:
-                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=codec)
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
+                           groups=groups, graph=not args.no_graph)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
-            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec)
+            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
+                       groups=groups, graph=not args.no_graph)
             return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
         raise ValueError(topology)
 
     labels = {
-        "replicated": "data-parallel SplitFed-V1 replicas (not a BASELINE config): every GPU hosts one client + "
+        "replicated": "data-parallel SplitFed-V1 replicas (NOT a BASELINE config): every GPU hosts one client + "
                       "one server replica of the reference split CNN, cut in place, one 444 KB gradient "
                       "all-reduce per step (= the reference step at the concatenated N*B batch)",
         "pipeline": "K3: 2xMI355X client-stage GPU <-> server-stage GPU, micro-batched RCCL send/recv of "
-                    "activations and cut gradients",
-        "hub": "K4: SplitFed, N-1 client GPUs feeding 1 server GPU (reference cut), micro-batched RCCL "
-               "send/recv, client-gradient all-reduce"}
-    cut_codec = ("lossless sparse codec: ReLU-cut bit mask + nonzero values out, gradient at those positions back "
-                 "(bit-identical results)" if codec else "dense fp32")
+                    "activations and cut gradients (BASELINE config 3)",
+        "hub": f"K4: SplitFed, {nc} client GPU(s) feeding 1 server GPU (reference cut), micro-batched RCCL "
+               "send/recv, client-gradient all-reduce (BASELINE config 4)"}
+    codec_label = {True: "lossless sparse codec: ReLU-cut bit mask + nonzero values out, gradient at those positions "
+                         "back (bit-identical results)", False: "dense fp32"}
 
     def wire(t):
         """rank 0 is a client in both exchange topologies: its link's bytes (both directions, labels and
@@ -470,61 +506,94 @@ def run_distributed(args, out, rank, world, local):
                          dtype=torch.float64, device=dev)
         dist.broadcast(v, 0)
         return int(v[0].item()), int(v[1].item())
-    fn, t, global_batch = build(topo, args.micro)
+
+    # 1. the link: RCCL p2p client 0 -> server, one direction, one cut's worth of bytes
+    peak = None
+    try:
+        progress("p2p peak")
+        p = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
+        pk = torch.tensor([p or 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+        peak = float(pk.item())
+        out["p2p_peak_GBps_measured"] = round(peak, 2)
+    except Exception as e:
+        out["p2p_peak_GBps_measured"] = {"error": repr(e)[:300]}
+
+    # 2. the exchange: predicted from the link, decided by a short trial of both on this topology
+    exch = {"vendor_link_GBps": XGMI_LINK_GBPS}
+    if topo == "replicated":
+        fn, t, global_batch = build(topo, args.micro, False)
+    else:
+        forced = {"dense": False, "codec": True}.get("dense" if args.dense_exchange else args.exchange)
+        exch["prediction_ms_per_step"] = predict_exchange(nc if topo == "hub" else 1, B, peak)
+        trials = {}
+        built = {}
+        for name, codec in (("dense", False), ("codec", True)):
+            if forced is not None and codec != forced:
+                continue
+            progress(f"{topo} x{world}: {name} exchange trial")
+            f, tt, gb = build(topo, args.micro, codec)
+            dtt = timed(f, 3, 2, dev)
+            trials[name] = round(dtt / 3 * 1e3, 3)
+            built[name] = (f, tt, gb)
+        choice = min(trials, key=trials.get)
+        exch.update(choice=choice, trial_ms_per_step=trials,
+                    rule=("forced by flag" if forced is not None else
+                          "the faster of a 3-step trial of each (after 2 warm-up steps) on this topology"),
+                    prediction_agrees=(min(exch["prediction_ms_per_step"], key=exch["prediction_ms_per_step"].get)
+                                       == choice) if peak else None)
+        fn, t, global_batch = built[choice]
+        for name in list(built):
+            if name != choice:
+                del built[name]
+        torch.cuda.empty_cache()
+
+    # 3. the headline
     progress(f"{topo} x{world}: timing {args.steps} steps")
     dt = timed(fn, args.steps, args.warmup, dev)
     out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
     out["config"] = {"workload": labels[topo], "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
-                     "parallelism": f"{topo}{world}", "graph": bool(getattr(t, "graph", False))}
-    if topo == "replicated":
-        out["config"]["replica_step"] = ("fused single-GPU step kernels (x3 conv2, client images, client backward "
-                                         "in the dgrad epilogue) captured in a HIP graph; bucket all-reduce "
-                                         "outside the graph; one launch steps both stages" if t.fused else "unfused")
+                     "parallelism": {"pipeline": "k3-client-server", "hub": f"k4-{nc}clients-1server"}.get(topo, f"dp{world}"),
+                     "graph": bool(getattr(t, "graph", False))}
     out["scaling"] = "weak"
     if topo != "replicated":
         out["config"]["micro_batches"] = args.micro
+        out["config"]["per_client_batch"] = B
+        out["config"]["cut_exchange"] = codec_label[exch["choice"] == "codec"]
         moved, dense = wire(t)
-        out["exchange"] = {"cut_codec": cut_codec, "link_bytes_per_step_moved": moved, "link_bytes_per_step_dense": dense,
-                           "dense_equivalent_GBps_per_link_per_direction": round(dense / 2 / (dt / args.steps) / 1e9, 2),
-                           "wire_GBps_per_link_per_direction": round(moved / 2 / (dt / args.steps) / 1e9, 2)}
+        step_s = dt / args.steps
+        per_dir_dense = B * CUT_BYTES
+        wgbps = moved / 2 / step_s / 1e9
+        exch.update(link_bytes_per_step_moved=moved, link_bytes_per_step_dense=dense,
+                    cut_bytes_per_link_per_direction_per_step_dense=per_dir_dense,
+                    dense_equivalent_GBps_per_link_per_direction=round(per_dir_dense / step_s / 1e9, 2),
+                    wire_GBps_per_link_per_direction=round(wgbps, 2),
+                    wire_frac_of_measured_p2p_peak=round(wgbps / peak, 3) if peak else None,
+                    wire_frac_of_vendor_link=round(wgbps / XGMI_LINK_GBPS, 3))
+        if topo == "hub":
+            exch["server_inbound_wire_GBps_all_links"] = round(wgbps * nc, 2)
+        out["exchange"] = exch
+    else:
+        out["config"]["replica_step"] = ("fused single-GPU step kernels (x3 conv2, client images, client backward "
+                                         "in the dgrad epilogue) captured in a HIP graph; bucket all-reduce "
+                                         "outside the graph; one launch steps both stages" if t.fused else "unfused")
+    del fn, t
+    torch.cuda.empty_cache()
 
-    peak = None
-    if not args.no_exchange_phase:
+    if topo != "replicated" and not args.no_exchange_phase:
+        # side object: data-parallel replicas of the fused K2 step on every GPU (not a BASELINE config)
         try:
-            progress("p2p peak")
-            p = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
-            pk = torch.tensor([p or 0.0], dtype=torch.float64, device=dev)
-            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
-            peak = float(pk.item())
-            out["p2p_peak_GBps_measured"] = round(peak, 2)
-        except Exception as e:
-            out["p2p_peak_GBps_measured"] = {"error": repr(e)[:300]}
-    if topo == "replicated" and not args.no_exchange_phase:
-        # the BASELINE topology of this N on the reference cut
-        ex = "pipeline" if world == 2 else "hub"
-        key = "k3_pipeline" if world == 2 else "k4_hub"
-        try:
-            fn2, t2, gb2 = build(ex, args.micro)
+            fn2, t2, gb2 = build("replicated", args.micro, False)
             K2 = args.exchange_steps
-            progress(f"{key} x{world}: timing {K2} steps")
+            progress(f"replicated x{world}: timing {K2} steps")
             dt2 = timed(fn2, K2, 2, dev)
-            per_dir = B * CUT_BYTES          # one client link, one direction, per step, dense
-            moved, dense = wire(t2)
-            gbps = per_dir / (dt2 / K2) / 1e9                    # dense-equivalent cut rate
-            wgbps = moved / 2 / (dt2 / K2) / 1e9                 # what actually crossed the link
-            r = {"workload": labels[ex], "samples_per_s": round(K2 * gb2 / dt2, 1), "ms_per_step": round(dt2 / K2 * 1e3, 3),
-                 "global_batch": gb2, "per_client_batch": B, "micro_batches": args.micro, "cut_codec": cut_codec,
-                 "cut_bytes_per_link_per_direction_per_step": per_dir,
-                 "link_bytes_per_step_moved": moved, "link_bytes_per_step_dense": dense,
-                 "exchange_GBps_per_link_per_direction": round(gbps, 2),
-                 "wire_GBps_per_link_per_direction": round(wgbps, 2),
-                 "wire_frac_of_measured_p2p_peak": round(wgbps / peak, 3) if peak else None,
-                 "wire_frac_of_vendor_link": round(wgbps / XGMI_LINK_GBPS, 3)}
-            if ex == "hub":
-                r["server_inbound_GBps_all_links"] = round(gbps * (world - 1), 2)
-            out[key] = r
+            out["replicated_dp"] = {"workload": labels["replicated"], "samples_per_s": round(K2 * gb2 / dt2, 1),
+                                    "ms_per_step": round(dt2 / K2 * 1e3, 3), "global_batch": gb2,
+                                    "replica_step": "fused" if t2.fused else "unfused"}
+            del fn2, t2
+            torch.cuda.empty_cache()
         except Exception as e:  # the headline number stands on its own
-            out[key] = {"error": repr(e)[:300]}
+            out["replicated_dp"] = {"error": repr(e)[:300]}
     if not args.no_k5:
         # BASELINE config 5 SplitFed: N-1 client GPUs run the widened conv stack, GPU N-1 the head
         try:
@@ -535,10 +604,12 @@ def run_distributed(args, out, rank, world, local):
                 data = SyntheticCIFAR(42 + rank)
                 xs, ys = zip(*(data.batch(Bk) for _ in range(2)))
                 WX, WY = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
-                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=grp, micro=args.micro)
+                wt = sd.WideHub(WideClientStage(wa, device=dev), rank, world, client_group=grp, micro=args.micro,
+                                groups=groups)
                 wfn = lambda i: wt.client_step(WX[i % 2], WY[i % 2])  # noqa: E731
             else:
-                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=grp, micro=args.micro)
+                wt = sd.WideHub(WideServerStage(wb, device=dev), rank, world, client_group=grp, micro=args.micro,
+                                groups=groups)
                 wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
             Kw = max(3, min(args.steps, 10))
             progress(f"k5_splitfed x{world}: timing {Kw} steps")
@@ -627,6 +698,11 @@ def main():
         out["cpu_baseline"] = cpu
         if cpu.get("value"):
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 1)
+    try:
+        from splitcnn import _lib
+        out["build"] = {"slk_build_id": _lib.build_id()[:16], "variant_defines": _lib.VARIANT_DEFINES}
+    except Exception as e:  # noqa: BLE001
+        out["build"] = {"error": repr(e)[:200]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

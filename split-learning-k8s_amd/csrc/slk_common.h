@@ -28,13 +28,6 @@ constexpr int W3_N = NCLS * P_SAMPLE;// 92160
 constexpr int CODE_NONE = 4;         // pooled value <= 0: ReLU blocks the gradient
 }  // namespace slk
 
-// Profiling-only ablation switch (tools/ablate.py builds separate libraries with -DSLK_ABL=...):
-// bit 1 = drop the MFMAs of the conv2 main loops (operands kept live), bit 2 = drop their LDS operand
-// reads, bit 4 = drop the per-unit staging (LDS-DMA + register-staged operands). Production = 0.
-#ifndef SLK_ABL
-#define SLK_ABL 0
-#endif
-
 // Pin gather-then-MFMA phases in the conv2 main loops with sched_barrier (A/B switch).
 #ifndef SLK_PIN_PHASES
 #define SLK_PIN_PHASES 0
@@ -58,28 +51,11 @@ static inline hipStream_t slk_stream(void* s) { return reinterpret_cast<hipStrea
 // 16x16x4: lane l supplies A[i=l&15][k=l>>4] and B[k=l>>4][j=l&15];
 //          D: col = l&15, row = 4*(l>>4) + r, r in [0,4).
 __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
-#if SLK_ABL & 1
-    c[0] += a * b;
-    return c;
-#else
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-#endif
 }
 __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
-#if SLK_ABL & 1
-    c[0] += a * b;
-    return c;
-#else
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-#endif
 }
-// LDS operand read (ablation bit 2 replaces it by a register value)
-#if SLK_ABL & 2
-#define SLK_LDS(ptr_expr) (slk_abl_reg)
-#else
-#define SLK_LDS(ptr_expr) (ptr_expr)
-#endif
-
 // Butterfly sum over the 64 lanes: every lane ends with the total, bit-identically (each step adds
 // the same two partial sums, commutatively, in both partner lanes). Inside a 16-lane row by DPP
 // (quad_perm 1032 / 2301, row_half_mirror, row_mirror: no LDS traffic), then across rows by

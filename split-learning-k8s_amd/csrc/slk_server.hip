@@ -91,12 +91,6 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
     __syncthreads();
 
     int buf = 0;
-    float slk_abl_reg = (float)lane;
-    slk_keep(slk_abl_reg);
-#if SLK_ABL & 16
-    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-    const int b_first = b;
-#endif
 #pragma unroll 1
     for (; b < B; b += gridDim.x) {
         f32x16 acc[C2F_TPW];
@@ -108,7 +102,7 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
         for (int hc = 0; hc < 2; ++hc) {
             // prefetch the next half (this sample's second half, or the next sample's first)
             const int nb = hc ? b + gridDim.x : b;
-            if (!(SLK_ABL & 4) && nb < B) c2f_dma_half(act + (size_t)nb * A_SAMPLE + (hc ? 0 : C2F_IMG), imgb + (buf ^ 1) * C2F_IMG,
+            if (nb < B) c2f_dma_half(act + (size_t)nb * A_SAMPLE + (hc ? 0 : C2F_IMG), imgb + (buf ^ 1) * C2F_IMG,
                                      wave, lane);
             const float* img = imgb + buf * C2F_IMG;
             const float* wl = w2s + hc * C2F_WH + h * 64 + ct * 32 + j;
@@ -122,10 +116,10 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
                 const float* wt = wl + tap * 8 * 128;
 #pragma unroll
                 for (int ci_lo = 0; ci_lo < 8; ++ci_lo) {
-                    const float bv = SLK_LDS(wt[ci_lo * 128]);
+                    const float bv = wt[ci_lo * 128];
 #pragma unroll
                     for (int t = 0; t < C2F_TPW; ++t)
-                        acc[t] = mfma32x32x2(SLK_LDS(img[tb[t] + ci_lo * A_PIX]), bv, acc[t]);
+                        acc[t] = mfma32x32x2(img[tb[t] + ci_lo * A_PIX], bv, acc[t]);
                 }
             }
             __syncthreads();  // all reads of `buf` done; the prefetch into buf^1 has landed
@@ -156,12 +150,6 @@ __global__ __launch_bounds__(C2F_THREADS, 3) void conv2_fwd_pool_kernel(
             *reinterpret_cast<unsigned int*>(crow + w0) = c4;
         }
     }
-#if SLK_ABL & 16
-    // diagnostic: in-kernel clock (GHz) of this workgroup into pooled[blockIdx.x] (output is garbage)
-    __syncthreads();
-    const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0 && b_first < B) pooled[blockIdx.x] = (float)((double)(clk_t1 - clk_t0) / (double)(clk_r1 - clk_r0) * 0.1);
-#endif
 }
 
 // ============================================================================ conv2 dgrad (cut grad)
@@ -189,8 +177,6 @@ constexpr int C2D_STG = (C2D_CO * P_WIN + C2D_THREADS - 1) / C2D_THREADS;  // 2 
 template <int NT>
 __device__ __forceinline__ void c2d_chunk(const float* __restrict__ dcp, const float* __restrict__ wc,
                                           const int (&pbase)[2], f32x16 (&acc)[2]) {
-    float slk_abl_reg = (float)threadIdx.x;
-    slk_keep(slk_abl_reg);
 #pragma unroll
     for (int co_lo = 0; co_lo < 4; ++co_lo) {
         // gather this channel's 9 taps of operands, then 9*NT MFMAs back to back
@@ -198,10 +184,10 @@ __device__ __forceinline__ void c2d_chunk(const float* __restrict__ dcp, const f
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int ky = tap / 3, kx = tap % 3;
-            av[tap] = SLK_LDS(wc[(co_lo * 9 + tap) * 64]);
+            av[tap] = wc[(co_lo * 9 + tap) * 64];
             const int imm = co_lo * C2D_PLANE + (2 - ky) * 28 + (2 - kx);
 #pragma unroll
-            for (int i = 0; i < NT; ++i) bv[tap][i] = SLK_LDS(dcp[pbase[i] + imm]);
+            for (int i = 0; i < NT; ++i) bv[tap][i] = dcp[pbase[i] + imm];
         }
 #if SLK_PIN_PHASES
         __builtin_amdgcn_sched_barrier(0);
@@ -296,12 +282,12 @@ __global__ __launch_bounds__(C2D_THREADS, 3) void conv2_dgrad_kernel(
         for (int ch = 0; ch < C2D_NCHUNK; ++ch) {
             const int nb = (ch + 1 < C2D_NCHUNK) ? b : b + gridDim.x;
             const int nch = (ch + 1 < C2D_NCHUNK) ? ch + 1 : 0;
-            if (!(SLK_ABL & 4)) load_chunk(nb, nch);
+            load_chunk(nb, nch);
             const float* dcp = dcb + buf * C2D_DC;
             const float* wc = w2d + ch * C2D_WC + h * 32 + j;
             if (nt == 2) c2d_chunk<2>(dcp, wc, pbase, acc);
             else c2d_chunk<1>(dcp, wc, pbase, acc);
-            if (!(SLK_ABL & 4) && nb < B) write_chunk(dcb + (buf ^ 1) * C2D_DC);
+            if (nb < B) write_chunk(dcb + (buf ^ 1) * C2D_DC);
             __syncthreads();
             buf ^= 1;
         }
@@ -430,16 +416,14 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
     __syncthreads();
 
     const int q0 = h, q1 = 2 + h;  // pixel of this lane half in k steps t = 0, 1
-    float slk_abl_reg = (float)lane;
-    slk_keep(slk_abl_reg);
     int buf = 0;
 #pragma unroll 1
     for (; u < nunit; u += gridDim.x) {
         const int nu = u + gridDim.x;
         float* cur = smem + buf * C2W_BUF;
         float* nxt = smem + (buf ^ 1) * C2W_BUF;
-        if (!(SLK_ABL & 4) && nu < nunit) c2w_dma_band(act + (size_t)(nu >> 1) * A_SAMPLE + (nu & 1) * 12 * A_HW, nxt, wave, lane);
-        if (!(SLK_ABL & 36)) load_dc(nu);
+        if (nu < nunit) c2w_dma_band(act + (size_t)(nu >> 1) * A_SAMPLE + (nu & 1) * 12 * A_HW, nxt, wave, lane);
+        load_dc(nu);
         db_accum(cur);
         const float* img = cur;
         const float* dcb = cur + C2W_IMG;
@@ -455,12 +439,12 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int px = 2 * i + kh;
-                dv[i] = SLK_LDS(dr[px * C2W_DSTR]);
-                cd[i] = SLK_LDS(cr[px * C2W_CDSTR]);
+                dv[i] = dr[px * C2W_DSTR];
+                cd[i] = cr[px * C2W_CDSTR];
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
 #pragma unroll
-                    for (int tt = 0; tt < 3; ++tt) bv[i][t][tt] = SLK_LDS(ir[base[tt] + t * A_HW + 2 * px]);
+                    for (int tt = 0; tt < 3; ++tt) bv[i][t][tt] = ir[base[tt] + t * A_HW + 2 * px];
             }
 #if SLK_PIN_PHASES
             __builtin_amdgcn_sched_barrier(0);
@@ -479,7 +463,7 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
             __builtin_amdgcn_sched_barrier(0);
 #endif
         }
-        if (!(SLK_ABL & 36) && nu < nunit) write_dc(nxt);
+        if (nu < nunit) write_dc(nxt);
         __syncthreads();
         buf ^= 1;
     }

@@ -39,18 +39,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef SLK_WIDE_XCD
 #define SLK_WIDE_XCD 1
 #endif
-// Profiling only (tools/ablate_wide.py): SLK_WABL bit 64 drops the conv epilogues, bit 128 the EXP
-// expansion in the main loop, bit 256 the barrier of odd taps, bit 512 the main loop's vmcnt waits,
-// bit 1024 the fragment reads, bit 2048 the DMA issue (8192 weights only, 16384 input only), bit 4096
-// every barrier (results wrong; timing only). Production = 0.
-// Profiling only: SLK_WIDE_FIXSRC = 1 stages every tile's input (conv) / output gradient (wgrad) from
-// sample 0 (L2-resident): the HBM-read share of a kernel's time.
-#ifndef SLK_WIDE_FIXSRC
-#define SLK_WIDE_FIXSRC 0
-#endif
-#ifndef SLK_WABL
-#define SLK_WABL 0
-#endif
 // Wave priority: raise it around each step's MFMA block (1: conv kernels, 2: also wgrad), so a wave
 // with MFMAs ready issues ahead of a co-resident wave's epilogue VALU / staging work.
 #ifndef SLK_WIDE_DMA_LATE
@@ -263,7 +251,7 @@ __device__ __forceinline__ void issue_input(const uint16_t* __restrict__ in, con
                                             const int (&poff)[C::NDW], int g, char* slot, int wave, int lane) {
     const int c = wave & 3;
     const char* plane = reinterpret_cast<const char*>(in) +
-                        ((size_t)((SLK_WIDE_FIXSRC ? 0 : s.n) * (C::CI / 8) + g * 4 + c) * (C::HW * C::HW)) * 16;
+                        ((size_t)(s.n * (C::CI / 8) + g * 4 + c) * (C::HW * C::HW)) * 16;
     const char* zero = reinterpret_cast<const char*>(slk_wide_zero);
     char* dst = slot + c * C::NPP * 16;
 #pragma unroll
@@ -508,7 +496,6 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                 const bool last = tail && g == C::G - 1 && tap == 8;
                 // step s+1's weight slice (and at tap 8 the next group's input tile) has landed
                 if (tail) wait_vmcnt<0>();
-                else if (SLK_WABL & 512) {}
                 else if (SLK_WIDE_EPI && tap < 2 && g == 0) {
                     // weight step +1 predates the previous epilogue and this tile's epilogue loads
                     if (tap == 0) {
@@ -524,7 +511,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                 // EXP: the next group's staged items landed by tap 3's wait and were expanded after its
                 // barrier; this wave's tile writes (and raw reads) complete before tap 4's barrier
                 if (C::EXP && tap == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (!((SLK_WABL & 256) && (tap & 1)) && !(SLK_WABL & 4096)) __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 // weight step +3 into the slot of step -1; at tap 0 the next group's input tile. Both
                 // after this step's MFMAs when SLK_WIDE_DMA_LATE (same order of VMEM operations, so
@@ -534,12 +521,10 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                         const int sl = g * 9 + tap + C::L;
                         int ws = wslot + C::L;
                         ws = ws >= C::RW ? ws - C::RW : ws;
-                        if (SLK_WABL & (2048 | 8192)) {}
-                        else if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
+                        if (sl < C::S) issue_weight<C>(wsh, cur.cob, sl, wslot0 + ws * C::W_SLOT, wave, lane);
                         else if (!tail) issue_weight<C>(wsh, nxt.cob, sl - C::S, wslot0 + ws * C::W_SLOT, wave, lane);
                     }
-                    if (SLK_WABL & (2048 | 16384)) {}
-                    else if constexpr (C::EXP) {
+                    if constexpr (C::EXP) {
                         if ((g + 1 < C::G || !tail) && tap == 0) {
                             if (g + 1 < C::G) exp_issue<C>(in, out2, cur, g + 1, raw, wave, lane);
                             else exp_issue<C>(in, out2, nxt, 0, raw, wave, lane);
@@ -554,7 +539,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                 // EXP: the next group's pooled input, staged by LDS-DMA at tap 0, is expanded into the
                 // free slot at tap 3 (read from tap 8 on)
                 if constexpr (C::EXP) {
-                    if ((g + 1 < C::G || !tail) && tap == 3 && !(SLK_WABL & 128))
+                    if ((g + 1 < C::G || !tail) && tap == 3)
                         exp_expand<C>(islot0 + (islot ^ 1) * C::IN_SLOT, raw, tid);
                 }
                 bf16x8 av[4], bv[C::FW];
@@ -563,7 +548,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
 #pragma unroll
                 for (int f = 0; f < C::FW; ++f) bv[f] = bv_n[f];
                 const int wn1 = wslot + 1 == C::RW ? 0 : wslot + 1;
-                if (!last && !(SLK_WABL & 1024)) {
+                if (!last) {
                     const char* wb = wslot0 + wn1 * C::W_SLOT;
                     const char* ib = islot0 + (tap == 8 ? (islot ^ 1) : islot) * C::IN_SLOT;
                     const int tn = tap == 8 ? 0 : tap + 1;
@@ -587,12 +572,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
         }
         // ------------------------------------------------------------------ epilogue
         const int ch_base = cur.cob * C::MT + wm * 64 + 4 * (lane >> 4);
-        if (SLK_WABL & 64) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int f = 0; f < C::FW; ++f) slk_keep(acc[i][f]);
-        } else if constexpr (C::MODE == wide::MODE_FWD_POOL) {
+        if constexpr (C::MODE == wide::MODE_FWD_POOL) {
             constexpr int PH = C::HW / 2;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1111,7 +1091,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
             const int piece = wave * ((16 * PPC) / 8) + k;
             const int c = piece / PPC, part = piece - (piece / PPC) * PPC;
             const char* src = reinterpret_cast<const char*>(dc) +
-                              (((size_t)((SLK_WIDE_FIXSRC ? 0 : n) * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
+                              (((size_t)(n * (C::CO / 8) + cob * 16 + c) * C::HW + rb * C::TR) * C::HW) * 16 +
                               part * 1024 + lane * 16;
             glds16((const void*)src, lds_u32(buf + c * C::NPXP * 16 + part * 1024));
         }

@@ -154,36 +154,18 @@ __device__ __forceinline__ void wg_wait_vmcnt() { asm volatile("s_waitcnt vmcnt(
 // Wait states: B comes from the colstep asm (ends with s_nop 1); the accumulators are read by VALU only
 // after mfma_drain(); AGPRs are written once per launch, long before the first MFMA.
 __device__ __forceinline__ void mfma_a(f32x4& acc, float a, float b) {
-#if SLK_ABL & 1
-    acc[0] += b;
-    asm volatile("" ::"a"(a));
-#else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "a"(a), "v"(b));
-#endif
 }
 // first k step: C = 0 (an inline constant), so the accumulators need no zeroing instructions
 __device__ __forceinline__ void mfma_a0(f32x4& acc, float a, float b) {
-#if SLK_ABL & 1
-    acc = f32x4{b, 0.f, 0.f, 0.f};
-    asm volatile("" ::"a"(a));
-#else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=v"(acc) : "a"(a), "v"(b));
-#endif
 }
 // accumulators kept in AGPRs (A, B in VGPRs): the weight gradient's 256 accumulator registers
 __device__ __forceinline__ void mfma_acc(f32x4& acc, float a, float b) {
-#if SLK_ABL & 1
-    acc[0] += a * b;
-#else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-#endif
 }
 __device__ __forceinline__ void mfma_acc0(f32x4& acc, float a, float b) {
-#if SLK_ABL & 1
-    acc = f32x4{a * b, 0.f, 0.f, 0.f};
-#else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
-#endif
 }
 // MFMA result -> VALU read: the 8-pass XDL op needs >= 11 wait states before hipcc's code reads acc
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15" ::: "memory"); }
@@ -399,13 +381,7 @@ __device__ __forceinline__ void lds_patch_pk(const float* ps, f2 (&lo)[4], f2 (&
 // ones, so it reaches all four outputs of the window with coefficient +1 (no bias adds in the
 // epilogue).
 __device__ __forceinline__ void mfma_ac(f32x4& acc, float a, float b, const f32x4& c) {
-#if SLK_ABL & 1
-    acc = c;
-    acc[0] += b;
-    asm volatile("" ::"a"(a));
-#else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=v"(acc) : "a"(a), "v"(b), "v"(c));
-#endif
 }
 
 // A band's staging DMA: wave pair half h moves chunks c = h, h+2, ... (< WF_CHUNKS) of 64 sixteen-byte
@@ -870,15 +846,6 @@ constexpr int WW_DP_CH = 64 * 13 / 64;                // 13 chunks (13 sixteen-b
 #endif
 constexpr int WW_CSTR = SLK_WW_CSTR;                  // code band row stride in bytes (48 used)
 constexpr int WW_LUTS = SLK_WW_LUTS;                  // ZT row stride in floats (16 used)
-// Profiling-only ablation bits (tools/build_variant.sh -DSLK_WW_ABL=...; outputs wrong): 1 = no code
-// reads (code 0), 2 = no dpooled reads, 4 = no ZT reads, 8 = code as a dword read + byte extract,
-// 16 = no DMA / wait / barrier in the unit loop, 32 = no act patch transform (raw patch as operand),
-// 64 = no MFMA (operands kept alive), 128 = no barrier per unit, 256 = no DMA issue per unit,
-// 512 = clock diagnostic: slab[0] of each workgroup = its mean shader clock in GHz, 1024 = every DMA
-// re-fetches the workgroup's first unit (L2-resident source: DMA mechanism vs memory traffic).
-#ifndef SLK_WW_ABL
-#define SLK_WW_ABL 0
-#endif
 constexpr int WW_CD_OFF = WW_DP_OFF + 64 * WW_DSTR;   // float offset of the code band
 constexpr int WW_CD_PC = WW_CSTR / 16;                // DMA pieces per code row (3 used)
 constexpr int WW_CD_CH = 64 * WW_CD_PC / 64;          // chunks of the code band
@@ -887,7 +854,7 @@ constexpr int WW_BSTR = WW_CD_OFF + 64 * WW_CSTR / 4; // 12800 floats = 51,200 B
 constexpr int WW_GRID = 256;
 constexpr int WW_SLAB = W2_N + C2;
 // Staging buffers (2: a unit's DMA is issued one unit ahead). Removing DMA + wait + barrier saves
-// 0.085 of 0.413 ms (tools/ablate.py, -DSLK_WW_ABL=16), but 3 buffers (DMA two units ahead) gain
+// 0.085 of 0.413 ms (a round-1 ablation build), but 3 buffers (DMA two units ahead) gain
 // nothing (0.422 vs 0.417 ms): not DMA latency. Knob kept for A/B.
 #ifndef SLK_WW_NBUF
 #define SLK_WW_NBUF 2
@@ -947,7 +914,6 @@ __device__ __forceinline__ void ww_dma_table(uint4* tab, int wave, int lane) {
 __device__ __forceinline__ void ww_dma_unit(const float* __restrict__ act, const float* __restrict__ dpool,
                                             const uint8_t* __restrict__ code, int u, const float* dst, int wave,
                                             int lane, const uint4* tab, int i0 = 0, int i1 = 1 << 20) {
-    if (SLK_WW_ABL & 1024) u = blockIdx.x;
     const int b = u / 3, band = u - 3 * (u / 3);
     wave &= WW_WAVES - 1;   // (known range: the chunk bound below folds away for i < WW_PPW - 1)
     const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
@@ -999,9 +965,6 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar branches on tp
     const int mh = wu & 1, tp = wu >> 1;
     const int nunit = 3 * B;
-#if SLK_WW_ABL & 512
-    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
 
     int u = blockIdx.x;
     ww_dma_table(dtab, wu, lane);   // read back only by the same lane: no barrier
@@ -1029,7 +992,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
         // this unit's DMA landed (no other vector memory ops in this loop: only the next unit's batch
         // may stay in flight) and every wave is done with the buffer refilled next
         const int nu = u + (WW_NBUF - 1) * (int)gridDim.x;
-        if (!(SLK_WW_ABL & 16)) {
+        {
             if (WW_NBUF > 2 && u + (int)gridDim.x < nunit) {
                 switch (wu) {
                     case 0: ww_wait_newest_batch<0>(); break;
@@ -1040,8 +1003,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             } else {
                 wg_wait_vmcnt<0>();
             }
-            if (!(SLK_WW_ABL & 128)) lds_barrier();
-            if (nu < nunit && !(SLK_WW_ABL & 256) && !WW_SPREAD) {
+            lds_barrier();
+            if (nu < nunit && !WW_SPREAD) {
                 const int nb = buf + WW_NBUF - 1 >= WW_NBUF ? buf - 1 : buf + WW_NBUF - 1;
                 ww_dma_unit(act, dpool, code, nu, smem + nb * WW_BSTR, wu, lane, dtab);
             }
@@ -1066,14 +1029,8 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             lds_patch_pk(pa + 16 * WF_CSTR, lo[1], hi[1]);
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
-                v[m] = (SLK_WW_ABL & 2) ? 1.f : dpb[m * 16 * WW_DSTR + tl];
-                if (SLK_WW_ABL & 1)
-                    c[m] = 0;
-                else if (SLK_WW_ABL & 8)
-                    c[m] = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(cdb + m * 16 * WW_CSTR + (tl & ~3)),
-                                                 8 * (tl & 3), 8);
-                else
-                    c[m] = cdb[m * 16 * WW_CSTR + tl];
+                v[m] = dpb[m * 16 * WW_DSTR + tl];
+                c[m] = cdb[m * 16 * WW_CSTR + tl];
             }
         };
         f2 v01[2][4], v23[2][4], z01[2][4], z23[2][4];
@@ -1084,19 +1041,12 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
             for (int m = 0; m < 2; ++m) {
                 const float4* zt = reinterpret_cast<const float4*>(lutz + WW_LUTS * c[m]);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) E[m][i] = (SLK_WW_ABL & 4) ? make_float4(1.f, 0.f, 1.f, 0.f) : zt[i];
+                for (int i = 0; i < 4; ++i) E[m][i] = zt[i];
             }
         };
         auto xform = [&](const f2 (&lo)[2][4], const f2 (&hi)[2][4], const float (&v)[2], const float4 (&E)[2][4]) {
-            if (SLK_WW_ABL & 32) {
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { v01[n][r] = lo[n][r]; v23[n][r] = hi[n][r]; }
-            } else {
-                pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
-                pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
-            }
+            pk_wino_in(lo[0], hi[0], v01[0], v23[0]);
+            pk_wino_in(lo[1], hi[1], v01[1], v23[1]);
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 const f2 vv = {v[m], v[m]};
@@ -1118,7 +1068,7 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             // (SLK_WW_SPREAD) the next unit's staging DMA, two or three pieces per K step
-            if (WW_SPREAD && !(SLK_WW_ABL & (16 | 256)) && nu < nunit)
+            if (WW_SPREAD && nu < nunit)
                 ww_dma_unit(act, dpool, code, nu, dma_dst, wu, lane, dtab, 2 * j, j == 5 ? 1 << 20 : 2 * j + 2);
             if (j < 5) zload(cd[(j + 1) & 1], E);                                  // under these MFMAs
             if (j < 4) load(j + 2, Rlo[j & 1], Rhi[j & 1], dv[j & 1], cd[j & 1]);  // likewise
@@ -1187,13 +1137,6 @@ __global__ __launch_bounds__(WW_THREADS, 1) void conv2_wgrad_wino_kernel(
 #pragma unroll
         for (int m = 0; m < 2; ++m) slab[W2_N + 32 * mh + 16 * m + li] = dbp[m] + park[(mh * 2 + m) * 16 + li];
     }
-#if SLK_WW_ABL & 512
-    lds_barrier();
-    if (tid == 0) {
-        const unsigned long long clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime();
-        slab[0] = (float)((double)(clk_t1 - clk_t0) / (double)(clk_r1 - clk_r0) * 0.1);
-    }
-#endif
 }
 
 extern "C" int slk_conv2_wgrad_nslab(int B) { return B > 0 ? (3 * B < WW_GRID ? 3 * B : WW_GRID) : 0; }

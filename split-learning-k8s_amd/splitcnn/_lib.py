@@ -111,9 +111,19 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    # profiling only: run the same Python path over a variant build (tools/build_variant.sh output,
-    # compiled from these very sources, so the provenance check below still applies)
-    path = os.environ.get("SLK_LIB_VARIANT", path)
+    # profiling only: run the same Python path over a variant build (tools/build_variant.sh output). Its
+    # build id hashes the sources AND its -D defines (recorded next to it), so it is checked against
+    # those, and VARIANT_DEFINES says so to every caller (bench.py prints it in its JSON line).
+    global VARIANT_DEFINES
+    defines = ()
+    if os.environ.get("SLK_LIB_VARIANT"):
+        path = os.environ["SLK_LIB_VARIANT"]
+        from .build import defines_path
+        try:
+            defines = tuple(open(defines_path(path)).read().split())
+        except OSError:
+            raise ImportError(f"splitcnn: variant {path} has no {defines_path(path)} (build it with "
+                              "tools/build_variant.sh)")
     if not os.path.exists(path):
         raise ImportError(
             f"splitcnn: {path} is missing. Build the HIP kernels first "
@@ -125,13 +135,22 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
     # provenance: the library must have been built from exactly the sources in this tree
     if os.path.isdir(CSRC_DIR):
-        built, want = lib.slk_build_id().decode(), source_hash()
+        built, want = lib.slk_build_id().decode(), source_hash(defines)
         if built != want:
             raise ImportError(
                 f"splitcnn: {path} was built from other sources (build id {built[:12]}, tree {want[:12]}). "
                 "Rebuild it (python -c 'import __graft_entry__ as g; g.build()').")
+    VARIANT_DEFINES = defines if os.environ.get("SLK_LIB_VARIANT") else None
     _lib = lib
     return lib
+
+
+VARIANT_DEFINES = None   # the -D defines of a loaded variant build (None: the product library)
+
+
+def build_id() -> str:
+    """slk_build_id of the loaded library (sha256 of its sources and defines)."""
+    return load().slk_build_id().decode()
 
 
 def call(name: str, *args) -> None:

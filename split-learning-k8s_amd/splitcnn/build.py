@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libslk.so")
 SOURCES = ["slk_client.hip", "slk_server.hip", "slk_optim.hip", "slk_data.hip", "slk_wide.hip",
            "slk_wide_head.hip", "slk_wino.hip", "slk_codec.hip", "slk_x3.hip"]
 ARCH = "gfx950"
-# Per-source extra hipcc flags (none needed at present; profiling variants pass -D defines).
+# Per-source extra hipcc flags (none needed at present; tools/build_variant.sh passes -D defines).
 EXTRA_FLAGS: dict = {}
 
 
@@ -39,11 +39,14 @@ def _inputs():
     return srcs, hdrs
 
 
-def source_hash() -> str:
-    """sha256 over every input of the library (the HIP sources, csrc/*.h, include/slk.h), by name and
-    content. It is compiled into libslk.so (slk_build_id) so a binary can be tied to its sources."""
+def source_hash(defines=()) -> str:
+    """sha256 over every input of the library (the HIP sources, csrc/*.h, include/slk.h, by name and
+    content) and the extra -D defines it is compiled with (none for the product library). It is
+    compiled into libslk.so (slk_build_id), so a binary is tied to its sources AND its defines: a
+    variant build with tuning defines never passes as the product library."""
     srcs, hdrs = _inputs()
     h = hashlib.sha256()
+    h.update(b"defines:" + " ".join(sorted(defines)).encode() + b"\0")
     for f in sorted(srcs + hdrs, key=os.path.basename):
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -72,7 +75,13 @@ def needs_build() -> bool:
 
 def _compile_cmd(src: str, obj: str, defines) -> list:
     return [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE_DIR, *defines,
-            f'-DSLK_BUILD_ID="{source_hash()}"', *EXTRA_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+            f'-DSLK_BUILD_ID="{source_hash(defines)}"', *EXTRA_FLAGS.get(os.path.basename(src), []), "-c", src,
+            "-o", obj]
+
+
+def defines_path(lib_path: str) -> str:
+    """Where a variant build records its -D defines (next to the library)."""
+    return os.path.splitext(lib_path)[0] + ".defines"
 
 
 def build_library(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
@@ -106,6 +115,9 @@ def build_library(force: bool = False, verbose: bool = False, out: str | None = 
         if res.returncode != 0:
             raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-4000:]}")
         os.replace(tmp, target)
+        if out is not None:
+            with open(defines_path(target), "w") as fh:
+                fh.write(" ".join(sorted(defines)) + "\n")
     finally:
         shutil.rmtree(tmpdir, ignore_errors=True)
     return target

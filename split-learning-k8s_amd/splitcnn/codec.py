@@ -22,10 +22,13 @@ class CutCodec:
         self._bufs = {}
 
     def _buf(self, key, shape, dtype, device):
-        t = self._bufs.get(key)
-        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != device:
+        # keyed by shape too: a buffer is never replaced, so a HIP graph captured around these kernels at
+        # one micro-batch size keeps valid pointers after another size has run (dist.Hub's chunk graphs)
+        k = (key, tuple(shape), dtype, str(torch.device(device)))
+        t = self._bufs.get(k)
+        if t is None:
             t = torch.empty(shape, dtype=dtype, device=device)
-            self._bufs[key] = t
+            self._bufs[k] = t
         return t
 
     def buffers(self, key, n: int, device):

@@ -30,7 +30,9 @@ stages in the CPU tests).
 """
 from __future__ import annotations
 
+import inspect
 import time
+import warnings
 from typing import Optional
 
 import torch
@@ -107,8 +109,10 @@ def _compute(server, client, act, y, scale):
 def _fused_pair(client, server) -> bool:
     """Same-device engine stages with every conv2 kernel on x3: the replica can run the single-GPU
     fused step's kernels (client conv1 writes the server's split images, the client backward runs in
-    the server's dgrad epilogue) — engine.SplitTrainer's launch sequence minus the optimizer."""
-    return (getattr(server, "conv", None) == "x3" and hasattr(client, "emit_act16")
+    the server's dgrad epilogue) — engine.SplitTrainer's launch sequence minus the optimizer. Decided
+    from the server's three impl_* fields (not its preset name), read at every step."""
+    impls = tuple(getattr(server, a, None) for a in ("impl_fwd", "impl_dgrad", "impl_wgrad"))
+    return (impls == ("x3", "x3", "x3") and hasattr(client, "emit_act16")
             and getattr(client, "device", None) is not None and client.device.type == "cuda"
             and client.device == server.device)
 
@@ -122,9 +126,12 @@ class Replicated:
     gradient instead of the slabs)."""
 
     def __init__(self, client, server, group=None, device=None, fused: Optional[bool] = None,
-                 graph: bool = False):
+                 graph: bool = False, overlap: Optional[bool] = None):
         self.client, self.server = client, server
         self.fused = _fused_pair(client, server) if fused is None else fused
+        if self.fused and overlap:
+            warnings.warn("Replicated: overlap applies to the unfused replica only (the fused replica's "
+                          "client backward runs inside the server's dgrad; its bucket is all-reduced once)")
         if self.fused:
             if not _fused_pair(client, server):
                 raise ValueError("Replicated(fused=True) needs same-device engine stages on the x3 conv preset")
@@ -139,7 +146,8 @@ class Replicated:
         server.bind_grads(self.bucket[CLIENT_N:CLIENT_N + SERVER_N])
         self.loss_slot = self.bucket[-1:]
         self.global_step = 0
-        self.overlap = True   # split the all-reduce so the server's part overlaps the client backward
+        # unfused replica: split the all-reduce so the server's part overlaps the client backward
+        self.overlap = True if overlap is None else bool(overlap)
         self.graph = graph and self.fused
         self._graphs = {}
 
@@ -205,6 +213,9 @@ class Replicated:
 
     def step(self, x, y):
         if self.fused:
+            if not _fused_pair(self.client, self.server):
+                raise RuntimeError("Replicated: the server's conv impls changed after construction; the fused "
+                                   "replica needs x3 for the forward, dgrad and wgrad")
             return self._step_fused(x, y)
         B = x.shape[0]
         scale = 1.0 / (self.world * B)
@@ -227,11 +238,28 @@ class Replicated:
         self.global_step += 1
 
 
+def exchange_groups():
+    """Two process groups over every rank, one per exchange direction (collective: every rank calls
+    this, in the same order).
+
+    RCCL runs all point-to-point ops between two ranks of ONE group in issue order on one communicator
+    stream, and a send larger than its staging buffer completes only once the peer's matching receive
+    runs. The hub server interleaves per chunk (receive micro-batch k, send gradient k, receive k+1)
+    while a client posts every micro-batch before its first gradient receive: on a single group the
+    server's send of gradient k would wait for a receive queued behind the client's send of k+1, which
+    waits for the server's receive of k+1, queued behind that send — a cycle. With the cut direction on
+    one group and the gradient direction on the other, each stream carries one direction, issued in the
+    same order by both sides (tests/test_p2p_order.py replays both sides under these semantics)."""
+    ranks = list(range(dist.get_world_size()))
+    return dist.new_group(ranks), dist.new_group(ranks)
+
+
 class Hub:
     """N-1 client ranks (0..N-2) feed one server rank (N-1) — SplitFed, BASELINE config 4; with one
     client it is the 2-GPU client/server pipeline (config 3, `Pipeline`). Each client cuts its batch
-    into `micro` micro-batches and sends micro-batch k's cut (+ labels, + its per-sample max on GPUs,
-    so the server's x3 kernels need not re-read the cut for their scales) while computing k+1.
+    into `micro` micro-batches and sends micro-batch k's cut (+ labels, + its per-sample max when
+    `ship_amax`, so the server's x3 kernels need not re-read the cut for their scales) while computing
+    k+1.
 
     Server: its buffers are laid out [micro-batch k][client c][b] so that micro-batch k of EVERY client
     is one contiguous chunk of nc*b samples: the server runs one forward/loss/backward per chunk (not
@@ -241,82 +269,108 @@ class Hub:
     the concatenated batch nc*B (src/server_part.py:47-52; the mean-loss scale 1/(nc*B) is applied in
     the cross-entropy kernel). Clients all-reduce their 320-float gradient and step.
 
-    compress (default on for CUDA tensors): the cut and its gradient travel through the lossless sparse
-    codec (codec.py): per micro-batch a 4-byte count, the bit mask and the nonzero activations out, the
-    gradient at those positions back. The sizes RCCL's point-to-point calls need are learned per
-    micro-batch (the client waits only for micro-batch k's encode before sending it, on a side stream,
-    while k+1 computes; the server posts micro-batch k's receives once its count has landed), so no
-    step-wide host sync holds the first send back. Results are bit-identical to the dense exchange.
+    Transport: `groups` = (cut direction, gradient direction), one process group each
+    (`exchange_groups()`, created here when not given; see there for why one group would deadlock).
+
+    compress (default True): the cut and its gradient travel through the lossless sparse codec
+    (codec.py, HIP kernels: CUDA tensors only): per micro-batch a 4-byte count, the bit mask and the
+    nonzero activations out, the gradient at those positions back. The sizes RCCL's point-to-point
+    calls need are learned per micro-batch (the client waits only for micro-batch k's encode before
+    sending it, on a side stream, while k+1 computes; the server posts micro-batch k's receives once
+    its count has landed), so no step-wide host sync holds the first send back. Results are
+    bit-identical to the dense exchange. False = the dense fp32 exchange; a codec object (the
+    CutCodec interface) is used as given. `compress` and `ship_amax` are constructor arguments that
+    both sides must agree on — neither side infers them from its own device.
     `exchange_bytes` counts what moved on this rank's link(s), `dense_bytes` what the dense exchange
     would have moved."""
 
-    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress: bool = True,
-                 group=None, server_rank: Optional[int] = None, client_ranks=None, graph: bool = True):
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress=True,
+                 server_rank: Optional[int] = None, client_ranks=None, graph: bool = True, groups=None,
+                 ship_amax: bool = True):
         self.stage, self.rank, self.world = stage, rank, world
         self.server_rank = world - 1 if server_rank is None else server_rank
         self.client_ranks = list(range(world - 1)) if client_ranks is None else list(client_ranks)
         self.nclients = len(self.client_ranks)
         self.client_group = client_group
-        self.group = group
+        if groups is None:
+            groups = exchange_groups() if dist.is_initialized() else (None, None)
+        self.groups = tuple(groups)
         self.micro = micro
         self.compress = compress
+        self.ship_amax = bool(ship_amax)
         self.graph = graph
         self.global_step = 0
+        self._pool = {}
         self._bufs = {}
         self._graphs = {}
         self._side = None
         self.exchange_bytes = 0
         self.dense_bytes = 0
         self._codec = None
+        # the server passes the shipped max on only to stages whose compute takes it (engine stages)
+        self._amax_kw = "act_amax" in inspect.signature(stage.compute).parameters if hasattr(stage, "compute") else False
 
     @property
     def is_server(self):
         return self.rank == self.server_rank
 
     def _use_codec(self, device):
-        if not (self.compress and torch.device(device).type == "cuda"):
+        if self.compress is False or self.compress is None:
             return None
         if self._codec is None:
-            from .codec import CutCodec
-            self._codec = CutCodec()
+            if self.compress is not True:
+                self._codec = self.compress          # a codec object (the CPU protocol tests)
+            elif torch.device(device).type == "cuda":
+                from .codec import CutCodec
+                self._codec = CutCodec()
+            else:
+                raise ValueError("the cut codec runs as HIP kernels on CUDA tensors: pass compress=False "
+                                 "(on BOTH sides) for CPU stages")
         return self._codec
 
-    @staticmethod
-    def _ship_amax(device) -> bool:
-        """GPU stages exchange the cut's per-sample max with the cut (both sides decide alike)."""
-        return torch.device(device).type == "cuda"
-
     def _buf(self, name, shape, dtype, device, pin=False):
-        t = self._bufs.get(name)
-        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or (not pin and t.device != device):
+        """Scratch keyed by (name, shape, dtype, device): a buffer is never replaced, so the chunk graphs
+        captured at one batch size keep valid pointers after another size has run."""
+        pin = pin and torch.device(device).type == "cuda"
+        key = (name, tuple(shape), dtype, "pinned" if pin else str(torch.device(device)))
+        t = self._pool.get(key)
+        if t is None:
             t = torch.empty(shape, dtype=dtype, pin_memory=True) if pin else torch.empty(shape, dtype=dtype, device=device)
-            self._bufs[name] = t
+            self._pool[key] = t
+        self._bufs[name] = t   # the latest buffer of each name (introspection: tests, cuts_by_client)
         return t
 
+    # streams / events: CUDA only; on the CPU every op is already ordered on the host
     def _side_stream(self, device):
+        if torch.device(device).type != "cuda":
+            return None
         if self._side is None:
             self._side = torch.cuda.Stream(device)
         return self._side
 
-    def _p2p(self, op, t, peer, side=None):
+    @staticmethod
+    def _record(device):
+        if torch.device(device).type != "cuda":
+            return None
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def _p2p(self, op, t, peer, group, side=None):
         """isend / irecv on `side` (a CUDA stream: RCCL then orders the transfer after that stream's
         work only, not after everything queued on the current stream)."""
         if side is None:
-            return op(t, peer, group=self.group)
+            return op(t, peer, group)
         with torch.cuda.stream(side):
-            return op(t, peer, group=self.group)
+            return op(t, peer, group)
 
-    def _recv_count(self, head, src, slot, pinned):
+    def _recv_count(self, head, src, slot, pinned, side):
         """Receive a 1-element int32 count from `src` and return it on the host, without waiting for
         the compute queued on the current stream (side stream + pinned copy)."""
-        dev = head.device
-        if _host_staged(head, self.group):
-            h = torch.empty(1, dtype=torch.int32)
-            dist.irecv(h, src, group=self.group).wait()
-            head.copy_(h)
-            return int(h.item())
-        side = self._side_stream(dev)
-        w = self._p2p(dist.irecv, head, src, side)
+        w = self._p2p(irecv, head, src, self.groups[0], side)
+        if side is None or _host_staged(head, self.groups[0]):
+            w.wait()
+            return int(head.item())
         with torch.cuda.stream(side):
             w.wait()
             pinned[slot:slot + 1].copy_(head, non_blocking=True)
@@ -335,49 +389,52 @@ class Hub:
         b = B // m
         dev = x.device
         srv = self.server_rank
+        fw, bw = self.groups
         act = self._buf("act", (B, 32, 26, 26), torch.float32, dev)
         cut = self._buf("cut", (B, 32, 26, 26), torch.float32, dev)
-        ship = self._ship_amax(dev)
-        if ship:
+        ship = self.ship_amax
+        amx = self._buf("amax", (B,), torch.float32, dev) if ship else None
+        if ship and hasattr(c, "emit_amax"):
             c.emit_amax = True
-            amx = self._buf("amax", (B,), torch.float32, dev)
         codec = self._use_codec(dev)
         n = b * 32 * 26 * 26
+        side = self._side_stream(dev)
+        if side is not None:
+            # this step's receives land in buffers the previous step's backward read on the current stream
+            side.wait_stream(torch.cuda.current_stream(dev))
         sends, bufs, evs = [], [], []
         counts = self._buf("counts_host", (m,), torch.int32, dev, pin=True) if codec is not None else None
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             c.forward(x[sl], out=act[sl])
             if ship:
-                amx[sl].copy_(c._act_amax)
+                if getattr(c, "_act_amax", None) is not None:
+                    amx[sl].copy_(c._act_amax)
+                else:                                   # stages without a fused max (CPU protocol tests)
+                    torch.amax(act[sl].reshape(b, -1), dim=1, out=amx[sl])
             if codec is None:
-                sends += [isend(act[sl], srv, self.group), isend(y[sl], srv, self.group)]
-                if ship:
-                    sends.append(isend(amx[sl], srv, self.group))
+                sends += [isend(act[sl], srv, fw), isend(y[sl], srv, fw)] + ([isend(amx[sl], srv, fw)] if ship else [])
                 continue
             bk = codec.buffers(("c", k), n, dev)
             codec.encode(act[sl], bk)
             bufs.append(bk)
             counts[k:k + 1].copy_(bk[3], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            evs.append(ev)
+            evs.append(self._record(dev))
         totals = []
         if codec is not None:
-            side = self._side_stream(dev)
             for k in range(m):
                 sl = slice(k * b, (k + 1) * b)
-                evs[k].synchronize()          # micro-batch k's encode only: k+1.. keep computing
+                if evs[k] is not None:
+                    evs[k].synchronize()          # micro-batch k's encode only: k+1.. keep computing
+                    side.wait_event(evs[k])
                 t = int(counts[k].item())
                 totals.append(t)
-                side.wait_event(evs[k])
                 seq = [bufs[k][3], bufs[k][0], y[sl]] + ([amx[sl]] if ship else []) + ([bufs[k][4][:t]] if t else [])
-                sends += [self._p2p(isend, u, srv, side) for u in seq]
+                sends += [self._p2p(isend, u, srv, fw, side) for u in seq]
             gv = [self._buf(("gvals", k), (n,), torch.float32, dev) for k in range(m)]
-            recvs = [self._p2p(irecv, gv[k][:totals[k]], srv, side) if totals[k] else None for k in range(m)]
+            recvs = [self._p2p(irecv, gv[k][:totals[k]], srv, bw, side) if totals[k] else None for k in range(m)]
         else:
-            side = self._side_stream(dev) if dev.type == "cuda" else None
-            recvs = [self._p2p(irecv, cut[k * b:(k + 1) * b], srv, side) for k in range(m)]
+            recvs = [self._p2p(irecv, cut[k * b:(k + 1) * b], srv, bw, side) for k in range(m)]
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             if recvs[k] is not None:
@@ -416,7 +473,7 @@ class Hub:
                 codec.offsets(n, bk)
                 codec.unpack(acts[k * CH + ci * b:k * CH + (ci + 1) * b], bk)
         kw = {}
-        if self._ship_amax(device):
+        if self.ship_amax and self._amax_kw:
             kw["act_amax"] = self._buf("amax", (G,), torch.float32, device)[ch]
         _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         _loss_sum(loss_i, 1.0 / G, parts[k:k + 1])
@@ -437,7 +494,7 @@ class Hub:
         G = self.nclients * B
         self._buf("acts", (G, 32, 26, 26), torch.float32, device).zero_()
         self._buf("labels", (G,), torch.int64, device).zero_()
-        if self._ship_amax(device):
+        if self.ship_amax:
             self._buf("amax", (G,), torch.float32, device).zero_()
         n = (B // self.micro) * 32 * 26 * 26
         st = torch.cuda.Stream(device)
@@ -469,7 +526,8 @@ class Hub:
         b, G = B // m, nc * B
         CH = nc * b
         n = b * 32 * 26 * 26
-        ship = self._ship_amax(device)
+        fw, bw = self.groups
+        ship = self.ship_amax
         acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
@@ -478,14 +536,18 @@ class Hub:
         codec = self._use_codec(device)
         self._prepare(B, device, codec)
         part = lambda k, ci: slice(k * CH + ci * b, k * CH + (ci + 1) * b)  # noqa: E731
+        side = self._side_stream(device)
+        if side is not None:
+            # receives on the side stream land in buffers the previous step's chunks read
+            side.wait_stream(torch.cuda.current_stream(device))
         reqs = {}
         if codec is None:
             for ci, cr in enumerate(self.client_ranks):
                 for k in range(m):
                     sl = part(k, ci)
-                    reqs[ci, k] = [irecv(acts[sl], cr, self.group), irecv(labels[sl], cr, self.group)]
+                    reqs[ci, k] = [irecv(acts[sl], cr, fw), irecv(labels[sl], cr, fw)]
                     if ship:
-                        reqs[ci, k].append(irecv(amx[sl], cr, self.group))
+                        reqs[ci, k].append(irecv(amx[sl], cr, fw))
         else:
             pinned = self._buf("counts_host", (m * nc,), torch.int32, device, pin=True)
         totals = {}
@@ -496,21 +558,22 @@ class Hub:
                 for ci, cr in enumerate(self.client_ranks):
                     sl = part(k, ci)
                     bk = codec.buffers(("s", ci, k), n, device)
-                    t = self._recv_count(self._buf(("head", ci, k), (1,), torch.int32, device), cr, k * nc + ci, pinned)
+                    t = self._recv_count(self._buf(("head", ci, k), (1,), torch.int32, device), cr, k * nc + ci,
+                                         pinned, side)
                     totals[ci, k] = t
                     seq = [bk[0], labels[sl]] + ([amx[sl]] if ship else []) + ([bk[4][:t]] if t else [])
                     # on the side stream: the transfer need not wait for chunk k-1's compute
-                    reqs[ci, k] = [self._p2p(irecv, u, cr, self._side_stream(device)) for u in seq]
+                    reqs[ci, k] = [self._p2p(irecv, u, cr, fw, side) for u in seq]
             for ci in range(nc):
                 for r in reqs[ci, k]:
                     r.wait()
             self._run_chunk(k, B, device, codec)
             for ci, cr in enumerate(self.client_ranks):
                 if codec is None:
-                    sends.append(isend(cuts[part(k, ci)], cr, self.group))
+                    sends.append(isend(cuts[part(k, ci)], cr, bw))
                 elif totals[ci, k]:
                     gv = self._buf(("gvals", ci, k), (n,), torch.float32, device)
-                    sends.append(isend(gv[:totals[ci, k]], cr, self.group))
+                    sends.append(isend(gv[:totals[ci, k]], cr, bw))
         s.step()
         s.log_loss(parts, scale=1.0, step=self.global_step)
         for w in sends:
@@ -534,13 +597,14 @@ class Pipeline(Hub):
     `role` is "client" or "server", `peer` the other rank. Both sides accumulate their gradient over
     the micro-batches and step once per batch (= the reference step at batch B)."""
 
-    def __init__(self, stage, role: str, peer: int, micro: int = 4, group=None, compress: bool = True,
-                 graph: bool = True):
+    def __init__(self, stage, role: str, peer: int, micro: int = 4, compress=True, graph: bool = True,
+                 groups=None, ship_amax: bool = True):
         assert role in ("client", "server")
         me = dist.get_rank()
-        super().__init__(stage, me, dist.get_world_size(), None, micro, compress, group=group,
+        super().__init__(stage, me, dist.get_world_size(), None, micro, compress,
                          server_rank=peer if role == "client" else me,
-                         client_ranks=[me] if role == "client" else [peer], graph=graph)
+                         client_ranks=[me] if role == "client" else [peer], graph=graph, groups=groups,
+                         ship_amax=ship_amax)
         self.role, self.peer = role, peer
 
 
@@ -656,21 +720,25 @@ class WideHub:
     Stages: client.forward(x, tag) / backward_grads(dcut, tag, accumulate) / step_from_grads / grads /
     cut_shape / cut_dtype; server.accumulate(cut, labels, scale, b0, k, nparts, dcut) / finish_step."""
 
-    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1):
+    def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, groups=None):
         self.stage, self.rank, self.world = stage, rank, world
         self.server_rank = world - 1
         self.nclients = world - 1
         self.client_group = client_group
+        if groups is None:   # one group per direction, as for Hub (exchange_groups)
+            groups = exchange_groups() if dist.is_initialized() else (None, None)
+        self.groups = tuple(groups)
         self.micro = micro
         self.global_step = 0
         self._bufs = {}
         self.exchange_bytes = 0
 
     def _buf(self, name, shape, dtype, device):
-        t = self._bufs.get(name)
-        if t is None or tuple(t.shape) != tuple(shape) or t.device != device or t.dtype != dtype:
+        key = (name, tuple(shape), dtype, str(torch.device(device)))
+        t = self._bufs.get(key)
+        if t is None:
             t = torch.empty(shape, dtype=dtype, device=device)
-            self._bufs[name] = t
+            self._bufs[key] = t
         return t
 
     def client_step(self, x, y):
@@ -679,14 +747,15 @@ class WideHub:
         assert B % m == 0, "batch must be divisible by the micro-batch count"
         b = B // m
         dcut = self._buf("dcut", c.cut_shape(B), c.cut_dtype, x.device)
+        fw, bw = self.groups
         sends, recvs = [], []
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
             cut = c.forward(x[sl], tag=k)
-            sends.append(isend(cut, self.server_rank))
-            sends.append(isend(y[sl], self.server_rank))
+            sends.append(isend(cut, self.server_rank, fw))
+            sends.append(isend(y[sl], self.server_rank, fw))
         for k in range(m):
-            recvs.append(irecv(dcut[k * b:(k + 1) * b], self.server_rank))
+            recvs.append(irecv(dcut[k * b:(k + 1) * b], self.server_rank, bw))
         for k in range(m):
             recvs[k].wait()
             c.backward_grads(dcut[k * b:(k + 1) * b], tag=k, accumulate=k > 0)
@@ -706,11 +775,12 @@ class WideHub:
         cuts = self._buf("cuts", cut_shape(G), cut_dtype, device)
         dcuts = self._buf("dcuts", cut_shape(G), cut_dtype, device)
         labels = self._buf("labels", (G,), torch.int64, device)
+        fw, bw = self.groups
         reqs = {}
         for c in range(nc):
             for k in range(m):
                 sl = slice(c * B + k * b, c * B + (k + 1) * b)
-                reqs[c, k] = (irecv(cuts[sl], c), irecv(labels[sl], c))
+                reqs[c, k] = (irecv(cuts[sl], c, fw), irecv(labels[sl], c, fw))
         sends, part = [], 0
         for k in range(m):
             for c in range(nc):
@@ -718,7 +788,7 @@ class WideHub:
                 for r in reqs[c, k]:
                     r.wait()
                 s.accumulate(cuts[sl], labels[sl], 1.0 / G, c * B + k * b, part, m * nc, dcut=dcuts[sl])
-                sends.append(isend(dcuts[sl], c))
+                sends.append(isend(dcuts[sl], c, bw))
                 part += 1
         s.finish_step(m * nc, step=self.global_step)
         for w in sends:

@@ -76,12 +76,12 @@ def _worker(rank, world, port, topo, outdir):
         elif topo == "pipeline":
             batches = _batches(B)
             if rank == 0:
-                t = sd.Pipeline(OracleClient(P), "client", 1, micro=2)
+                t = sd.Pipeline(OracleClient(P), "client", 1, micro=2, compress=False)
                 for x, y in batches:
                     t.client_step(x, y)
                 res = t.stage.named()
             else:
-                t = sd.Pipeline(OracleServer(P), "server", 0, micro=2)
+                t = sd.Pipeline(OracleServer(P), "server", 0, micro=2, compress=False)
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"))
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
@@ -103,13 +103,13 @@ def _worker(rank, world, port, topo, outdir):
             grp = sd.client_group_for(world)
             micro = 2 if topo == "hub_m2" else 1
             if rank < world - 1:
-                t = sd.Hub(OracleClient(P), rank, world, client_group=grp, micro=micro)
+                t = sd.Hub(OracleClient(P), rank, world, client_group=grp, micro=micro, compress=False)
                 for x, y in batches:
                     sl = slice(rank * B, (rank + 1) * B)
                     t.client_step(x[sl].contiguous(), y[sl].contiguous())
                 res = t.stage.named()
             else:
-                t = sd.Hub(OracleServer(P), rank, world, client_group=grp, micro=micro)
+                t = sd.Hub(OracleServer(P), rank, world, client_group=grp, micro=micro, compress=False)
                 for _ in batches:
                     t.server_step(B, torch.device("cpu"))
                 res = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}

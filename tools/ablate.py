@@ -1,5 +1,5 @@
-"""Profiling-only: time the conv2 kernels of several libslk builds (e.g. -DSLK_ABL=1/2/4 ablations,
-or alternative kernels) side by side in ONE process, interleaved rounds, HIP events on one stream.
+"""Profiling-only: time the conv2 kernels of several libslk builds (tuning-knob variants from
+tools/build_variant.sh, or older trees) side by side in ONE process, interleaved rounds, HIP events on one stream.
 usage: python tools/ablate.py lib0.so lib1.so ... [--batch 4096 --rounds 5]"""
 import argparse
 import ctypes

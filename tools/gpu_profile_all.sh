@@ -16,6 +16,8 @@ rc=$?; echo "bench k5 rc=$rc"; stop_if_fatal $rc bench_k5
 for cfg in k2 k5; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-pass > gpurun_out/prof_$cfg.log 2>&1
   rc=$?; echo "rocprof $cfg rc=$rc"; stop_if_fatal $rc rocprof
+  # the library build this profile belongs to (bench.py reports rocprof_avg_ms only for a matching build)
+  python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_$cfg.build_id
   OUT=gpurun_out/pmc_$cfg KARGS="--config $cfg --steps 3" bash tools/pmc.sh || exit $?
   python tools/pmc_summary.py --dir gpurun_out/pmc_$cfg --out gpurun_out/pmc_${cfg}_summary.json > /dev/null
 done
