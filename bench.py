@@ -320,6 +320,47 @@ def run_single(args, out):
     out["step_direct_equivalent_tflops"] = round(out["value"] * FLOP_PER_SAMPLE / 1e12, 2)
 
 
+def run_dropin(X, Y, steps, warmup):
+    """The reference's own step code (src/client_part.py:112-133 <-> src/server_part.py:45-57, HTTP and
+    pickle removed) on the drop-in modules (splitcnn.model_def: torch.library ops over the x3 kernels,
+    library.py) at the K2 batch: eager autograd + torch.optim.SGD, the payload clone, the server's
+    .grad clone and the per-step loss.item() of its log_metric call (server_part.py:55)."""
+    import torch
+
+    from splitcnn.data import init_models
+    from splitcnn.library import conv_impls
+    from splitcnn.model_def import CrossEntropyLoss
+    dev = X.device
+    client, server = (m.to(dev) for m in init_models(seed=0))
+    copt = torch.optim.SGD(client.parameters(), lr=0.01)
+    sopt = torch.optim.SGD(server.parameters(), lr=0.01)
+    criterion = CrossEntropyLoss()
+    losses = []
+
+    def step(i):
+        data, target = X[i % 4], Y[i % 4]
+        copt.zero_grad()
+        activations = client(data)
+        client_activations = activations.clone().detach()       # the payload (client_part.py:118)
+        client_activations.requires_grad_(True)                  # server_part.py:45
+        sopt.zero_grad()
+        loss = criterion(server(client_activations), target)
+        loss.backward()
+        sopt.step()
+        losses.append(loss.item())                               # mlflow.log_metric (server_part.py:55)
+        cut_layer_gradient = client_activations.grad.clone().detach()
+        activations.backward(cut_layer_gradient)                 # client_part.py:132-133
+        copt.step()
+    dt = timed(step, steps, warmup, dev)
+    B = X.shape[1]
+    return {"workload": "the reference's step code (client_part.py:112-133 / server_part.py:45-57, no HTTP) on "
+                        "the drop-in ModelPartA/ModelPartB/CrossEntropyLoss modules, eager autograd + "
+                        "torch.optim.SGD, loss.item() per step", "conv2_kernels": dict(zip(("fwd_pool", "dgrad", "wgrad"),
+                                                                                          conv_impls())),
+            "samples_per_s": round(steps * B / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3), "batch": B,
+            "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)]}
+
+
 def run_hub_loopback(args, nc=7):
     """K4's bottleneck measured on ONE GPU: the hub server's step for nc clients x B samples (the chunked,
     graph-captured sequence dist.Hub.server_step runs: per micro-batch chunk of nc*B/m samples codec
@@ -688,6 +729,13 @@ def main():
                     if k in ("samples_per_s", "ms_per_step", "ratio")}
             except Exception as e:  # the headline stands on its own
                 out.setdefault("k4_server_loopback", {})["error"] = repr(e)[:300]
+        try:
+            import torch
+            X, Y = make_pool(args.batch, 4, torch.device("cuda:0"))
+            out["dropin_modules"] = run_dropin(X, Y, max(5, min(args.steps, 20)), 3)
+            del X, Y
+        except Exception as e:  # the headline stands on its own
+            out["dropin_modules"] = {"error": repr(e)[:300]}
         if not args.no_k5:
             try:
                 out["widened"] = run_wide(args, args.k5_batch, max(5, min(args.steps, 20)), 3,

@@ -10,14 +10,15 @@ otherwise); there is no CPU implementation.
 
 The ops and the reference calls they replace (src/model_def.py, src/server_part.py):
   conv1_relu(x, W1, b1) -> act                              ModelPartA.forward (model_def.py:11-12)
-  conv2_relu_pool(act, W2, b2) -> (pooled, code)            model_def.py:25-26
+  conv2_relu_pool(act, W2, b2) -> (pooled, code, amax, act16) model_def.py:25-26 (x3 kernels by default)
   linear(flat, W3, b3) -> logits                            fc1 (model_def.py:22,28)
   cross_entropy(logits, labels) -> loss                     nn.CrossEntropyLoss() (server_part.py:16,49)
-and their backward helpers conv1_wgrad, conv2_dgrad, conv2_wgrad, linear_dgrad, linear_wgrad,
-cross_entropy_grad.
+and their backward helpers conv1_wgrad, row_amax, conv2_dgrad(_x3), conv2_wgrad(_x3), linear_dgrad,
+linear_wgrad, cross_entropy_grad.
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -69,20 +70,62 @@ conv1_relu.register_autograd(_conv1_backward, setup_context=_conv1_setup)
 
 
 # ----------------------------------------------------------------------------------- conv2 + ReLU + pool
+# conv2 kernels of the drop-in modules: the engine's presets (engine.CONV_PRESETS), default "x3" — the f16
+# MFMA with hi/lo-split fp32 operands for the forward, dgrad and wgrad, as in the fused trainer; "x3w"
+# keeps the Winograd f32 wgrad, "f32" is Winograd on the f32 MFMA throughout. SLK_CONV selects.
+_PRESETS = {"f32": ("wino", "wino", "wino"), "x3": ("x3", "x3", "x3"), "x3w": ("x3", "x3", "wino")}
+
+
+def conv_impls() -> Tuple[str, str, str]:
+    """(forward, dgrad, wgrad) kernels the conv2 ops run, from SLK_CONV (default "x3")."""
+    p = os.environ.get("SLK_CONV", "x3")
+    if p not in _PRESETS:
+        raise ValueError(f"SLK_CONV must be one of {sorted(_PRESETS)}, got {p!r}")
+    return _PRESETS[p]
+
+
+@torch.library.custom_op(f"{_NS}::row_amax", mutates_args=())
+def row_amax(x: Tensor) -> Tensor:
+    """Per-row max |x| (the x3 kernels' per-sample operand scales)."""
+    return ops.row_amax(x.contiguous())
+
+
+@row_amax.register_fake
+def _(x):
+    return x.new_empty((x.shape[0],))
+
+
 @torch.library.custom_op(f"{_NS}::conv2_relu_pool", mutates_args=())
-def conv2_relu_pool(act: Tensor, W2: Tensor, b2: Tensor) -> Tuple[Tensor, Tensor]:
-    return ops.conv2_fwd_pool(act.contiguous(), W2.contiguous(), b2.contiguous())
+def conv2_relu_pool(act: Tensor, W2: Tensor, b2: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """(pooled, code, act_amax, act16). With the x3 forward, act_amax = the per-sample max |act| (the
+    kernels' scales; the received cut carries none, src/server_part.py:39-45) and, when the wgrad is x3
+    too, act16 = the split input images the forward writes for it (the backward then saves these, not
+    act). Otherwise both are empty."""
+    fi, _di, wi = conv_impls()
+    act = act.contiguous()
+    B = act.shape[0]
+    if fi != "x3":
+        pooled, code = ops.conv2_fwd_pool(act, W2.contiguous(), b2.contiguous(), impl=fi)
+        return pooled, code, act.new_empty((0,)), act.new_empty((0,), dtype=torch.uint8)
+    amax = ops.row_amax(act)
+    a16 = act.new_empty((ops.conv2_act16_bytes(B) if wi == "x3" else 0,), dtype=torch.uint8)
+    pooled, code = ops.conv2_fwd_pool(act, W2.contiguous(), b2.contiguous(), impl="x3", act_amax=amax,
+                                      act16=a16 if wi == "x3" else None)
+    return pooled, code, amax, a16
 
 
 @conv2_relu_pool.register_fake
 def _(act, W2, b2):
+    fi, _di, wi = conv_impls()
     B = act.shape[0]
-    return act.new_empty((B, 64, 12, 12)), act.new_empty((B, 64, 12, 12), dtype=torch.uint8)
+    n16 = ops.conv2_act16_bytes(B) if (fi, wi) == ("x3", "x3") else 0
+    return (act.new_empty((B, 64, 12, 12)), act.new_empty((B, 64, 12, 12), dtype=torch.uint8),
+            act.new_empty((B if fi == "x3" else 0,)), act.new_empty((n16,), dtype=torch.uint8))
 
 
 @torch.library.custom_op(f"{_NS}::conv2_dgrad", mutates_args=())
 def conv2_dgrad(dpooled: Tensor, code: Tensor, W2: Tensor) -> Tensor:
-    """Cut gradient: conv2 input gradient of the pool/ReLU-routed dpooled."""
+    """Cut gradient: conv2 input gradient of the pool/ReLU-routed dpooled (Winograd f32)."""
     return ops.conv2_dgrad(dpooled.contiguous(), code.contiguous(), W2.contiguous())
 
 
@@ -91,9 +134,20 @@ def _(dpooled, code, W2):
     return dpooled.new_empty((dpooled.shape[0], 32, 26, 26))
 
 
+@torch.library.custom_op(f"{_NS}::conv2_dgrad_x3", mutates_args=())
+def conv2_dgrad_x3(dpooled: Tensor, code: Tensor, W2: Tensor, dp_amax: Tensor) -> Tensor:
+    """Cut gradient on the x3 kernel (dp_amax = per-sample max |dpooled|)."""
+    return ops.conv2_dgrad(dpooled.contiguous(), code.contiguous(), W2.contiguous(), impl="x3", dp_amax=dp_amax)
+
+
+@conv2_dgrad_x3.register_fake
+def _(dpooled, code, W2, dp_amax):
+    return dpooled.new_empty((dpooled.shape[0], 32, 26, 26))
+
+
 @torch.library.custom_op(f"{_NS}::conv2_wgrad", mutates_args=())
 def conv2_wgrad(act: Tensor, dpooled: Tensor, code: Tensor) -> Tensor:
-    """[dW2 (18432) | db2 (64)]."""
+    """[dW2 (18432) | db2 (64)] (Winograd f32)."""
     return ops.reduce_slabs(ops.conv2_wgrad_slabs(act.contiguous(), dpooled.contiguous(), code.contiguous()))
 
 
@@ -102,19 +156,40 @@ def _(act, dpooled, code):
     return act.new_empty((ops.CONV2_SLAB,))
 
 
+@torch.library.custom_op(f"{_NS}::conv2_wgrad_x3", mutates_args=())
+def conv2_wgrad_x3(act16: Tensor, act_amax: Tensor, dpooled: Tensor, dp_amax: Tensor, code: Tensor) -> Tensor:
+    """[dW2 | db2] on the x3 kernel from the forward's split input images (act itself is not needed)."""
+    return ops.reduce_slabs(ops.conv2_wgrad_slabs(None, dpooled.contiguous(), code.contiguous(), impl="x3",
+                                                  act_amax=act_amax, dp_amax=dp_amax, act16=act16))
+
+
+@conv2_wgrad_x3.register_fake
+def _(act16, act_amax, dpooled, dp_amax, code):
+    return dpooled.new_empty((ops.CONV2_SLAB,))
+
+
 def _conv2_setup(ctx, inputs, output):
     act, W2, _b2 = inputs
-    _pooled, code = output
-    ctx.save_for_backward(act, code, W2)
-    ctx.mark_non_differentiable(code)
+    _pooled, code, amax, a16 = output
+    ctx.impls = conv_impls()
+    # the x3 wgrad reads the forward's split images: keep those (same size as act), not act
+    keep = (a16, amax) if ctx.impls[2] == "x3" else (act,)
+    ctx.save_for_backward(code, W2, *keep)
+    ctx.mark_non_differentiable(code, amax, a16)
 
 
-def _conv2_backward(ctx, dpooled, _dcode):
-    act, code, W2 = ctx.saved_tensors
-    gact = torch.ops.splitcnn.conv2_dgrad(dpooled, code, W2) if ctx.needs_input_grad[0] else None
+def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16):
+    code, W2, *kept = ctx.saved_tensors
+    _fi, di, wi = ctx.impls
+    dpa = torch.ops.splitcnn.row_amax(dpooled) if "x3" in (di, wi) else None
+    gact = None
+    if ctx.needs_input_grad[0]:
+        gact = (torch.ops.splitcnn.conv2_dgrad_x3(dpooled, code, W2, dpa) if di == "x3"
+                else torch.ops.splitcnn.conv2_dgrad(dpooled, code, W2))
     dW2 = db2 = None
     if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-        flat = torch.ops.splitcnn.conv2_wgrad(act, dpooled, code)
+        flat = (torch.ops.splitcnn.conv2_wgrad_x3(kept[0], kept[1], dpooled, dpa, code) if wi == "x3"
+                else torch.ops.splitcnn.conv2_wgrad(kept[0], dpooled, code))
         dW2, db2 = flat[:18432].view(64, 32, 3, 3), flat[18432:].view(64)
     return gact, dW2, db2
 

@@ -67,7 +67,7 @@ class ModelPartB(nn.Module):
 
     def forward(self, x):
         _require_device(x, "ModelPartB")
-        pooled, _code = _OPS.conv2_relu_pool(x, self.conv2.weight, self.conv2.bias)
+        pooled = _OPS.conv2_relu_pool(x, self.conv2.weight, self.conv2.bias)[0]
         return _OPS.linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
 
 
@@ -86,7 +86,7 @@ class FullModel(nn.Module):
     def forward(self, x):
         _require_device(x, "FullModel")
         act = _OPS.conv1_relu(x, self.conv1.weight, self.conv1.bias)
-        pooled, _code = _OPS.conv2_relu_pool(act, self.conv2.weight, self.conv2.bias)
+        pooled = _OPS.conv2_relu_pool(act, self.conv2.weight, self.conv2.bias)[0]
         return _OPS.linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
 
 

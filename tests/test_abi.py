@@ -158,7 +158,8 @@ def test_custom_op_fake_kernels_shapes():
     with FakeTensorMode():
         x = torch.empty(3, 1, 28, 28, device="cuda")
         act = O.conv1_relu(x, torch.empty(32, 1, 3, 3, device="cuda"), torch.empty(32, device="cuda"))
-        pooled, code = O.conv2_relu_pool(act, torch.empty(64, 32, 3, 3, device="cuda"), torch.empty(64, device="cuda"))
+        pooled, code, amax, a16 = O.conv2_relu_pool(act, torch.empty(64, 32, 3, 3, device="cuda"),
+                                                     torch.empty(64, device="cuda"))
         flat = pooled.view(3, 9216)
         logits = O.linear(flat, torch.empty(10, 9216, device="cuda"), torch.empty(10, device="cuda"))
         y = torch.zeros(3, dtype=torch.int64, device="cuda")
@@ -166,13 +167,17 @@ def test_custom_op_fake_kernels_shapes():
                "loss": O.cross_entropy(logits, y), "dlogits": O.cross_entropy_grad(logits, y, logits.new_ones(())),
                "dflat": O.linear_dgrad(logits, torch.empty(10, 9216, device="cuda")),
                "g3": O.linear_wgrad(logits, flat), "cut": O.conv2_dgrad(pooled, code, torch.empty(64, 32, 3, 3, device="cuda")),
-               "g2": O.conv2_wgrad(act, pooled, code), "g1": O.conv1_wgrad(x, act, act)}
+               "g2": O.conv2_wgrad(act, pooled, code), "g1": O.conv1_wgrad(x, act, act),
+               "amax": amax, "a16": a16, "dpa": O.row_amax(pooled),
+               "cut_x3": O.conv2_dgrad_x3(pooled, code, torch.empty(64, 32, 3, 3, device="cuda"), amax),
+               "g2_x3": O.conv2_wgrad_x3(a16, amax, pooled, amax, code)}
     want = {"act": (3, 32, 26, 26), "pooled": (3, 64, 12, 12), "code": (3, 64, 12, 12), "logits": (3, 10),
             "loss": (), "dlogits": (3, 10), "dflat": (3, 9216), "g3": (92170,), "cut": (3, 32, 26, 26),
-            "g2": (18496,), "g1": (320,)}
+            "g2": (18496,), "g1": (320,), "amax": (3,), "a16": (3 * 86528,), "dpa": (3,), "cut_x3": (3, 32, 26, 26),
+            "g2_x3": (18496,)}
     for k, shp in want.items():
         assert tuple(got[k].shape) == shp, k
-        assert got[k].dtype == (torch.uint8 if k == "code" else torch.float32), k
+        assert got[k].dtype == (torch.uint8 if k in ("code", "a16") else torch.float32), k
 
 
 def test_fused_step_preconditions_without_gpu():

@@ -438,3 +438,54 @@ def test_replicated_fused_world1_rccl_bitwise_vs_split_trainer(gpu, graph):
         assert tr.loss_log.flush() == rep.server.loss_log.flush()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("codec", [False, True])
+def test_hub_server_graphs_survive_batch_size_changes(gpu, codec):
+    """the hub server's chunk graphs are captured per (chunk, B); after a step at
+    another B they must still read the buffers the receives fill. B = 8 -> 4 -> 8 -> 4 with graphs
+    must equal the eager server bit for bit (parameters and every cut gradient)."""
+    from splitcnn import dist as sd
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    nc, m = 2, 2
+
+    def make(graph):
+        a, b = init_models(seed=0)
+        return (sd.Hub(ServerStage(b, device=gpu), rank=nc, world=nc + 1, micro=m, compress=codec, graph=graph),
+                ClientStage(a, device=gpu))
+    runs = [make(True), make(False)]
+    data = SyntheticMNIST(3)
+    for B in (8, 4, 8, 4):
+        b = B // m
+        n = b * 32 * 26 * 26
+        parts = [data.batch(b) for _ in range(m * nc)]
+        cuts = []
+        for hub, cl in runs:
+            cl.emit_amax = True
+            cdc = hub._use_codec(gpu)
+            hub._prepare(B, gpu, cdc)      # (captures at a new B; zeroes the receive buffers)
+            G = nc * B
+            acts = hub._buf("acts", (G, 32, 26, 26), torch.float32, gpu)
+            labels = hub._buf("labels", (G,), torch.int64, gpu)
+            amx = hub._buf("amax", (G,), torch.float32, gpu)
+            hub._buf("cuts", (G, 32, 26, 26), torch.float32, gpu)
+            hub._buf("loss_parts", (m,), torch.float32, gpu)
+            for k in range(m):
+                for ci in range(nc):
+                    sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
+                    x, y = parts[k * nc + ci]
+                    cl.forward(x.to(gpu), out=acts[sl])     # what the receives would deliver
+                    amx[sl].copy_(cl._act_amax)
+                    labels[sl].copy_(y.to(gpu))
+                    if cdc is not None:
+                        cdc.encode(acts[sl], cdc.buffers(("s", ci, k), n, gpu))
+            for k in range(m):
+                hub._run_chunk(k, B, gpu, cdc)
+            hub.stage.step()
+            torch.cuda.synchronize()
+            cuts.append(hub.cuts_by_client(B).clone() if cdc is None else
+                        torch.cat([hub._buf(("gvals", ci, k), (n,), torch.float32, gpu).clone()
+                                   for k in range(m) for ci in range(nc)]))
+        torch.testing.assert_close(cuts[0], cuts[1], rtol=0, atol=0)
+        torch.testing.assert_close(runs[0][0].stage.params, runs[1][0].stage.params, rtol=0, atol=0)

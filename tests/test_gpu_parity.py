@@ -378,7 +378,7 @@ def test_traced_step_runs_the_custom_ops(gpu):
     gm = make_fx(step, tracing_mode="fake")(x, y, *params)
     targets = {str(n.target) for n in gm.graph.nodes if n.op == "call_function"}
     for op in ("conv1_relu", "conv2_relu_pool", "linear", "cross_entropy", "cross_entropy_grad", "linear_dgrad",
-               "linear_wgrad", "conv2_dgrad", "conv2_wgrad", "conv1_wgrad"):
+               "linear_wgrad", "row_amax", "conv2_dgrad_x3", "conv2_wgrad_x3", "conv1_wgrad"):
         assert f"splitcnn.{op}.default" in targets, op
     assert not any("convolution" in t or "addmm" in t or "nll_loss" in t for t in targets)
     got = gm(x, y, *params)
