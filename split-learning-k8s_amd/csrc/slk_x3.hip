@@ -492,6 +492,9 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     // C1W: each wave's conv1-gradient accumulator D1[ci 16 nt + 4 (lane >> 4) + r][col lane & 15] (col =
     // tap 0-8, 9 = bias), kept here between epilogues (not in the MFMA loop's registers)
     __shared__ __attribute__((aligned(16))) f32x4 d1s[C1W ? X3D_THREADS : 1];
+    // C1W: an x-shaped plane of 1.0 that the bias column's lanes (col 9) read in place of x, so the B
+    // operand needs no per-element select (cols 10-15 read x: their D1 columns are never stored)
+    __shared__ __attribute__((aligned(16))) float ones[C1W ? IN_HW * IN_HW : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
@@ -624,6 +627,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     };
     if constexpr (C1W) {
         d1s[tid] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int e = tid; e < IN_HW * IN_HW; e += X3D_THREADS) ones[e] = 1.f;
         if (pr < p1) issue_xb(pr, 0);
     }
     if (pr < p1) {
@@ -635,41 +639,55 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     int k = 0, q = 0;
     // C1W epilogue of one pair: client ReLU backward + conv1 wgrad (the cut gradient g is the value the
     // C1W = false store would write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels
-    // 16 t + 4 kc + r
+    // 16 t + 4 kc + r. All of the pair's x / bit-map reads are issued first; the ReLU mask is an integer
+    // AND of the accumulator bits (no compare/select/multiply per element); the 16 MFMAs run as 4
+    // independent chains (one per r; one dependent chain exposed the MFMA latency 16 times) started
+    // from zero per pair, and the per-sample unscale 2^-s_b is applied once to their sum (exact: a power
+    // of two), which is then added to the wave's launch-long accumulator.
     auto c1w_epi = [&](int T0e, int T1e, float us1e, int qe) {
         const int ci = 16 * nt + n16;
-        const float* xs = reinterpret_cast<const float*>(xbm[qe & 1]);
+        // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff;
+        // the bias col 9 reads the ones plane; cols 10-15 read x (their D1 columns are never stored)
+        const float* xs = n16 == 9 ? ones : reinterpret_cast<const float*>(xbm[qe & 1]);
         const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbm[qe & 1] + XB_X);
-        f32x4 d1 = d1s[tid];
-        // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff
-        // (every lane reads a valid pixel; cols 10-15 and the bias col 9 select their constant after)
         const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
-        const float bsel = n16 == 9 ? 1.f : 0.f;
-        // a tile's reads first (unconditional, clamped), then its 4 MFMAs: no exec-masked block between
-        // each read and its MFMA (which exposed every ds_read's latency, all eight waves at once)
+        const bool t3 = T0e + g + 12 < T1e;  // wave-uniform: tiles 0-2 exist for every wave and part
+        uint32_t mw[X3D_MPW];
+        float xv[X3D_MPW][4];
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) {
             const int t = T0e + g + 4 * i;
-            if (i < 3 || t < T1e) {  // wave-uniform (tiles 0-2 exist for every wave and part)
-                const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
-                const uint32_t mraw = bs[(ci >> 3) * (A_PIX / 4) + min(tq, A_PIX / 4 - 1)];
-                float xv[4];
+            const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
+            // pixels past 675 (tile 42's tail) and a missing tile 3: clamped reads, mask 0 below
+            const int p0 = min(16 * t + 4 * kc, A_PIX - 4);
+            const int q0 = p0 / A_HW, rem = p0 - A_HW * q0;
+            const int base = p0 + 2 * q0 + toff;  // x index of pixel p: p + 2 (p / 26)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xv[i][r] = xs[base + r + 2 * ((rem + r + 6) >> 5)];  // +2 past a row end
+            const uint32_t mraw = bs[(ci >> 3) * (A_PIX / 4) + min(tq, A_PIX / 4 - 1)];
+            mw[i] = (tq < A_PIX / 4 && (i < 3 || t3)) ? mraw >> (4 * (ci & 7)) : 0u;
+        }
+        f32x4 dr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+            slk_keep(dr[r]);  // zero chains in VGPRs, not an inline-constant C
+        }
+#pragma unroll
+        for (int i = 0; i < X3D_MPW; ++i) {
+            if (i < 3 || t3) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int p = min(16 * t + 4 * kc + r, A_PIX - 1);
-                    xv[r] = xs[p + 2 * (p / A_HW) + toff];
-                }
-                // (pixels past 675: no conv1 thread, mask 0, so A = 0 there)
-                const uint32_t mw = tq < A_PIX / 4 ? mraw >> (4 * (ci & 7)) : 0u;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    // g * 2^sw: the weight scale's 2^-sw is applied once to the slab (exact either way)
-                    const float gm = ((mw >> r) & 1u) ? acc[i][r] * us1e : 0.f;
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, n16 < 9 ? xv[r] : bsel, d1, 0, 0, 0);
+                    // g * 2^(s_b + sw) where the client's ReLU passes, +0 elsewhere (AND with 0 / ~0)
+                    const uint32_t keep = 0u - ((mw[i] >> r) & 1u);
+                    // (by value: __builtin_bit_cast of the vector element acc[i][r] read one element for all r)
+                    const float gm = __uint_as_float(__float_as_uint(acc[i][r]) & keep);
+                    dr[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, xv[i][r], dr[r], 0, 0, 0);
                 }
             }
         }
-        d1s[tid] = d1;
+        // the weight scale's 2^-sw is applied once to the slab (exact either way)
+        d1s[tid] = d1s[tid] + ((dr[0] + dr[1]) + (dr[2] + dr[3])) * us1e;
     };
 #pragma unroll 1
     for (; pr < p1; ++pr) {

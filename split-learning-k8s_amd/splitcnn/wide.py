@@ -560,6 +560,7 @@ class WideTrainer:
         self.server = WideServerStage(server, self.device, seed=seed)
         self.graph = graph
         self._graphs = {}
+        self.graph_inputs = 4   # caller input buffers captured directly (as engine.SplitTrainer)
         self.global_step = 0
 
     @property
@@ -575,12 +576,15 @@ class WideTrainer:
         c, s = self.client, self.server
         return [c.params, c.m, c.v, c.step_ctr, s.params, s.m, s.v, s.step_ctr, s.loss_log.counter]
 
-    def _graph_for(self, B):
-        g = self._graphs.get(B)
+    def _graph_for(self, B, x=None, y=None):
+        """The step's graph on the static inputs, or (x, y given) on those caller buffers."""
+        key = B if x is None else (B, x.data_ptr(), y.data_ptr())
+        g = self._graphs.get(key)
         if g is not None:
             return g
-        x = torch.zeros((B, 3, 32, 32), dtype=_F32, device=self.device)
-        y = torch.zeros((B,), dtype=torch.int64, device=self.device)
+        if x is None:
+            x = torch.zeros((B, 3, 32, 32), dtype=_F32, device=self.device)
+            y = torch.zeros((B,), dtype=torch.int64, device=self.device)
         saved = [t.clone() for t in self._state()]
         st = torch.cuda.Stream(self.device)
         st.wait_stream(torch.cuda.current_stream(self.device))
@@ -595,8 +599,13 @@ class WideTrainer:
         self.client.refresh_shadows()
         self.server.refresh_shadows()
         g = {"graph": graph, "x": x, "y": y}
-        self._graphs[B] = g
+        self._graphs[key] = g
         return g
+
+    def _own_buffers_ok(self, x, y) -> bool:
+        return (x.device == self.device and y.device == self.device and x.dtype == _F32 and y.dtype == torch.int64
+                and x.is_contiguous() and y.is_contiguous() and tuple(x.shape[1:]) == (3, 32, 32)
+                and y.shape == (x.shape[0],))
 
     def static_inputs(self, B):
         g = self._graph_for(B)
@@ -605,6 +614,16 @@ class WideTrainer:
     def step(self, x, y):
         B = x.shape[0]
         if self.graph:
+            key = (B, x.data_ptr(), y.data_ptr())
+            g = self._graphs.get(key)
+            if g is None and self._own_buffers_ok(x, y) and \
+                    sum(1 for k in self._graphs if isinstance(k, tuple) and k[0] == B) < self.graph_inputs:
+                g = self._graph_for(B, x, y)
+            if g is not None and self._own_buffers_ok(x, y):
+                g["graph"].replay()
+                self.server.loss_log.note_step(self.global_step)
+                self.global_step += 1
+                return
             g = self._graph_for(B)
             if x.data_ptr() != g["x"].data_ptr():
                 g["x"].copy_(x, non_blocking=True)

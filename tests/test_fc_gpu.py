@@ -61,3 +61,4 @@ def test_fc_xent_bad_label_sets_flag(gpu):
     assert int(flag.item()) == 1
     assert torch.isnan(loss_i[17]) and torch.isnan(dlogits[17]).all()
     assert torch.isfinite(loss_i[:17]).all() and torch.isfinite(loss_i[18:]).all()
+

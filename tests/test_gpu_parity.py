@@ -385,3 +385,30 @@ def test_traced_step_runs_the_custom_ops(gpu):
     want = step(x, y, *params)
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+def test_graphs_on_caller_buffers_bitwise_vs_static_inputs(gpu):
+    """SplitTrainer replays graphs captured on the caller's own input buffers (a loader's ring; no copy
+    into the static inputs) for up to `graph_inputs` buffer pairs per batch size, and falls back to the
+    static inputs for others (here: a fresh tensor every step past the ring): all bit-identical to a
+    trainer that always copies into the static inputs."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    data = SyntheticMNIST(12)
+    B = 96
+    xs, ys = zip(*(data.batch(B) for _ in range(3)))
+    X, Y = torch.stack(xs).to(gpu), torch.stack(ys).to(gpu)
+    own = SplitTrainer(*init_models(seed=5), device=gpu, graph=True, graph_inputs=2)
+    cpy = SplitTrainer(*init_models(seed=5), device=gpu, graph=True, graph_inputs=0)
+    for i in range(9):
+        x, y = X[i % 3], Y[i % 3]          # buffers 0, 1 captured; buffer 2 goes through the copy
+        if i >= 6:
+            x, y = x.clone(), y.clone()    # fresh tensors
+        own.step(x, y)
+        cpy.step(x, y)
+    torch.cuda.synchronize()
+    assert sum(1 for k in own._graphs if isinstance(k, tuple)) == 2
+    assert not any(isinstance(k, tuple) for k in cpy._graphs)
+    assert torch.equal(own.client.params, cpy.client.params)
+    assert torch.equal(own.server.params, cpy.server.params)
+    assert [l for _, l in own.loss_log.flush()] == [l for _, l in cpy.loss_log.flush()]
