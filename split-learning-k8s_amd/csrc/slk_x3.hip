@@ -654,18 +654,33 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         const bool t3 = T0e + g + 12 < T1e;  // wave-uniform: tiles 0-2 exist for every wave and part
         uint32_t mw[X3D_MPW];
         float xv[X3D_MPW][4];
+        // x index of pixel p = 26 y + x is p + 2 y. The lane's 4-pixel group of tile i starts at
+        // p0 = 16 (T0e + g) + 4 kc + 64 i; p0 % 26 (rem) is even, so the group crosses a row end only when
+        // rem == 24, between r = 1 and r = 2: two bases per tile, immediate offsets for r, and (y, rem)
+        // advanced per tile (+64 = 2 rows + 12) instead of a division per pixel
+        const float* xl = xs + toff;
+        int p0 = 16 * (T0e + g) + 4 * kc;
+        int y0 = p0 / A_HW, rem = p0 - A_HW * y0;
 #pragma unroll
         for (int i = 0; i < X3D_MPW; ++i) {
-            const int t = T0e + g + 4 * i;
-            const int tq = 4 * t + kc;  // conv1_fwd_x3's thread of these 4 pixels
-            // pixels past 675 (tile 42's tail) and a missing tile 3: clamped reads, mask 0 below
-            const int p0 = min(16 * t + 4 * kc, A_PIX - 4);
-            const int q0 = p0 / A_HW, rem = p0 - A_HW * q0;
-            const int base = p0 + 2 * q0 + toff;  // x index of pixel p: p + 2 (p / 26)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) xv[i][r] = xs[base + r + 2 * ((rem + r + 6) >> 5)];  // +2 past a row end
+            const int tq = (p0 >> 2);  // conv1_fwd_x3's thread of these 4 pixels (= 4 t + kc)
+            // pixels past 675 (tile 42's tail) and a missing tile 3: any valid pixel, mask 0 below
+            const bool ok = tq < A_PIX / 4;
+            const int base = ok ? p0 + 2 * y0 : 0;
+            const int cross = (ok && rem == 24) ? 2 : 0;
+            xv[i][0] = xl[base];
+            xv[i][1] = xl[base + 1];
+            xv[i][2] = xl[base + cross + 2];
+            xv[i][3] = xl[base + cross + 3];
             const uint32_t mraw = bs[(ci >> 3) * (A_PIX / 4) + min(tq, A_PIX / 4 - 1)];
-            mw[i] = (tq < A_PIX / 4 && (i < 3 || t3)) ? mraw >> (4 * (ci & 7)) : 0u;
+            mw[i] = (ok && (i < 3 || t3)) ? mraw >> (4 * (ci & 7)) : 0u;
+            p0 += 64;
+            rem += 12;
+            y0 += 2;
+            if (rem >= A_HW) {
+                rem -= A_HW;
+                ++y0;
+            }
         }
         f32x4 dr[4];
 #pragma unroll
