@@ -123,7 +123,7 @@ constexpr int X3F_WPIECES = (X3F_PIECES16 / 64 + 1 + X3F_WAVES - 1) / X3F_WAVES;
 constexpr int X3F_ITEMS = X3F_PIX * 4;            // (pixel, 8-ci chunk) split items
 constexpr int X3F_IPT = (X3F_ITEMS + X3F_THREADS - 1) / X3F_THREADS;  // 3
 constexpr int X3F_GRID = 256;
-constexpr int X3F_STORES = 6 * X3F_NT;            // epilogue global stores per wave and unit
+constexpr int X3F_STORES = 2 * X3F_NT;            // epilogue global stores per wave and unit (x3f_store_row)
 static_assert(X3F_RAW % 1024 == 512, "the last DMA wave-instruction is a half piece");
 // act16 images in HBM: per SAMPLE, the whole 26 x 26 cut as an h plane then an l plane ([pixel][32 ci]
 // f16, 64-B pixels, chunk slot c8 ^ (x & 2)), 86,528 B a sample: a unit (sample, third t3) is rows
@@ -176,6 +176,38 @@ __device__ __forceinline__ void x3f_issue_raw(const float* act, int uu, int wave
         } else if (piece == X3F_PIECES16 / 64 && lane < 32) {
             glds16_so(base, voff[k], raw_lds + piece * 1024);
         }
+    }
+}
+
+// pooled / code of one (unit, co) output row (12 windows). Lane (n16, kc) holds windows kc, 4 + kc, 8 + kc
+// (M tiles 0-2); a 4 x 4 transpose across the four 16-lane groups (two v_permlane32_swap + two
+// v_permlane16_swap per value) gives lane kc' windows 4 kc' .. 4 kc' + 3: one float4 + one u32 store on
+// lanes kc' < 3 instead of three 4-B and three 1-B stores per lane (16 scattered pieces each; the six
+// stores cost ~15 % of the kernel, interleaved A/B)
+__device__ __forceinline__ void x3f_t4(uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
+    auto s = __builtin_amdgcn_permlane32_swap(r0, r2, false, false);  // r0 lanes 32-63 <-> r2 lanes 0-31
+    r0 = s[0];
+    r2 = s[1];
+    s = __builtin_amdgcn_permlane32_swap(r1, r3, false, false);
+    r1 = s[0];
+    r3 = s[1];
+    s = __builtin_amdgcn_permlane16_swap(r0, r1, false, false);  // r0 odd 16-lane rows <-> r1 even rows
+    r0 = s[0];
+    r1 = s[1];
+    s = __builtin_amdgcn_permlane16_swap(r2, r3, false, false);
+    r2 = s[0];
+    r3 = s[1];
+}
+__device__ __forceinline__ void x3f_store_row(float m0, float m1, float m2, uint32_t c0, uint32_t c1, uint32_t c2,
+                                              int kc, float* __restrict__ prow, uint8_t* __restrict__ crow) {
+    uint32_t v0 = __float_as_uint(m0), v1 = __float_as_uint(m1), v2 = __float_as_uint(m2), v3 = 0u;
+    uint32_t q3 = 0u;
+    x3f_t4(v0, v1, v2, v3);
+    x3f_t4(c0, c1, c2, q3);
+    if (kc < 3) {
+        *reinterpret_cast<float4*>(prow + 4 * kc) =
+            make_float4(__uint_as_float(v0), __uint_as_float(v1), __uint_as_float(v2), __uint_as_float(v3));
+        *reinterpret_cast<uint32_t*>(crow + 4 * kc) = c0 | (c1 << 8) | (c2 << 16) | (q3 << 24);
     }
 }
 
@@ -300,19 +332,22 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     // stream — the previous unit's M tile 2 during M tile 0, M tile 0 during M tile 1, M tile 1 during M
     // tile 2 — so its VALU issues between MFMAs instead of after them (0.226 -> 0.218 ms interleaved
     // A/B; an epilogue after the stream with a rare-case scale branch: 0.237).
+    // The pooled value + code of a lane's window in M tiles 0 and 1 are held (hm / hc) until the row's
+    // tile 2 is done, then the row is stored by x3f_store_row.
     f32x4 pend[X3F_NT];
-    size_t p_o = 0;
+    float hm[2][X3F_NT];
+    uint32_t hc[2][X3F_NT];
+    size_t p_o = 0;  // output row of the pending tile 2 (window 0 of co 32 ch + n16)
     float p_pre = 1.f, p_us = 1.f;
-    auto epi_piece = [&](const f32x4& a, float pre, float us, float bs, size_t o) {
+    auto pool_piece = [&](const f32x4& a, float pre, float us, float bs, float& m, uint32_t& c) {
         float am = a[0];
         int idx = 0;
 #pragma unroll
         for (int q = 1; q < 4; ++q)
             if (a[q] > am) { am = a[q]; idx = q; }
-        float m = fmaf(am * pre, us, bs);
+        m = fmaf(am * pre, us, bs);
         m = m > 0.f ? m : 0.f;
-        pooled[o] = m;
-        code[o] = (uint8_t)(m > 0.f ? idx : CODE_NONE);
+        c = m > 0.f ? (uint32_t)idx : (uint32_t)CODE_NONE;
     };
 #pragma unroll 1
     for (; u < u1; ++u, ++k) {
@@ -355,10 +390,15 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             // this unit's scales and output offsets (for the pieces of its epilogue issued in-stream)
             const int b_ = u / 3, t3_ = u - (u / 3) * 3, se_ = sexp(b_) + sw;
             const float pre_ = ldexpf(1.f, min(126 - se_, 0)), us_ = ldexpf(1.f, -min(se_, 126));
-            const size_t o_ = (size_t)b_ * P_SAMPLE + (32 * ch + n16) * P_WIN + (4 * t3_ + wr) * P_HW + kc;
-            if (k == 0) {  // no pending piece yet: a zero piece aimed at this unit's mt-2 outputs (rewritten later)
-                pend[0] = pend[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                p_o = o_ + 8;
+            const size_t o_ = (size_t)b_ * P_SAMPLE + (32 * ch + n16) * P_WIN + (4 * t3_ + wr) * P_HW;
+            if (k == 0) {  // no pending row yet: a zero row aimed at this unit's outputs (rewritten later)
+#pragma unroll
+                for (int nt = 0; nt < X3F_NT; ++nt) {
+                    pend[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    hm[0][nt] = hm[1][nt] = 0.f;
+                    hc[0][nt] = hc[1][nt] = 0u;
+                }
+                p_o = o_;
                 p_pre = 1.f;
                 p_us = 1.f;
             }
@@ -372,13 +412,20 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
                     acc[mt][nt] = mfma_x3(fh[st % (RA + 1)], fl[st % (RA + 1)], wh[nt][tap], wl[nt][tap], acc[mt][nt]);
                 if (tap == 3 || tap == 6) {
                     const int nt = tap == 3 ? 0 : 1;
-                    if (mt == 0) epi_piece(pend[nt], p_pre, p_us, bias[nt], p_o + nt * 16 * P_WIN);
-                    else epi_piece(acc[mt - 1][nt], pre_, us_, bias[nt], o_ + nt * 16 * P_WIN + 4 * (mt - 1));
+                    if (mt == 0) {  // the previous unit's tile 2 completes its row
+                        float m2;
+                        uint32_t c2;
+                        pool_piece(pend[nt], p_pre, p_us, bias[nt], m2, c2);
+                        const size_t ro = p_o + nt * 16 * P_WIN;
+                        x3f_store_row(hm[0][nt], hm[1][nt], m2, hc[0][nt], hc[1][nt], c2, kc, pooled + ro, code + ro);
+                    } else {
+                        pool_piece(acc[mt - 1][nt], pre_, us_, bias[nt], hm[mt - 1][nt], hc[mt - 1][nt]);
+                    }
                 }
             }
             pend[0] = acc[2][0];
             pend[1] = acc[2][1];
-            p_o = o_ + 8;
+            p_o = o_;
             p_pre = pre_;
             p_us = us_;
             // (measured: leaving the order to the compiler beats pinning it with sched_group_barrier,
@@ -416,16 +463,27 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         if constexpr (!IN16) {  // epilogue after the stream (the f32-cut path stages mid-stream)
             const int b = u / 3, t3 = u - (u / 3) * 3, se = sexp(b) + sw;
             const float pre = ldexpf(1.f, min(126 - se, 0)), us = ldexpf(1.f, -min(se, 126));
-            const size_t o = (size_t)b * P_SAMPLE + (32 * ch + n16) * P_WIN + (4 * t3 + wr) * P_HW + kc;
+            const size_t o = (size_t)b * P_SAMPLE + (32 * ch + n16) * P_WIN + (4 * t3 + wr) * P_HW;
 #pragma unroll
-            for (int mt = 0; mt < 3; ++mt)
+            for (int nt = 0; nt < X3F_NT; ++nt) {
+                float m[3];
+                uint32_t c[3];
 #pragma unroll
-                for (int nt = 0; nt < X3F_NT; ++nt) epi_piece(acc[mt][nt], pre, us, bias[nt], o + nt * 16 * P_WIN + 4 * mt);
+                for (int mt = 0; mt < 3; ++mt) pool_piece(acc[mt][nt], pre, us, bias[nt], m[mt], c[mt]);
+                const size_t ro = o + nt * 16 * P_WIN;
+                x3f_store_row(m[0], m[1], m[2], c[0], c[1], c[2], kc, pooled + ro, code + ro);
+            }
         }
     }
     if (IN16 && k > 0) {  // the last unit's M tile 2
 #pragma unroll
-        for (int nt = 0; nt < X3F_NT; ++nt) epi_piece(pend[nt], p_pre, p_us, bias[nt], p_o + nt * 16 * P_WIN);
+        for (int nt = 0; nt < X3F_NT; ++nt) {
+            float m2;
+            uint32_t c2;
+            pool_piece(pend[nt], p_pre, p_us, bias[nt], m2, c2);
+            const size_t ro = p_o + nt * 16 * P_WIN;
+            x3f_store_row(hm[0][nt], hm[1][nt], m2, hc[0][nt], hc[1][nt], c2, kc, pooled + ro, code + ro);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }

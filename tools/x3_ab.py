@@ -100,6 +100,15 @@ def main():
             L.slk_fc_xent_amax.argtypes = [P] * 9 + [ctypes.c_float, P, ctypes.c_int, P]
             cases[f"fc {tag}"] = (lambda L=L, lg=lg, li=li, dlg=dlg, dpo=dpo, dpam=dpam, yl=yl: L.slk_fc_xent_amax(
                 p(pooled), p(W3), p(b3), p(yl), p(lg), p(li), p(dlg), p(dpo), p(dpam), 1.0 / B, None, B, st))
+            outs[f"fc {tag}"] = dpo
+        if "fcw" in args.ops.split(","):
+            L.slk_fc_wgrad_nslab.restype = ctypes.c_int
+            L.slk_fc_wgrad.restype = ctypes.c_int
+            L.slk_fc_wgrad.argtypes = [P] * 3 + [ctypes.c_int, P]
+            dlw = torch.randn(B, 10, device=dev, generator=torch.Generator(device=dev).manual_seed(5)) / B
+            slw = torch.empty(L.slk_fc_wgrad_nslab(B), 92170, device=dev)
+            cases[f"fcw {tag}"] = (lambda L=L, dlw=dlw, slw=slw: L.slk_fc_wgrad(p(dlw), p(pooled), p(slw), B, st))
+            outs[f"fcw {tag}"] = slw
         if "wgrad" in args.ops:
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
@@ -127,7 +136,7 @@ def main():
             first[op] = t
             continue
         r = first[op]
-        red = (lambda z: z.sum(0)) if op == "dgc1" else (lambda z: z)
+        red = (lambda z: z.sum(0)) if op in ("dgc1", "fcw") else (lambda z: z)
         a, b_ = red(t.double()), red(r.double())
         print(f"check {k:18s} max|diff|/max|ref| {((a - b_).abs().max() / b_.abs().max()).item():.3e}", flush=True)
 
