@@ -542,17 +542,26 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ W2, float* __restrict__ cut_grad, int B, const float* __restrict__ xin = nullptr,
     const uint32_t* __restrict__ relu_bits = nullptr, float* __restrict__ c1slabs = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
-    // C1W: per pair, x (3,136 B) then its ReLU bits (2,704 B), double-buffered, moved by LDS-DMA
-    constexpr int XB_X = IN_HW * IN_HW * 4, XB_BYTES = XB_X + RB_SAMPLE * 4;
+    // C1W: per pair, x (3,136 B), a second copy of x, then its ReLU bits (2,704 B), double-buffered
+    // (XB_BYTES apart, a multiple of 128 B), moved by LDS-DMA; after both buffers the plane of ones (below).
+    // The epilogue's x reads (ds_read2_b32: banks = dword % 32 over 32-lane halves) of lane groups kc and
+    // kc + 1 collided 2-way (taps 28-30 / 56-58 dwords over the other's 0-2 / 24-26 after the +4 pixel
+    // shift); odd kc reads the copy, 784 dwords = 16 banks further, and the ones plane sits 4 banks off
+    // both x planes (at 0 its lanes collided with tap 0's): 680 -> 54 modelled conflict cycles per sample
+    // and co tile (the guide's LDS bank table; SQ_LDS_BANK_CONFLICT 4.55 M -> measured below)
+    constexpr int XB_X = IN_HW * IN_HW * 4, XB_BITS = 2 * XB_X;
+    constexpr int XB_BYTES = (XB_BITS + RB_SAMPLE * 4 + 127) / 128 * 128;
     static_assert(XB_X > 3072 && XB_X <= 4096 && XB_X % 16 == 0 && RB_SAMPLE * 4 > 2048 && RB_SAMPLE * 4 <= 3072 &&
                   RB_SAMPLE % 4 == 0, "DMA pieces of issue_xb");
-    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 : 1][C1W ? XB_BYTES : 16];
+    static_assert((XB_X / 4) % 32 == 16, "x copy 16 banks over");
+    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 * XB_BYTES + 16 + XB_X : 16];
     // C1W: each wave's conv1-gradient accumulator D1[ci 16 nt + 4 (lane >> 4) + r][col lane & 15] (col =
     // tap 0-8, 9 = bias), kept here between epilogues (not in the MFMA loop's registers)
     __shared__ __attribute__((aligned(16))) f32x4 d1s[C1W ? X3D_THREADS : 1];
     // C1W: an x-shaped plane of 1.0 that the bias column's lanes (col 9) read in place of x, so the B
-    // operand needs no per-element select (cols 10-15 read x: their D1 columns are never stored)
-    __shared__ __attribute__((aligned(16))) float ones[C1W ? IN_HW * IN_HW : 1];
+    // operand needs no per-element select (cols 10-15 read x: their D1 columns are never stored); 4 banks
+    // off both x planes (above)
+    float* const ones = reinterpret_cast<float*>(xbm + (C1W ? 2 * XB_BYTES + 16 : 0));
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
@@ -670,18 +679,19 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const int per = (P + G - 1) / G;
     const int p0 = min((int)blockIdx.x * per, P), p1 = min(p0 + per, P);
     int pr = p0;
-    // pair pp's x and bits -> xbm[buf]: waves 0-3 move x (3 x 1 KiB + 64 B), waves 4-6 the bits (2 x
-    // 1 KiB + 656 B), one 16-B piece per lane (retired by the s_waitcnt before the barrier that opens the next pair)
+    // pair pp's x, x copy and bits -> buffer buf: waves 0-3 move x, waves 4-7 its copy (3 x 1 KiB + 64 B
+    // each), waves 0-2 the bits (2 x 1 KiB + 656 B), one 16-B piece per lane (retired by the s_waitcnt before
+    // the barrier that opens the next pair)
     auto issue_xb = [&](int pp, int buf) {
         const size_t b = (size_t)(pp / 3);
-        if (wave < 4) {
-            if (wave < 3 || lane < (XB_X % 1024) / 16)
-                glds16_so(reinterpret_cast<const char*>(xin + b * IN_HW * IN_HW) + wave * 1024, (uint32_t)lane * 16,
-                          lds_u32(xbm[buf]) + wave * 1024);
-        } else if (wave < 6 || (wave == 6 && lane < (RB_SAMPLE * 4 - 2048) / 16)) {
-            glds16_so(reinterpret_cast<const char*>(relu_bits + b * RB_SAMPLE) + (wave - 4) * 1024, (uint32_t)lane * 16,
-                      lds_u32(xbm[buf]) + XB_X + (wave - 4) * 1024);
-        }
+        const uint32_t dst = lds_u32(xbm) + buf * XB_BYTES;
+        const int w4 = wave & 3;
+        if (w4 < 3 || lane < (XB_X % 1024) / 16)
+            glds16_so(reinterpret_cast<const char*>(xin + b * IN_HW * IN_HW) + w4 * 1024, (uint32_t)lane * 16,
+                      dst + (wave >= 4 ? XB_X : 0) + w4 * 1024);
+        if (wave < 2 || (wave == 2 && lane < (RB_SAMPLE * 4 - 2048) / 16))
+            glds16_so(reinterpret_cast<const char*>(relu_bits + b * RB_SAMPLE) + wave * 1024, (uint32_t)lane * 16,
+                      dst + XB_BITS + wave * 1024);
     };
     if constexpr (C1W) {
         d1s[tid] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -706,8 +716,9 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         const int ci = 16 * nt + n16;
         // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff;
         // the bias col 9 reads the ones plane; cols 10-15 read x (their D1 columns are never stored)
-        const float* xs = n16 == 9 ? ones : reinterpret_cast<const float*>(xbm[qe & 1]);
-        const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbm[qe & 1] + XB_X);
+        const char* xbb = xbm + (qe & 1) * XB_BYTES;
+        const float* xs = n16 == 9 ? ones : reinterpret_cast<const float*>(xbb + ((kc & 1) ? XB_X : 0));
+        const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbb + XB_BITS);
         const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
         const bool t3 = T0e + g + 12 < T1e;  // wave-uniform: tiles 0-2 exist for every wave and part
         uint32_t mw[X3D_MPW];
