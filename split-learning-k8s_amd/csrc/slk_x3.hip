@@ -1031,8 +1031,13 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
         const uint32_t dc = dcb[0] | (dcb[1] << 8) | (dcb[2] << 16) | (dcb[3] << 24);
         const uint32_t cA = __builtin_amdgcn_perm(0u, dc, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dc, 0x03030202u);
         const int wy = dw / 12, wx = dw % 12;
+        // a 16-lane group of ds_write_b64 (banks = dword % 32) holds the 8 co groups of windows dw and dw + 1:
+        // the odd window walks the positions in the order pos ^ 1, so the two windows write pixels of
+        // opposite parity, 16 banks apart (same order: 2-way on every store, SQ_LDS_BANK_CONFLICT 4.8 M)
+        const int pf = dw & 1;
 #pragma unroll
-        for (int pos = 0; pos < 4; ++pos) {
+        for (int pos0 = 0; pos0 < 4; ++pos0) {
+            const int pos = pos0 ^ pf;
             const uint32_t T = 0xFFu << (8 * pos);
             const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
             const int q = (2 * wy + (pos >> 1)) * 24 + 2 * wx + (pos & 1);
