@@ -70,6 +70,12 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
 // ---------------------------------------------------------------------------- LDS-DMA as inline asm
 // global_load_lds issued through asm: hipcc then neither counts it nor inserts its own vmcnt(0) in
 // front of LDS reads and writes it cannot prove disjoint from a DMA in flight (it cannot tell a

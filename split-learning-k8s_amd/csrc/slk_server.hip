@@ -502,87 +502,124 @@ __global__ __launch_bounds__(C2W_THREADS, 3) void conv2_wgrad_kernel(
 extern "C" int slk_conv2_wgrad_direct_nslab(int B) { return B > 0 ? (2 * B < C2W_MAXSLAB ? 2 * B : C2W_MAXSLAB) : 0; }
 
 // ============================================================================ fc1 + cross-entropy
-// FC_S = 4 samples per 256-thread workgroup. MODE bits: 1 = fc forward (logits), 2 = cross-entropy
-// fwd+bwd, 4 = fc input gradient (dpooled = dlogits @ W3). W3 (368 KB) is L2/MALL-resident and is
-// re-read once per FC_S samples per phase; pooled is streamed from HBM once. Measured at B = 4096
-// (tools/ablate.py, threads x samples): 512x8 0.106 ms (134 VGPRs: one workgroup per CU, two dispatch
-// rounds), 512x8 forced to 2/CU 0.087 (spills), 256x4 0.074, 512x4 0.087, 128x4 0.093, 256x2 0.116
-// (W3 re-reads double): 1024 four-wave workgroups all resident at once is the sweet spot.
-#ifndef SLK_FC_S
-#define SLK_FC_S 4
-#endif
-#ifndef SLK_FC_T
-#define SLK_FC_T 256
-#endif
-#ifndef SLK_FC_WPE
-#define SLK_FC_WPE 1
-#endif
-constexpr int FC_S = SLK_FC_S;
-constexpr int FC_T = SLK_FC_T;
-constexpr int FC_K4 = P_SAMPLE / 4;  // 2304
+// FCH_S = 16 samples per 512-thread workgroup (B = 4096: one workgroup per CU, one dispatch round).
+// MODE bits: 1 = fc forward (logits), 2 = cross-entropy fwd+bwd, 4 = fc input gradient (dpooled =
+// dlogits @ W3, + dp_amax = per-sample max |dpooled| when asked).
+// Logits on v_mfma_f32_16x16x4_f32 (A = 16 samples x 4 features, B = 4 features x 16 classes, 10 used):
+// wave w owns features [1152 w, 1152 (w + 1)) and streams them in 18 chunks of 64 features — the 16
+// sample rows and W3's 10 rows of the chunk — by LDS-DMA into its own two slots (no barrier in the
+// loop: each wave waits for its own DMA with a counted vmcnt). Rows sit 288 B apart in LDS, so the
+// fragment reads (ds_read_b128, lane = (row, 4-feature group)) are conflict-free. W3 crosses L2 once per
+// 16 samples: the VALU head this replaces (4 samples per workgroup) re-read all of W3 per 4 samples
+// (377 MB of L2 reads per pass at B = 4096) and its logits pass read pooled at 2.7 TB/s.
+// dpooled on the VALU: thread = float4 column k4 with W3's 10 float4 of it in registers, every sample's
+// row stored as 1-KiB-contiguous wave stores (the 10-term fmaf chain per output, classes in order).
+constexpr int FCH_S = 16, FCH_T = 512, FCH_W = FCH_T / 64;
+constexpr int FCH_KW = P_SAMPLE / FCH_W;  // 1152 features per wave
+constexpr int FCH_CK = 64;                // features per chunk
+constexpr int FCH_NCH = FCH_KW / FCH_CK;  // 18
+constexpr int FCH_ROW = FCH_CK * 4 + 32;  // 288-B LDS rows: (72 s + 4 kg) dwords are 16 distinct 4-bank slots per lane group
+constexpr int FCH_A = FCH_S * FCH_ROW;    // 4,608 B of sample rows (4 full DMA pieces + half of a fifth)
+constexpr int FCH_SLOT = FCH_A + 3 * 1024;  // + W3 rows (10 x 288 = 2,880 B in 3 DMA pieces)
+constexpr int FC_K4 = P_SAMPLE / 4;         // 2304 float4 columns
+static_assert(P_SAMPLE % FCH_W == 0 && FCH_KW % FCH_CK == 0 && FCH_NCH >= 2 && NCLS * FCH_ROW <= 3 * 1024 &&
+                  FCH_A > 4096 && FCH_A <= 5120, "fc head tiling");
 
 template <int MODE>
-__global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
+__global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
     const float* __restrict__ pooled, const float* __restrict__ W3, const float* __restrict__ b3,
     const int64_t* __restrict__ labels, float* __restrict__ logits, float* __restrict__ loss_i,
     float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B,
-    float* __restrict__ dp_amax = nullptr) {
-    __shared__ float red[FC_T / 64][FC_S * NCLS];
-    __shared__ float zl[FC_S][NCLS];
-    __shared__ float dl[FC_S][NCLS];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * FC_S;
-    const int ns = min(FC_S, B - b0);
-    const float4* W34 = reinterpret_cast<const float4*>(W3);
+    float* __restrict__ dp_amax) {
+    __shared__ __attribute__((aligned(1024))) char smem[(MODE & 1) ? FCH_W * 2 * FCH_SLOT : 16];
+    __shared__ __attribute__((aligned(16))) f32x4 red[(MODE & 1) ? FCH_W * 64 : 1];
+    __shared__ float zl[FCH_S][NCLS];
+    __shared__ float dl[FCH_S][NCLS];
+    __shared__ float mx[FCH_W][FCH_S];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int s0 = blockIdx.x * FCH_S;
+    const int ns = min(FCH_S, B - s0);
 
-    if (MODE & 1) {
-        float acc[FC_S][NCLS];
+    if constexpr ((MODE & 1) != 0) {
+        char* const slots = smem + wave * 2 * FCH_SLOT;
+        const int kb = wave * FCH_KW;
+        // DMA lane offsets: piece j fills slot bytes [1024 j, 1024 j + 1024), lane l the 16 B at
+        // X = 1024 j + 16 l = row X / 288, byte X % 288 (pad bytes and rows past the batch: a valid dummy)
+        uint32_t va[5], vw[3];
 #pragma unroll
-        for (int s = 0; s < FC_S; ++s)
-#pragma unroll
-            for (int jj = 0; jj < NCLS; ++jj) acc[s][jj] = 0.f;
-        const float4* P4 = reinterpret_cast<const float4*>(pooled + (size_t)b0 * P_SAMPLE);
-        for (int k4 = tid; k4 < FC_K4; k4 += FC_T) {
-            float4 w[NCLS];
-#pragma unroll
-            for (int jj = 0; jj < NCLS; ++jj) w[jj] = W34[jj * FC_K4 + k4];
-#pragma unroll
-            for (int s = 0; s < FC_S; ++s) {
-                if (s < ns) {
-                    const float4 p = P4[s * FC_K4 + k4];
-#pragma unroll
-                    for (int jj = 0; jj < NCLS; ++jj)
-                        acc[s][jj] = fmaf(p.w, w[jj].w, fmaf(p.z, w[jj].z, fmaf(p.y, w[jj].y, fmaf(p.x, w[jj].x, acc[s][jj]))));
-                }
-            }
+        for (int j = 0; j < 5; ++j) {
+            const int X = 1024 * j + 16 * lane, r = X / FCH_ROW, off = X - (X / FCH_ROW) * FCH_ROW;
+            va[j] = (r < FCH_S && off < FCH_CK * 4) ? (uint32_t)(min(r, ns - 1) * P_SAMPLE * 4 + off) : 0u;
         }
 #pragma unroll
-        for (int s = 0; s < FC_S; ++s)
+        for (int j = 0; j < 3; ++j) {
+            const int X = 1024 * j + 16 * lane, r = X / FCH_ROW, off = X - (X / FCH_ROW) * FCH_ROW;
+            vw[j] = (r < NCLS && off < FCH_CK * 4) ? (uint32_t)(r * P_SAMPLE * 4 + off) : 0u;
+        }
+        auto issue = [&](int c) {  // 8 DMA instructions per chunk (the fifth A piece: lanes 0-31)
+            const uint32_t la = lds_u32(slots + (c & 1) * FCH_SLOT);
+            const float* pa = pooled + (size_t)s0 * P_SAMPLE + kb + c * FCH_CK;
+            const float* pw = W3 + kb + c * FCH_CK;
 #pragma unroll
-            for (int jj = 0; jj < NCLS; ++jj) {
-                const float v = wave_sum(acc[s][jj]);
-                if (lane == 0) red[wave][s * NCLS + jj] = v;
+            for (int j = 0; j < 4; ++j) glds16_so(pa, va[j], la + 1024 * j);
+            if (lane < (FCH_A - 4096) / 16) glds16_so(pa, va[4], la + 4096);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) glds16_so(pw, vw[j], la + FCH_A + 1024 * j);
+        };
+        issue(0);
+        issue(1);
+        // A fragment: lane (sample s16, group kg) holds features 16 blk + 4 kg + i; B: lane (class, kg) the
+        // same features of W3 row min(class, 9) (classes 10-15: duplicates, never stored)
+        const int s16 = lane & 15, kg = lane >> 4, nrow = min(s16, NCLS - 1);
+        f32x4 acc[4];
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+            acc[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
+            slk_keep(acc[blk]);
+        }
+#pragma unroll 2
+        for (int c = 0; c < FCH_NCH; ++c) {
+            if (c + 1 < FCH_NCH) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // chunk c landed, c + 1 in flight
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const char* sl = slots + (c & 1) * FCH_SLOT;
+            f32x4 a[4], w[4];
+#pragma unroll
+            for (int blk = 0; blk < 4; ++blk) {
+                a[blk] = *reinterpret_cast<const f32x4*>(sl + s16 * FCH_ROW + 64 * blk + 16 * kg);
+                w[blk] = *reinterpret_cast<const f32x4*>(sl + FCH_A + nrow * FCH_ROW + 64 * blk + 16 * kg);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before chunk c + 2 overwrites it
+            if (c + 2 < FCH_NCH) issue(c + 2);
+#pragma unroll
+            for (int blk = 0; blk < 4; ++blk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[blk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[blk][i], w[blk][i], acc[blk], 0, 0, 0);
+        }
+        // D[4 (lane >> 4) + r][lane & 15] = (sample, class) partial over this wave's features
+        red[wave * 64 + lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         __syncthreads();
-        if (tid < FC_S * NCLS) {
-            const int s = tid / NCLS, jj = tid - s * NCLS;
+        if (tid < 256) {
+            const int l = tid & 63, r = tid >> 6, n = l & 15, s = 4 * (l >> 4) + r;
             float v = 0.f;
 #pragma unroll
-            for (int w = 0; w < FC_T / 64; ++w) v += red[w][tid];
-            v += b3[jj];
-            zl[s][jj] = v;
-            if (s < ns) logits[(size_t)(b0 + s) * NCLS + jj] = v;
+            for (int w = 0; w < FCH_W; ++w) v += red[w * 64 + l][r];
+            if (n < NCLS) {
+                v += b3[n];
+                zl[s][n] = v;
+                if (s < ns) logits[(size_t)(s0 + s) * NCLS + n] = v;
+            }
         }
         __syncthreads();
-    } else if (MODE & 2) {
-        if (tid < FC_S * NCLS) {
+    } else if constexpr ((MODE & 2) != 0) {
+        if (tid < FCH_S * NCLS) {
             const int s = tid / NCLS, jj = tid - s * NCLS;
-            zl[s][jj] = s < ns ? logits[(size_t)(b0 + s) * NCLS + jj] : 0.f;
+            zl[s][jj] = s < ns ? logits[(size_t)(s0 + s) * NCLS + jj] : 0.f;
         }
         __syncthreads();
     }
 
-    if (MODE & 2) {
+    if constexpr ((MODE & 2) != 0) {
         if (tid < ns) {
             const int s = tid;
             float z[NCLS];
@@ -595,71 +632,71 @@ __global__ __launch_bounds__(FC_T, SLK_FC_WPE) void fc_head_kernel(
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) se += expf(z[jj] - m);
             const float lse = m + logf(se);
-            const int64_t y = labels[b0 + s];
+            const int64_t y = labels[s0 + s];
             const bool ok = (y >= 0 && y < NCLS);
             if (!ok && err_flag) atomicOr(err_flag, 1);
             float yz = 0.f;
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) yz = (jj == y) ? z[jj] : yz;
             const float nanv = __builtin_nanf("");
-            loss_i[b0 + s] = ok ? (lse - yz) : nanv;
+            loss_i[s0 + s] = ok ? (lse - yz) : nanv;
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) {
                 const float g = ok ? (expf(z[jj] - lse) - (jj == y ? 1.f : 0.f)) * grad_scale : nanv;
                 dl[s][jj] = g;
-                dlogits[(size_t)(b0 + s) * NCLS + jj] = g;
+                dlogits[(size_t)(s0 + s) * NCLS + jj] = g;
             }
         }
         __syncthreads();
-    } else if (MODE & 4) {
-        if (tid < FC_S * NCLS) {
+    } else if constexpr ((MODE & 4) != 0) {
+        if (tid < FCH_S * NCLS) {
             const int s = tid / NCLS, jj = tid - s * NCLS;
-            dl[s][jj] = s < ns ? dlogits[(size_t)(b0 + s) * NCLS + jj] : 0.f;
+            dl[s][jj] = s < ns ? dlogits[(size_t)(s0 + s) * NCLS + jj] : 0.f;
         }
         __syncthreads();
     }
 
-    if (MODE & 4) {
-        float4* D4 = reinterpret_cast<float4*>(dpooled + (size_t)b0 * P_SAMPLE);
-        float dmx[FC_S];  // per-sample max |dpooled| (dp_amax, the x3 kernels' scales)
+    if constexpr ((MODE & 4) != 0) {
+        const float4* W34 = reinterpret_cast<const float4*>(W3);
+        float4* D4 = reinterpret_cast<float4*>(dpooled + (size_t)s0 * P_SAMPLE);
+        float dmx[FCH_S];
 #pragma unroll
-        for (int s = 0; s < FC_S; ++s) dmx[s] = 0.f;
-        for (int k4 = tid; k4 < FC_K4; k4 += FC_T) {
+        for (int s = 0; s < FCH_S; ++s) dmx[s] = 0.f;
+        for (int k4 = tid; k4 < FC_K4; k4 += FCH_T) {
+            // dl stays in LDS (broadcast reads per use): hoisted out of this loop it took 160 VGPRs and spilled
+            asm volatile("" ::: "memory");
             float4 w[NCLS];
 #pragma unroll
             for (int jj = 0; jj < NCLS; ++jj) w[jj] = W34[jj * FC_K4 + k4];
-#pragma unroll 2
-            for (int s = 0; s < ns; ++s) {
-                float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                for (int jj = 0; jj < NCLS; ++jj) {
-                    const float d = dl[s][jj];  // LDS broadcast
-                    o.x = fmaf(d, w[jj].x, o.x); o.y = fmaf(d, w[jj].y, o.y);
-                    o.z = fmaf(d, w[jj].z, o.z); o.w = fmaf(d, w[jj].w, o.w);
-                }
-                D4[s * FC_K4 + k4] = o;
-                if (dp_amax) {
-                    const float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+            for (int s = 0; s < FCH_S; ++s) {
+                if (s < ns) {
+                    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                    for (int t = 0; t < FC_S; ++t) dmx[t] = (t == s) ? fmaxf(dmx[t], mo) : dmx[t];
+                    for (int jj = 0; jj < NCLS; ++jj) {
+                        const float d = dl[s][jj];  // LDS broadcast
+                        o.x = fmaf(d, w[jj].x, o.x);
+                        o.y = fmaf(d, w[jj].y, o.y);
+                        o.z = fmaf(d, w[jj].z, o.z);
+                        o.w = fmaf(d, w[jj].w, o.w);
+                    }
+                    D4[s * FC_K4 + k4] = o;
+                    dmx[s] = fmaxf(dmx[s], fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
                 }
             }
         }
         if (dp_amax) {
-            __syncthreads();  // red[] reuse
 #pragma unroll
-            for (int s = 0; s < FC_S; ++s) {
-                float v = dmx[s];
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-                if (lane == 0) red[wave][s] = v;
+            for (int s = 0; s < FCH_S; ++s) {
+                const float v = wave_max(dmx[s]);
+                if (lane == 0) mx[wave][s] = v;
             }
             __syncthreads();
             if (tid < ns) {
-                float v = red[0][tid];
+                float v = mx[0][tid];
 #pragma unroll
-                for (int w = 1; w < FC_T / 64; ++w) v = fmaxf(v, red[w][tid]);
-                dp_amax[b0 + tid] = v;
+                for (int w = 1; w < FCH_W; ++w) v = fmaxf(v, mx[w][tid]);
+                dp_amax[s0 + tid] = v;
             }
         }
     }
@@ -764,8 +801,8 @@ extern "C" int slk_fc_fwd(const float* pooled, const float* W3, const float* b3,
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(pooled && W3 && b3 && logits);
-    fc_head_kernel<1><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
-        pooled, W3, b3, nullptr, logits, nullptr, nullptr, nullptr, 0.f, nullptr, B);
+    fc_head16_kernel<1><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
+        pooled, W3, b3, nullptr, logits, nullptr, nullptr, nullptr, 0.f, nullptr, B, nullptr);
     return slk_launch_status();
 }
 
@@ -774,9 +811,9 @@ extern "C" int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, floa
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(logits && labels && loss_i && dlogits);
-    fc_head_kernel<2><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
+    fc_head16_kernel<2><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
         nullptr, nullptr, nullptr, labels, const_cast<float*>(logits), loss_i, dlogits, nullptr,
-        grad_scale, err_flag, B);
+        grad_scale, err_flag, B, nullptr);
     return slk_launch_status();
 }
 
@@ -785,9 +822,9 @@ extern "C" int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpoole
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(dlogits && W3 && dpooled);
-    fc_head_kernel<4><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
+    fc_head16_kernel<4><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
         nullptr, W3, nullptr, nullptr, nullptr, nullptr, const_cast<float*>(dlogits), dpooled, 0.f,
-        nullptr, B);
+        nullptr, B, nullptr);
     return slk_launch_status();
 }
 
@@ -797,8 +834,8 @@ extern "C" int slk_fc_xent(const float* pooled, const float* W3, const float* b3
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits && dpooled);
-    fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
-        pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B);
+    fc_head16_kernel<7><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
+        pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B, nullptr);
     return slk_launch_status();
 }
 
@@ -808,7 +845,7 @@ extern "C" int slk_fc_xent_amax(const float* pooled, const float* W3, const floa
     SLK_CHECK_ARG(B >= 0);
     if (B == 0) return 0;
     SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits && dpooled && dp_amax);
-    fc_head_kernel<7><<<(B + FC_S - 1) / FC_S, FC_T, 0, slk_stream(stream)>>>(
+    fc_head16_kernel<7><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
         pooled, W3, b3, labels, logits, loss_i, dlogits, dpooled, grad_scale, err_flag, B, dp_amax);
     return slk_launch_status();
 }

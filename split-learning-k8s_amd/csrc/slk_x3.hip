@@ -40,12 +40,6 @@ __device__ __forceinline__ int x3_exp(float amax) {
 // 2^-s1 * 2^-s2 applied as two exact power-of-two multiplies (each factor a normal float)
 __device__ __forceinline__ float x3_unscale(float v, float u1, float u2) { return (v * u1) * u2; }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
 // 8 scaled f32 values -> 8 f16 hi + 8 f16 lo (v_cvt_pk_f16_f32, RNE).
 __device__ __forceinline__ void x3_split8(const float* v, float sc, f16x8& h, f16x8& l) {
 #pragma unroll

@@ -1,6 +1,6 @@
 """The fused server head (slk_fc_xent / slk_fc_xent_amax: fc1 forward, cross-entropy forward + backward,
 fc1 input gradient — src/model_def.py:28, src/server_part.py:49-51) against float64 and against the
-separate launches (slk_fc_fwd -> slk_fc_dgrad), over ragged batch sizes (a workgroup holds 4 samples)."""
+separate launches (slk_fc_fwd -> slk_fc_dgrad), over ragged batch sizes (a workgroup holds 16 samples)."""
 import numpy as np
 import pytest
 import torch
@@ -22,7 +22,7 @@ def _ref64(pooled, W3, b3, y, scale):
     return z, loss, dz, (dz @ W).reshape(pooled.shape)
 
 
-@pytest.mark.parametrize("B", [1, 7, 16, 17, 100, 4096])
+@pytest.mark.parametrize("B", [1, 7, 15, 16, 17, 33, 100, 4096])
 def test_fc_xent_mfma_vs_float64_and_separate_kernels(gpu, B):
     from splitcnn import ops
     g = torch.Generator().manual_seed(B)

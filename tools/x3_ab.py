@@ -101,6 +101,21 @@ def main():
             cases[f"fc {tag}"] = (lambda L=L, lg=lg, li=li, dlg=dlg, dpo=dpo, dpam=dpam, yl=yl: L.slk_fc_xent_amax(
                 p(pooled), p(W3), p(b3), p(yl), p(lg), p(li), p(dlg), p(dpo), p(dpam), 1.0 / B, None, B, st))
             outs[f"fc {tag}"] = dpo
+        if "fc3" in args.ops.split(","):  # the same head as three launches: logits, CE, dpooled
+            lg3, li3, dl3, dpo3 = (torch.empty(B, 10, device=dev), torch.empty(B, device=dev),
+                                   torch.empty(B, 10, device=dev), torch.empty_like(dp))
+            yl3 = y.to(dev)
+            for n in ("slk_fc_fwd", "slk_xent_fwd_bwd", "slk_fc_dgrad"):
+                getattr(L, n).restype = ctypes.c_int
+            L.slk_fc_fwd.argtypes = [P] * 4 + [ctypes.c_int, P]
+            L.slk_xent_fwd_bwd.argtypes = [P] * 4 + [ctypes.c_float, P, ctypes.c_int, P]
+            L.slk_fc_dgrad.argtypes = [P] * 3 + [ctypes.c_int, P]
+            cases[f"fc3 {tag}"] = (lambda L=L, lg=lg3, li=li3, dl=dl3, dpo=dpo3, yl=yl3: L.slk_fc_fwd(
+                p(pooled), p(W3), p(b3), p(lg), B, st) | L.slk_xent_fwd_bwd(p(lg), p(yl), p(li), p(dl), 1.0 / B, None, B, st)
+                | L.slk_fc_dgrad(p(dl), p(W3), p(dpo), B, st))
+            cases[f"fc1 {tag}"] = (lambda L=L, lg=lg3: L.slk_fc_fwd(p(pooled), p(W3), p(b3), p(lg), B, st))
+            cases[f"fc4 {tag}"] = (lambda L=L, dl=dl3, dpo=dpo3: L.slk_fc_dgrad(p(dl), p(W3), p(dpo), B, st))
+            outs[f"fc {tag}3"] = dpo3
         if "fcw" in args.ops.split(","):
             L.slk_fc_wgrad_nslab.restype = ctypes.c_int
             L.slk_fc_wgrad.restype = ctypes.c_int
