@@ -66,6 +66,7 @@ def main():
         if "c1x3" in args.ops:
             i1 = torch.empty_like(a16)
             cases[f"c1x3 {tag}"] = (lambda L=L, am1=am1, i1=i1, f=c1x: f(L, am1, i1))
+            outs[f"c1x3 {tag}"] = i1
         dgc1_args = (lambda: (p(xg), p(bits))) if abi2 else (lambda: (p(xg), p(W1), p(b1)))
         if "fwd," in args.ops + "," :
             po, co, a16o = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16)
