@@ -1,12 +1,14 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 300 python tools/x3_ab.py build_abl/base2.so split-learning-k8s_amd/splitcnn/libslk.so --ops c1x3 --rounds 30 > gpurun_out/ab_c1.txt 2>&1 && \
-timeout -k 10 600 python -u -m pytest tests/test_x3_gpu.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t.txt 2>&1 && \
-timeout -k 10 400 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-k5 --no-conv-compare --no-hub-loopback > gpurun_out/b.log 2>&1; rc=$?
-cat gpurun_out/ab_c1.txt; tail -2 gpurun_out/t.txt
+rm -rf gpurun_out/prof_ng
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ng -o run --output-format csv -- python bench.py --config k2 --no-k5 --steps 10 --warmup 3 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-graph > gpurun_out/prof_ng.log 2>&1; rc=$?
 python3 - <<'PY'
-import json
-for l in open("gpurun_out/b.log"):
+import csv, glob, json
+for l in open("gpurun_out/prof_ng.log"):
     if l.startswith("{"):
-        d = json.loads(l); print("value", d["value"], "ms", d["ms_per_step"], "kernels", d.get("kernels"))
+        d = json.loads(l); print("events kernels", d.get("kernels"), "ms/step", round(d["ms_per_step"], 4))
+f = glob.glob("gpurun_out/prof_ng/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    if any(t in r["Name"] for t in ("x3_kernel<true>", "fc_head16", "fc_wgrad", "conv1_fwd_x3")):
+        print("rocprof", r["Name"][:44], r["Calls"], round(float(r["AverageNs"]) / 1e6, 4))
 PY
 exit $rc

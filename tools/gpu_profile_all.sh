@@ -14,7 +14,9 @@ rc=$?; echo "bench rc=$rc"; stop_if_fatal $rc bench
 timeout -k 10 300 python -u bench.py --config k5 --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/bench_k5.log 2>&1
 rc=$?; echo "bench k5 rc=$rc"; stop_if_fatal $rc bench_k5
 for cfg in k2 k5; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-pass > gpurun_out/prof_$cfg.log 2>&1
+  # eager steps (--no-graph): under --kernel-trace the graph-replayed step runs ~1/3 slower and its kernels
+  # 7-15 % slower, while eager launches time the same with and without the profiler (tools/x3_ab.py control)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 10 --warmup 3 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-graph > gpurun_out/prof_$cfg.log 2>&1
   rc=$?; echo "rocprof $cfg rc=$rc"; stop_if_fatal $rc rocprof
   # the library build this profile belongs to (bench.py reports rocprof_avg_ms only for a matching build)
   python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_$cfg.build_id
