@@ -261,6 +261,10 @@ class ServerStage:
         self.loss_log = loss_log if loss_log is not None else LossLog(self.device)
         self.err_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.fuse_optim = True  # step_request: SGD of both slab kinds + the loss log in one launch
+        # launch order knobs (profiling, tools/ab_trainers.py): fc1 wgrad right after the head (pooled
+        # just read by it), conv2 wgrad before the dgrad. Defaults: the measured fastest order.
+        self.fc_wgrad_early = False
+        self.wgrad_first = False
         self._buf = _Buffers()
 
     def bind_grads(self, view: torch.Tensor):
@@ -313,6 +317,17 @@ class ServerStage:
                 loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
                 dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
         # launch order dgrad -> wgrad -> fc wgrad (measured fastest: DESIGN.md §3a "Launch order")
+        if self.fc_wgrad_early:
+            with TIMER("fc_wgrad"):
+                s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+
+        def wgrad():
+            with TIMER("conv2_wgrad"):
+                return ops.conv2_wgrad_slabs(act, dpooled, code,
+                                             slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
+                                             impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
+        if self.wgrad_first:
+            s2 = wgrad()
         if client_fuse is not None:
             if di != "x3":
                 raise ValueError("client_fuse needs the x3 dgrad (conv preset 'x3' or 'x3w')")
@@ -325,12 +340,11 @@ class ServerStage:
                 cut_grad = self._b("cut_grad", (B, 32, 26, 26))
             with TIMER("conv2_dgrad"):
                 ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
-        with TIMER("conv2_wgrad"):
-            s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
-                                       slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=wi), ops.CONV2_SLAB)),
-                                       impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
-        with TIMER("fc_wgrad"):
-            s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+        if not self.wgrad_first:
+            s2 = wgrad()
+        if not self.fc_wgrad_early:
+            with TIMER("fc_wgrad"):
+                s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3
 
     def apply_grad_slabs(self, s2, s3):

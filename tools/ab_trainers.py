@@ -1,7 +1,8 @@
 """Profiling only: K2 SplitTrainer variants (engine attributes) captured as HIP graphs and timed
 interleaved in ONE process, B = 4096. usage: python tools/ab_trainers.py [--rounds 8]
 Variants: the conv presets (engine.CONV_PRESETS) and the default without its fusions. (Round 2 also timed
-launch-order knobs here — fc wgrad early, conv2 wgrad first — both slower; removed from the engine.)"""
+launch-order knobs here — fc wgrad early, conv2 wgrad first — both slower; round 4 re-times them with
+--order after the head moved to the MFMA.)"""
 import argparse
 import os
 import sys
@@ -20,14 +21,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--order", action="store_true", help="the launch-order knobs instead of the presets")
     args = ap.parse_args()
     B = 4096
     dev = torch.device("cuda:0")
     X, Y = make_pool(B, 4, dev)
     variants = {}
     configs = {"x3": {}, "x3_unfused": {"fuse_client_backward": False}, "x3w": {"conv": "x3w"}, "f32": {"conv": "f32"}}
+    server_attrs = {"x3_fcw_early": {"fc_wgrad_early": True}, "x3_wgrad_first": {"wgrad_first": True},
+                    "x3_both": {"fc_wgrad_early": True, "wgrad_first": True}}
+    if args.order:
+        configs = {"x3": {}, **{k: {} for k in server_attrs}}
     for name, kw in configs.items():
         tr = SplitTrainer(*init_models(seed=0), device=dev, graph=True, **kw)
+        for a, v in server_attrs.get(name, {}).items():
+            setattr(tr.server, a, v)
         for i in range(5):
             tr.step(X[i % 4], Y[i % 4])
         variants[name] = tr
