@@ -540,22 +540,23 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     // (XB_BYTES apart, a multiple of 128 B), moved by LDS-DMA; after both buffers the plane of ones (below).
     // The epilogue's x reads (ds_read2_b32: banks = dword % 32 over 32-lane halves) of lane groups kc and
     // kc + 1 collided 2-way (taps 28-30 / 56-58 dwords over the other's 0-2 / 24-26 after the +4 pixel
-    // shift); odd kc reads the copy, 784 dwords = 16 banks further, and the ones plane sits 4 banks off
-    // both x planes (at 0 its lanes collided with tap 0's): 680 -> 54 modelled conflict cycles per sample
-    // and co tile (the guide's LDS bank table; SQ_LDS_BANK_CONFLICT 4.55 M -> measured below)
-    constexpr int XB_X = IN_HW * IN_HW * 4, XB_BITS = 2 * XB_X;
+    // shift); odd kc reads the copy, 812 dwords (12 banks) further, and the ones plane sits 7 banks off
+    // both x planes (at 0 its lanes collided with tap 0's): 680 -> 4 modelled conflict cycles per sample
+    // and co tile (the guide's LDS bank table over every tile, tap and row-crossing case; a copy 16 banks
+    // over left 54, the row-crossing groups)
+    constexpr int XB_X = IN_HW * IN_HW * 4, XB_COPY = XB_X + 112, XB_BITS = XB_COPY + XB_X, XB_ONES = 28;
     constexpr int XB_BYTES = (XB_BITS + RB_SAMPLE * 4 + 127) / 128 * 128;
     static_assert(XB_X > 3072 && XB_X <= 4096 && XB_X % 16 == 0 && RB_SAMPLE * 4 > 2048 && RB_SAMPLE * 4 <= 3072 &&
-                  RB_SAMPLE % 4 == 0, "DMA pieces of issue_xb");
-    static_assert((XB_X / 4) % 32 == 16, "x copy 16 banks over");
-    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 * XB_BYTES + 16 + XB_X : 16];
+                  RB_SAMPLE % 4 == 0 && XB_COPY % 16 == 0 && XB_BITS % 16 == 0, "DMA pieces of issue_xb");
+    static_assert((XB_COPY / 4) % 32 == 12 && XB_BYTES % 128 == 0, "x copy 12 banks over");
+    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 * XB_BYTES + 32 + XB_X : 16];
     // C1W: each wave's conv1-gradient accumulator D1[ci 16 nt + 4 (lane >> 4) + r][col lane & 15] (col =
     // tap 0-8, 9 = bias), kept here between epilogues (not in the MFMA loop's registers)
     __shared__ __attribute__((aligned(16))) f32x4 d1s[C1W ? X3D_THREADS : 1];
     // C1W: an x-shaped plane of 1.0 that the bias column's lanes (col 9) read in place of x, so the B
     // operand needs no per-element select (cols 10-15 read x: their D1 columns are never stored); 4 banks
     // off both x planes (above)
-    float* const ones = reinterpret_cast<float*>(xbm + (C1W ? 2 * XB_BYTES + 16 : 0));
+    float* const ones = reinterpret_cast<float*>(xbm + (C1W ? 2 * XB_BYTES + XB_ONES : 0));
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nt = wave & 1, g = wave >> 1;
@@ -682,7 +683,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         const int w4 = wave & 3;
         if (w4 < 3 || lane < (XB_X % 1024) / 16)
             glds16_so(reinterpret_cast<const char*>(xin + b * IN_HW * IN_HW) + w4 * 1024, (uint32_t)lane * 16,
-                      dst + (wave >= 4 ? XB_X : 0) + w4 * 1024);
+                      dst + (wave >= 4 ? XB_COPY : 0) + w4 * 1024);
         if (wave < 2 || (wave == 2 && lane < (RB_SAMPLE * 4 - 2048) / 16))
             glds16_so(reinterpret_cast<const char*>(relu_bits + b * RB_SAMPLE) + wave * 1024, (uint32_t)lane * 16,
                       dst + XB_BITS + wave * 1024);
@@ -711,7 +712,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         // B operand of the conv1-gradient GEMM: lane col n16 = tap (ky, kx) reads x at pixel offset toff;
         // the bias col 9 reads the ones plane; cols 10-15 read x (their D1 columns are never stored)
         const char* xbb = xbm + (qe & 1) * XB_BYTES;
-        const float* xs = n16 == 9 ? ones : reinterpret_cast<const float*>(xbb + ((kc & 1) ? XB_X : 0));
+        const float* xs = n16 == 9 ? ones : reinterpret_cast<const float*>(xbb + ((kc & 1) ? XB_COPY : 0));
         const uint32_t* bs = reinterpret_cast<const uint32_t*>(xbb + XB_BITS);
         const int toff = n16 < 9 ? (n16 / 3) * IN_HW + n16 % 3 : 0;
         const bool t3 = T0e + g + 12 < T1e;  // wave-uniform: tiles 0-2 exist for every wave and part
