@@ -79,6 +79,8 @@ def parse():
                          "F(2x2,3x3) on the f32 MFMA throughout (default: splitcnn.engine.CONV_DEFAULT)")
     ap.add_argument("--no-conv-compare", action="store_true",
                     help="skip the short run of the other conv preset reported beside the headline")
+    ap.add_argument("--no-images", action="store_true",
+                    help="dense exchange of the f32 cut instead of the client's x3 split images (same bytes)")
     ap.add_argument("--no-hub-loopback", action="store_true",
                     help="skip the 1-GPU loopback of the K4 hub server's compute (7 clients x --micro chunks)")
     return ap.parse_args()
@@ -377,14 +379,15 @@ def run_hub_loopback(args, nc=7):
     B, m = args.batch, args.micro
     b, G = B // m, nc * B
     a, srv = init_models(seed=0)
+    images = bool(args.dense_exchange) and not getattr(args, "no_images", False)
     hub = sd.Hub(ServerStage(srv, device=dev), rank=nc, world=nc + 1, micro=m, compress=not args.dense_exchange,
-                 graph=not args.no_graph)
+                 graph=not args.no_graph, images=images)
     codec = hub._use_codec(dev)
     hub._prepare(B, dev, codec)  # the chunk graphs (their warm-up zeroes the receive buffers)
     cl = ClientStage(a, device=dev)
     cl.emit_amax = True
     n = b * 32 * 26 * 26
-    acts = hub._buf("acts", (G, 32, 26, 26), torch.float32, dev)
+    acts = hub._inputs(G, dev)
     labels = hub._buf("labels", (G,), torch.int64, dev)
     amx = hub._buf("amax", (G,), torch.float32, dev)
     hub._buf("cuts", (G, 32, 26, 26), torch.float32, dev)
@@ -394,8 +397,11 @@ def run_hub_loopback(args, nc=7):
         for ci in range(nc):
             sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
             x, y = data.batch(b)
-            cl.forward(x.to(dev), out=acts[sl])
-            amx[sl].copy_(cl._act_amax)
+            if images:
+                cl.forward_images(x.to(dev), acts[sl.start * sd.IMG_BYTES:sl.stop * sd.IMG_BYTES], amx[sl])
+            else:
+                cl.forward(x.to(dev), out=acts[sl])
+                amx[sl].copy_(cl._act_amax)
             labels[sl].copy_(y.to(dev))
             if codec is not None:
                 codec.encode(acts[sl], codec.buffers(("s", ci, k), n, dev))
@@ -421,7 +427,8 @@ def hub_loopback_rate(args, ref_value, conv1_ms):
     rate = K * nc * B / dt
     fused_minus_conv1 = B / (B / ref_value - conv1_ms * 1e-3) if ref_value and conv1_ms else None
     return {"workload": f"K4 hub server compute, {nc} clients x {B} samples in {m} chunks of {nc * b} "
-                        f"(codec unpack/pack {'on' if codec is not None else 'off'}, HIP graph per chunk), "
+                        f"(codec unpack/pack {'on' if codec is not None else 'off'}"
+                        f"{', x3 split images in' if hub.images else ''}, HIP graph per chunk), "
                         "inputs already in the receive buffers: the 1-GPU bound of BASELINE config 4",
             "samples_per_s": round(rate, 1), "ms_per_step": round(dt / K * 1e3, 3), "global_batch": nc * B,
             "fused_1gpu_minus_conv1_samples_per_s": round(fused_minus_conv1, 1) if fused_minus_conv1 else None,
@@ -465,7 +472,7 @@ XGMI_LINK_GBPS = 153.6   # vendor per-link xGMI figure (task brief: 7 links x ~1
 # Server-side rates of the hub step on one GPU (bench k4_server_loopback; samples/s at B = 4096 per
 # client): with the dense exchange the server runs the plain stage kernels, with the codec it also unpacks
 # and packs. Used only for the exchange PREDICTION reported next to the measured trial that decides.
-HUB_SERVER_RATE = {"dense": 4.4e6, "codec": 3.4e6}
+HUB_SERVER_RATE = {"dense": 5.2e6, "codec": 3.5e6}   # round 4: dense = the image exchange (Hub images=True)
 CODEC_WIRE_FRACTION = 0.456   # wire bytes / dense bytes of the codec on the synthetic data
 
 
@@ -510,22 +517,24 @@ def run_distributed(args, out, rank, world, local):
         if topology == "replicated":
             t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev), graph=not args.no_graph)
             return (lambda i: t.step(X[i % 4], Y[i % 4])), t, world * B
+        # the dense exchange ships the client's x3 split images (the f32 cut's bytes) unless --no-images
+        images = not codec and not args.no_images
         if topology == "pipeline":
             assert world == 2
             if rank == 0:
                 t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=codec, groups=groups,
-                                graph=not args.no_graph)
+                                graph=not args.no_graph, images=images)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
             t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec, groups=groups,
-                            graph=not args.no_graph)
+                            graph=not args.no_graph, images=images)
             return (lambda i: t.server_step(B, dev)), t, B
         if topology == "hub":
             if rank < world - 1:
                 t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
-                           groups=groups, graph=not args.no_graph)
+                           groups=groups, graph=not args.no_graph, images=images)
                 return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
             t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
-                       groups=groups, graph=not args.no_graph)
+                       groups=groups, graph=not args.no_graph, images=images)
             return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
         raise ValueError(topology)
 
@@ -538,7 +547,9 @@ def run_distributed(args, out, rank, world, local):
         "hub": f"K4: SplitFed, {nc} client GPU(s) feeding 1 server GPU (reference cut), micro-batched RCCL "
                "send/recv, client-gradient all-reduce (BASELINE config 4)"}
     codec_label = {True: "lossless sparse codec: ReLU-cut bit mask + nonzero values out, gradient at those positions "
-                         "back (bit-identical results)", False: "dense fp32"}
+                         "back (bit-identical results)",
+                   False: "dense: the client's x3 split images (f16 hi/lo, per-sample scale; the f32 cut's bytes) "
+                          "+ per-sample max out, fp32 cut gradient back" if not args.no_images else "dense fp32"}
 
     def wire(t):
         """rank 0 is a client in both exchange topologies: its link's bytes (both directions, labels and
@@ -725,6 +736,13 @@ def main():
                 torch.cuda.empty_cache()
                 out["k4_server_loopback"]["dense_exchange"] = {
                     k: v for k, v in hub_loopback_rate(argparse.Namespace(**{**vars(args), "dense_exchange": True}),
+                                                       out["value"], c1).items()
+                    if k in ("samples_per_s", "ms_per_step", "ratio", "workload")}
+                torch.cuda.empty_cache()
+                # the dense exchange of the f32 cut (--no-images): the server stages and splits f32 rows
+                out["k4_server_loopback"]["dense_f32_cut"] = {
+                    k: v for k, v in hub_loopback_rate(argparse.Namespace(**{**vars(args), "dense_exchange": True,
+                                                                             "no_images": True}),
                                                        out["value"], c1).items()
                     if k in ("samples_per_s", "ms_per_step", "ratio")}
             except Exception as e:  # the headline stands on its own

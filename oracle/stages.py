@@ -49,7 +49,18 @@ class OracleClient:
         self._x, self._act = x, t
         return t
 
+    def forward_images(self, x, act16, act_amax):
+        """dist.Hub(images=True)'s client call, emulated for the protocol tests: the f32 act's bytes fill
+        act16 (an x3 image sample has the same 86,528 bytes as an f32 cut sample) and act_amax takes
+        the per-sample max; OracleServer.compute reads them back as the f32 act."""
+        t = self.forward(x)
+        act16.copy_(t.to(torch.float32).contiguous().view(-1).view(torch.uint8))
+        act_amax.copy_(t.reshape(t.shape[0], -1).amax(dim=1).to(act_amax.dtype))
+
     def backward(self, cut_grad, x=None, act=None, accumulate=False):
+        if act is None and x is not None:   # as engine.ClientStage: the mask re-derived from x
+            p = _unflat(self.params, KEYS_C)
+            act = torch.from_numpy(O.client_forward(x.double().numpy(), p["W1"], p["b1"]))
         x = self._x if x is None else x
         act = self._act if act is None else act
         dW, db = O.client_backward(x.double().numpy(), act.double().numpy(), cut_grad.double().numpy())
@@ -77,7 +88,9 @@ class OracleServer:
         view.copy_(self.grads)
         self.grads = view
 
-    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None):
+    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act16=None):
+        if act is None:   # the image exchange, emulated: act16 carries the f32 act's bytes
+            act = act16.view(torch.float32).view(-1, 32, 26, 26)
         p = _unflat(self.params, KEYS_S)
         r = O.server_step(act.double().numpy(), labels.numpy(), p["W2"], p["b2"], p["W3"], p["b3"],
                           grad_scale_batch=1.0 / grad_scale)

@@ -40,6 +40,9 @@ import torch.distributed as dist
 
 CLIENT_N = 320
 SERVER_N = 110666
+# bytes per sample of the x3 split images (act16: 32 channels x 676 pixels x (hi, lo) f16) = the f32 cut's
+# 32 x 26 x 26 x 4: the image exchange moves the same bytes (ops.conv2_act16_bytes(1), checked in the GPU tests)
+IMG_BYTES = 2 * 2 * 32 * 26 * 26
 
 
 class _Staged:
@@ -286,8 +289,14 @@ class Hub:
 
     def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress=True,
                  server_rank: Optional[int] = None, client_ranks=None, graph: bool = True, groups=None,
-                 ship_amax: bool = True):
+                 ship_amax: bool = True, images: bool = False):
         self.stage, self.rank, self.world = stage, rank, world
+        # images (dense exchange only): the client ships its x3 split images (act16, the same 86,528 B a
+        # sample as the f32 cut) + per-sample max instead of the f32 act, and the server runs the image
+        # forward (conv2_fwd_pool_x3i) instead of staging + splitting f32 rows in-kernel
+        self.images = bool(images)
+        if self.images and (compress not in (False, None) or not ship_amax):
+            raise ValueError("images=True is the dense exchange with the per-sample max: compress=False, ship_amax=True")
         self.server_rank = world - 1 if server_rank is None else server_rank
         self.client_ranks = list(range(world - 1)) if client_ranks is None else list(client_ranks)
         self.nclients = len(self.client_ranks)
@@ -390,7 +399,8 @@ class Hub:
         dev = x.device
         srv = self.server_rank
         fw, bw = self.groups
-        act = self._buf("act", (B, 32, 26, 26), torch.float32, dev)
+        act = None if self.images else self._buf("act", (B, 32, 26, 26), torch.float32, dev)
+        img = self._buf("img", (B * IMG_BYTES,), torch.uint8, dev) if self.images else None
         cut = self._buf("cut", (B, 32, 26, 26), torch.float32, dev)
         ship = self.ship_amax
         amx = self._buf("amax", (B,), torch.float32, dev) if ship else None
@@ -406,6 +416,11 @@ class Hub:
         counts = self._buf("counts_host", (m,), torch.int32, dev, pin=True) if codec is not None else None
         for k in range(m):
             sl = slice(k * b, (k + 1) * b)
+            if img is not None:
+                isl = img[k * b * IMG_BYTES:(k + 1) * b * IMG_BYTES]
+                c.forward_images(x[sl], isl, amx[sl])
+                sends += [isend(isl, srv, fw), isend(y[sl], srv, fw), isend(amx[sl], srv, fw)]
+                continue
             c.forward(x[sl], out=act[sl])
             if ship:
                 if getattr(c, "_act_amax", None) is not None:
@@ -441,14 +456,14 @@ class Hub:
                 recvs[k].wait()
             if codec is not None:
                 codec.unpack(cut[sl], bufs[k], vals=gv[k])
-            c.backward(cut[sl], x=x[sl], act=act[sl], accumulate=k > 0)
+            c.backward(cut[sl], x=x[sl], act=None if act is None else act[sl], accumulate=k > 0)
         for w in sends:
             w.wait()
         if self.nclients > 1:
             dist.all_reduce(c.grads, group=self.client_group)
         c.step()
         extra = y.numel() * 8 + (B * 4 if ship else 0)
-        self.dense_bytes = 2 * act.numel() * 4 + extra
+        self.dense_bytes = 2 * cut.numel() * 4 + extra
         self.exchange_bytes = (self.dense_bytes if codec is None else
                                m * 4 + sum(bufs[k][0].numel() * 4 + 2 * totals[k] * 4 for k in range(m)) + extra)
         self.global_step += 1
@@ -462,7 +477,7 @@ class Hub:
         b, G = B // m, nc * B
         CH = nc * b
         n = b * 32 * 26 * 26
-        acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
+        acts = self._inputs(G, device)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         parts = self._buf("loss_parts", (m,), torch.float32, device)
@@ -475,13 +490,23 @@ class Hub:
         kw = {}
         if self.ship_amax and self._amax_kw:
             kw["act_amax"] = self._buf("amax", (G,), torch.float32, device)[ch]
-        _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
+        if self.images:
+            kw["act16"] = acts[k * CH * IMG_BYTES:(k + 1) * CH * IMG_BYTES]
+            _, loss_i = s.compute(None, labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
+        else:
+            _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         _loss_sum(loss_i, 1.0 / G, parts[k:k + 1])
         if codec is not None:
             for ci in range(nc):
                 bk = codec.buffers(("s", ci, k), n, device)
                 codec.pack(cuts[k * CH + ci * b:k * CH + (ci + 1) * b], bk,
                            vals=self._buf(("gvals", ci, k), (n,), torch.float32, device))
+
+    def _inputs(self, G, device):
+        """The server's receive buffer of the cut: f32 act [G, 32, 26, 26], or the images' bytes."""
+        if self.images:
+            return self._buf("imgs", (G * IMG_BYTES,), torch.uint8, device)
+        return self._buf("acts", (G, 32, 26, 26), torch.float32, device)
 
     def _graphed(self, device) -> bool:
         return self.graph and torch.device(device).type == "cuda"
@@ -492,7 +517,7 @@ class Hub:
         if not self._graphed(device) or all((k, B, codec is not None) in self._graphs for k in range(self.micro)):
             return
         G = self.nclients * B
-        self._buf("acts", (G, 32, 26, 26), torch.float32, device).zero_()
+        self._inputs(G, device).zero_()
         self._buf("labels", (G,), torch.int64, device).zero_()
         if self.ship_amax:
             self._buf("amax", (G,), torch.float32, device).zero_()
@@ -528,7 +553,7 @@ class Hub:
         n = b * 32 * 26 * 26
         fw, bw = self.groups
         ship = self.ship_amax
-        acts = self._buf("acts", (G, 32, 26, 26), torch.float32, device)
+        acts = self._inputs(G, device)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         amx = self._buf("amax", (G,), torch.float32, device) if ship else None
@@ -545,7 +570,8 @@ class Hub:
             for ci, cr in enumerate(self.client_ranks):
                 for k in range(m):
                     sl = part(k, ci)
-                    reqs[ci, k] = [irecv(acts[sl], cr, fw), irecv(labels[sl], cr, fw)]
+                    asl = slice(sl.start * IMG_BYTES, sl.stop * IMG_BYTES) if self.images else sl
+                    reqs[ci, k] = [irecv(acts[asl], cr, fw), irecv(labels[sl], cr, fw)]
                     if ship:
                         reqs[ci, k].append(irecv(amx[sl], cr, fw))
         else:
@@ -579,7 +605,7 @@ class Hub:
         for w in sends:
             w.wait()
         extra = labels.numel() * 8 + (G * 4 if ship else 0)
-        self.dense_bytes = 2 * acts.numel() * 4 + extra
+        self.dense_bytes = 2 * cuts.numel() * 4 + extra
         self.exchange_bytes = (self.dense_bytes if codec is None else
                                nc * m * 4 + sum(codec.buffers(("s", ci, k), n, device)[0].numel() * 4 + 2 * t * 4
                                                 for (ci, k), t in totals.items()) + extra)
@@ -598,13 +624,13 @@ class Pipeline(Hub):
     the micro-batches and step once per batch (= the reference step at batch B)."""
 
     def __init__(self, stage, role: str, peer: int, micro: int = 4, compress=True, graph: bool = True,
-                 groups=None, ship_amax: bool = True):
+                 groups=None, ship_amax: bool = True, images: bool = False):
         assert role in ("client", "server")
         me = dist.get_rank()
         super().__init__(stage, me, dist.get_world_size(), None, micro, compress,
                          server_rank=peer if role == "client" else me,
                          client_ranks=[me] if role == "client" else [peer], graph=graph, groups=groups,
-                         ship_amax=ship_amax)
+                         ship_amax=ship_amax, images=images)
         self.role, self.peer = role, peer
 
 

@@ -207,6 +207,15 @@ class ClientStage:
         self._x, self._act, self._act_amax = x, act, amax
         return act
 
+    def forward_images(self, x: torch.Tensor, act16: torch.Tensor, act_amax: torch.Tensor) -> None:
+        """act = relu(conv1(x)) (client_part.py:114) written as the server's x3 operand into caller
+        buffers — act16 images (ops.conv2_act16_bytes(B) bytes) + the per-sample max — for the image
+        exchange of dist.Hub (images=True). No f32 act and no ReLU bit map: this client's backward
+        re-derives its mask from x."""
+        with TIMER("conv1_fwd"):
+            ops.conv1_fwd_x3(x, self.W1.detach(), self.b1.detach(), act_amax, act16)
+        self._x, self._act, self._act_amax, self._act16 = x, None, act_amax, act16
+
     def _slabs(self, cut_grad, x, act, tag="slabs"):
         x = self._x if x is None else x
         act = self._act if act is None else act

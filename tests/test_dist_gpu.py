@@ -489,3 +489,48 @@ def test_hub_server_graphs_survive_batch_size_changes(gpu, codec):
                                    for k in range(m) for ci in range(nc)]))
         torch.testing.assert_close(cuts[0], cuts[1], rtol=0, atol=0)
         torch.testing.assert_close(runs[0][0].stage.params, runs[1][0].stage.params, rtol=0, atol=0)
+
+
+def test_hub_image_exchange_matches_f32_cut_bitwise(gpu):
+    """dist.Hub(images=True): the server's chunk graphs fed with the client's x3 split images + maxima
+    (ClientStage.forward_images, what the receives deliver) equal the same server fed with the f32 cut
+    bit for bit — losses, every cut gradient and the parameters after the SGD step (the image forward
+    reads the images conv2_fwd_pool_x3 itself splits from the f32 act). K4 shape: 3 clients x 2 chunks."""
+    from splitcnn import dist as sd
+    from splitcnn import ops
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    assert ops.conv2_act16_bytes(1) == sd.IMG_BYTES
+    nc, m, B = 3, 2, 64
+    b, G = B // m, nc * B
+    data = SyntheticMNIST(5)
+    parts = [data.batch(b) for _ in range(m * nc)]
+    res = []
+    for images in (False, True):
+        a, s = init_models(seed=0)
+        hub = sd.Hub(ServerStage(s, device=gpu), rank=nc, world=nc + 1, micro=m, compress=False, images=images)
+        cl = ClientStage(a, device=gpu)
+        cl.emit_amax = True
+        hub._prepare(B, gpu, None)
+        inp = hub._inputs(G, gpu)
+        labels = hub._buf("labels", (G,), torch.int64, gpu)
+        amx = hub._buf("amax", (G,), torch.float32, gpu)
+        hub._buf("cuts", (G, 32, 26, 26), torch.float32, gpu)
+        hub._buf("loss_parts", (m,), torch.float32, gpu)
+        for k in range(m):
+            for ci in range(nc):
+                sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
+                x, y = parts[k * nc + ci]
+                if images:
+                    cl.forward_images(x.to(gpu), inp[sl.start * sd.IMG_BYTES:sl.stop * sd.IMG_BYTES], amx[sl])
+                else:
+                    cl.forward(x.to(gpu), out=inp[sl])
+                    amx[sl].copy_(cl._act_amax)
+                labels[sl].copy_(y.to(gpu))
+        for k in range(m):
+            hub._run_chunk(k, B, gpu, None)
+        hub.stage.step()
+        torch.cuda.synchronize()
+        res.append((hub._bufs["loss_parts"].clone(), hub.cuts_by_client(B).clone(), hub.stage.params.clone()))
+    for u, v in zip(*res):
+        assert torch.equal(u, v)

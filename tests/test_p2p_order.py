@@ -286,7 +286,7 @@ def _reference(P, batches):
     return P, losses
 
 
-def _run_hub(monkeypatch, nclients, micro, codec, shared, ship_amax=True):
+def _run_hub(monkeypatch, nclients, micro, codec, shared, ship_amax=True, images=False):
     sd, OC, OS, Data, P = _setup()
     world = nclients + 1
     fab = _Fabric(world, shared=shared)
@@ -299,7 +299,7 @@ def _run_hub(monkeypatch, nclients, micro, codec, shared, ship_amax=True):
         def fn():
             grp = sd.client_group_for(world)
             t = sd.Hub(OC(P), r, world, client_group=grp, micro=micro,
-                       compress=_TorchCodec() if codec else False, ship_amax=ship_amax)
+                       compress=_TorchCodec() if codec else False, ship_amax=ship_amax, images=images)
             for x, y in batches:
                 sl = slice(r * B, (r + 1) * B)
                 t.client_step(x[sl].contiguous(), y[sl].contiguous())
@@ -309,7 +309,7 @@ def _run_hub(monkeypatch, nclients, micro, codec, shared, ship_amax=True):
     def server():
         grp = sd.client_group_for(world)
         t = sd.Hub(OS(P), world - 1, world, client_group=grp, micro=micro,
-                   compress=_TorchCodec() if codec else False, ship_amax=ship_amax)
+                   compress=_TorchCodec() if codec else False, ship_amax=ship_amax, images=images)
         for _ in batches:
             t.server_step(B, torch.device("cpu"))
         out["server"] = {**t.stage.named(), "losses": [l for _, l in t.stage.losses]}
@@ -369,6 +369,25 @@ def test_codec_double_matches_dense(monkeypatch):
     for r in range(2):
         for k in a[r]:
             np.testing.assert_array_equal(a[r][k], b[r][k])
+
+
+@pytest.mark.parametrize("nclients,micro", [(1, 1), (1, 4), (3, 2)])
+def test_image_exchange_drains_and_matches_dense(monkeypatch, nclients, micro):
+    """The image exchange (Hub images=True: act16 bytes + per-sample max up, the cut gradient back) drains
+    under strict RCCL semantics for K3 / K4 and ends bit-identical to the dense f32 exchange (the oracle
+    stages carry the f32 act's bytes in the image buffer)."""
+    sd, *_ = _setup()
+    assert sd.IMG_BYTES == 32 * 26 * 26 * 4
+    fab, a, ref = _run_hub(monkeypatch, nclients, micro, False, True, images=True)
+    _check(a, ref, nclients)
+    _, b, _ = _run_hub(monkeypatch, nclients, micro, False, True)
+    for k in a["server"]:
+        np.testing.assert_array_equal(np.asarray(a["server"][k]), np.asarray(b["server"][k]))
+    for r in range(nclients):
+        for k in a[r]:
+            np.testing.assert_array_equal(a[r][k], b[r][k])
+    with pytest.raises(ValueError):
+        sd.Hub(None, 0, 2, compress=True, images=True, groups=(None, None))
 
 
 def test_widehub_drains_under_rccl_semantics(monkeypatch):
