@@ -230,18 +230,22 @@ def _worker(rank, world, port, topo, fixture, micro, outdir, compress=True):
     a, b = _models(fx)
     nsteps = int(fx["nsteps"])
     res = {}
+    images = compress == "images"   # the dense exchange of the client's x3 images
+    if images:
+        compress = False
     try:
         if topo == "pipeline":
             if rank == 0:
-                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=compress)
+                t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=compress, images=images)
             else:
-                t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=compress)
+                t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=compress, images=images)
             for s in range(1, nsteps + 1):
                 x = torch.from_numpy(fx[f"x_{s}"]).to(dev)
                 y = torch.from_numpy(fx[f"y_{s}"]).to(dev)
                 if rank == 0:
                     t.client_step(x, y)
-                    res[f"act_{s}"] = t._bufs["act"].cpu().numpy()
+                    if not images:
+                        res[f"act_{s}"] = t._bufs["act"].cpu().numpy()
                     res[f"params_{s}"] = t.stage.params.cpu().numpy()
                     res[f"grads_{s}"] = t.stage.grads.cpu().numpy()
                     res[f"bytes_{s}"] = np.array([t.exchange_bytes, t.dense_bytes])
@@ -260,12 +264,15 @@ def _worker(rank, world, port, topo, fixture, micro, outdir, compress=True):
             y = torch.from_numpy(fx["y_1"]).to(dev)
             B = x.shape[0] // nc
             if rank < nc:
-                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=compress)
+                t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=compress,
+                           images=images)
                 sl = slice(rank * B, (rank + 1) * B)
                 t.client_step(x[sl].contiguous(), y[sl].contiguous())
-                res["act_1"] = t._bufs["act"].cpu().numpy()
+                if not images:
+                    res["act_1"] = t._bufs["act"].cpu().numpy()
             else:
-                t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=compress)
+                t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=compress,
+                           images=images)
                 t.server_step(B, dev)
                 res["cut_1"] = t.cuts_by_client(B).cpu().numpy()
                 torch.cuda.synchronize()
@@ -534,3 +541,17 @@ def test_hub_image_exchange_matches_f32_cut_bitwise(gpu):
         res.append((hub._bufs["loss_parts"].clone(), hub.cuts_by_client(B).clone(), hub.stage.params.clone()))
     for u, v in zip(*res):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("topo,world,micro,fixture", [("pipeline", 2, 2, "split_step_b4.npz"),
+                                                      ("hub", 3, 2, "split_step_b12.npz")])
+def test_image_exchange_bit_identical_to_dense(gpu, tmp_path, topo, world, micro, fixture):
+    """The image exchange (images=True: the client's x3 split images + per-sample max up, the f32 cut
+    gradient back) vs the dense f32 exchange, multi-process: every rank's weights, gradients, cut
+    gradients and losses are BIT-identical and the same bytes moved."""
+    dense = _spawn(world, topo, fixture, micro, tmp_path / "dense", compress=False)
+    imgs = _spawn(world, topo, fixture, micro, tmp_path / "images", compress="images")
+    for r in range(world):
+        for k in imgs[r]:
+            assert np.array_equal(dense[r][k], imgs[r][k]), (r, k)
+        assert set(dense[r]) - set(imgs[r]) <= {k for k in dense[r] if k.startswith("act_")}

@@ -1,2 +1,2 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 300 python tools/x3_ab.py build_abl/base9.so build_abl/fcwt128.so build_abl/fcwt768.so --ops fcw --rounds 30 > gpurun_out/ab.txt 2>&1; rc=$?; cat gpurun_out/ab.txt; exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_dist_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/t.txt 2>&1; rc=$?; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/t.txt | tail -30; exit $rc
