@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU (per-client) batch")
     ap.add_argument("--topology", default="auto", choices=["auto", "replicated", "pipeline", "hub"])
     ap.add_argument("--micro", type=int, default=4, help="micro-batches of the pipeline / hub topologies")
+    ap.add_argument("--no-micro-trial", action="store_true",
+                    help="N > 1: time only --micro micro-batches in the exchange trial (default: also 2x --micro)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "dense", "codec"],
                     help="pipeline / hub cut exchange: auto = measure the link, then the faster of a short trial "
                          "of each; dense = fp32 cut + gradient; codec = the lossless sparse codec")
@@ -580,24 +582,31 @@ def run_distributed(args, out, rank, world, local):
         exch["prediction_ms_per_step"] = predict_exchange(nc if topo == "hub" else 1, B, peak)
         trials = {}
         built = {}
+        # micro-batch counts tried: a link-bound pipeline takes ~(1 + 1/m) x its link time, while each
+        # micro-batch adds fixed costs (p2p op latency, the codec's count round trip), so the link decides
+        micros = [args.micro] + ([2 * args.micro] if not args.no_micro_trial and B % (2 * args.micro) == 0 else [])
         for name, codec in (("dense", False), ("codec", True)):
             if forced is not None and codec != forced:
                 continue
-            progress(f"{topo} x{world}: {name} exchange trial")
-            f, tt, gb = build(topo, args.micro, codec)
-            dtt = timed(f, 3, 2, dev)
-            trials[name] = round(dtt / 3 * 1e3, 3)
-            built[name] = (f, tt, gb)
-        choice = min(trials, key=trials.get)
-        exch.update(choice=choice, trial_ms_per_step=trials,
-                    rule=("forced by flag" if forced is not None else
-                          "the faster of a 3-step trial of each (after 2 warm-up steps) on this topology"),
+            for m in micros:
+                key = f"{name}/m{m}"
+                progress(f"{topo} x{world}: {key} exchange trial")
+                f, tt, gb = build(topo, m, codec)
+                dtt = timed(f, 3, 2, dev)
+                trials[key] = round(dtt / 3 * 1e3, 3)
+                built[key] = (f, tt, gb, m)
+        best = min(trials, key=trials.get)
+        choice, micro = best.split("/")[0], built[best][3]
+        exch.update(choice=choice, micro_batches=micro, trial_ms_per_step=trials,
+                    rule=("exchange forced by flag; " if forced is not None else "") +
+                         "the fastest of a 3-step trial (after 2 warm-up steps) of each exchange x micro-batch count "
+                         "on this topology",
                     prediction_agrees=(min(exch["prediction_ms_per_step"], key=exch["prediction_ms_per_step"].get)
                                        == choice) if peak else None)
-        fn, t, global_batch = built[choice]
-        for name in list(built):
-            if name != choice:
-                del built[name]
+        fn, t, global_batch, _ = built[best]
+        for key in list(built):
+            if key != best:
+                del built[key]
         torch.cuda.empty_cache()
 
     # 3. the headline
@@ -609,7 +618,7 @@ def run_distributed(args, out, rank, world, local):
                      "graph": bool(getattr(t, "graph", False))}
     out["scaling"] = "weak"
     if topo != "replicated":
-        out["config"]["micro_batches"] = args.micro
+        out["config"]["micro_batches"] = exch["micro_batches"]
         out["config"]["per_client_batch"] = B
         out["config"]["cut_exchange"] = codec_label[exch["choice"] == "codec"]
         moved, dense = wire(t)
