@@ -48,9 +48,23 @@ s = torch.cuda.current_stream().cuda_stream
 p = lambda t: P(t.data_ptr())  # noqa: E731
 FLOP = 150_994_944 * B
 
+# the head (dropout p = 0.25 as WideServerStage: keep iff hash >= 2^30, kept values x 4/3)
+wf8 = torch.randn(10 * 16384, device=dev, generator=g) * 0.01
+bfc = torch.randn(10, device=dev, generator=g) * 0.01
+stepc = torch.zeros(1, dtype=torch.int32, device=dev)
+hlog = torch.empty(B, 10, device=dev)
+hdl = torch.randn(B, 10, device=dev, generator=g) / B
+hdcut = torch.empty_like(cut)
+
 libs = []
 for path in args.libs:
     L = ctypes.CDLL(path)
+    L.slk_wide_head_work.restype = ctypes.c_int
+    L.slk_wide_head_nslab.restype = ctypes.c_int
+    L.slk_wide_head_fwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] * 2 + [ctypes.c_int] * 2 + [P]
+    L.slk_wide_head_bwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] * 2 + [ctypes.c_int] * 2 + [P]
+    L._hwork = torch.empty(L.slk_wide_head_work(B), device=dev)
+    L._hslabs = torch.empty(L.slk_wide_head_nslab(B), 163850, device=dev)
     libs.append(L)
 
 
@@ -65,6 +79,10 @@ def calls(L):
         "conv2_wgrad": lambda: L.slk_wide_conv2_wgrad(p(dp2), p(code2), p(a1), p(slabs), B, P(s)),
         "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1), p(out_da1m), B, P(s)),
         "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
+        "head_fwd": lambda: L.slk_wide_head_fwd(p(cut), p(wf8), p(bfc), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hlog),
+                                                p(L._hwork), 0, B, P(s)),
+        "head_bwd": lambda: L.slk_wide_head_bwd(p(cut), p(wf8), p(hdl), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hdcut),
+                                                p(L._hslabs), 0, B, P(s)),
     }
 
 
