@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--flush", action="store_true",
+                    help="read 600 MB before every timed call (outside the timing): operands come from HBM, "
+                         "not the 256 MB Infinity Cache, as inside the step")
     args = ap.parse_args()
     from splitcnn import ops
     from splitcnn.data import SyntheticMNIST, init_models
@@ -134,8 +137,13 @@ def main():
         for f in cases.values():
             assert f() == 0
     torch.cuda.synchronize()
+    # a READ of 600 MB evicts with clean lines (a write would leave dirty ones the next kernel pays for)
+    flushbuf = torch.ones(150_000_000, device=dev) if args.flush else None
+    flushout = torch.empty((), device=dev) if args.flush else None
     for _ in range(args.rounds):
         for k, f in cases.items():
+            if flushbuf is not None:
+                torch.sum(flushbuf, dim=0, out=flushout)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             f()
