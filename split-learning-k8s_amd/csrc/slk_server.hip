@@ -514,16 +514,33 @@ extern "C" int slk_conv2_wgrad_direct_nslab(int B) { return B > 0 ? (2 * B < C2W
 // (377 MB of L2 reads per pass at B = 4096) and its logits pass read pooled at 2.7 TB/s.
 // dpooled on the VALU: thread = float4 column k4 with W3's 10 float4 of it in registers, every sample's
 // row stored as 1-KiB-contiguous wave stores (the 10-term fmaf chain per output, classes in order).
+#ifndef SLK_FCH_CK
+#define SLK_FCH_CK 64
+#endif
+#ifndef SLK_FCH_NS
+#define SLK_FCH_NS 2
+#endif
 constexpr int FCH_S = 16, FCH_T = 512, FCH_W = FCH_T / 64;
 constexpr int FCH_KW = P_SAMPLE / FCH_W;  // 1152 features per wave
-constexpr int FCH_CK = 64;                // features per chunk
+constexpr int FCH_CK = SLK_FCH_CK;        // features per chunk (64)
+constexpr int FCH_NS = SLK_FCH_NS;        // LDS slots per wave = chunks in flight + 1 (2)
 constexpr int FCH_NCH = FCH_KW / FCH_CK;  // 18
 constexpr int FCH_ROW = FCH_CK * 4 + 32;  // 288-B LDS rows: (72 s + 4 kg) dwords are 16 distinct 4-bank slots per lane group
 constexpr int FCH_A = FCH_S * FCH_ROW;    // 4,608 B of sample rows (4 full DMA pieces + half of a fifth)
-constexpr int FCH_SLOT = FCH_A + 3 * 1024;  // + W3 rows (10 x 288 = 2,880 B in 3 DMA pieces)
+constexpr int FCH_PA = (FCH_A + 1023) / 1024, FCH_ALAST = FCH_A - 1024 * (FCH_PA - 1);
+constexpr int FCH_PW = (NCLS * FCH_ROW + 1023) / 1024;  // W3 rows (10 x 288 = 2,880 B in 3 DMA pieces)
+constexpr int FCH_NDMA = FCH_PA + FCH_PW;               // DMA instructions per chunk (8)
+constexpr int FCH_SLOT = FCH_A + FCH_PW * 1024;
+constexpr int FCH_U = 64 / FCH_CK;                      // chunks per 64 features (accumulator rotation)
 constexpr int FC_K4 = P_SAMPLE / 4;         // 2304 float4 columns
-static_assert(P_SAMPLE % FCH_W == 0 && FCH_KW % FCH_CK == 0 && FCH_NCH >= 2 && NCLS * FCH_ROW <= 3 * 1024 &&
-                  FCH_A > 4096 && FCH_A <= 5120, "fc head tiling");
+static_assert(P_SAMPLE % FCH_W == 0 && FCH_KW % 64 == 0 && (FCH_CK == 64 || FCH_CK == 32) && FCH_NS >= 2 &&
+                  FCH_NS <= 4 && FCH_NCH >= FCH_NS && FCH_ALAST % 16 == 0 && FCH_NDMA * (FCH_NS - 1) <= 63,
+              "fc head tiling");
+
+template <int N>
+__device__ __forceinline__ void fch_vmwait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 template <int MODE>
 __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
@@ -531,7 +548,7 @@ __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
     const int64_t* __restrict__ labels, float* __restrict__ logits, float* __restrict__ loss_i,
     float* __restrict__ dlogits, float* __restrict__ dpooled, float grad_scale, int* err_flag, int B,
     float* __restrict__ dp_amax) {
-    __shared__ __attribute__((aligned(1024))) char smem[(MODE & 1) ? FCH_W * 2 * FCH_SLOT : 16];
+    __shared__ __attribute__((aligned(1024))) char smem[(MODE & 1) ? FCH_W * FCH_NS * FCH_SLOT : 16];
     __shared__ __attribute__((aligned(16))) f32x4 red[(MODE & 1) ? FCH_W * 64 : 1];
     __shared__ float zl[FCH_S][NCLS];
     __shared__ float dl[FCH_S][NCLS];
@@ -542,35 +559,36 @@ __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
     const int ns = min(FCH_S, B - s0);
 
     if constexpr ((MODE & 1) != 0) {
-        char* const slots = smem + wave * 2 * FCH_SLOT;
+        char* const slots = smem + wave * FCH_NS * FCH_SLOT;
         const int kb = wave * FCH_KW;
         // DMA lane offsets: piece j fills slot bytes [1024 j, 1024 j + 1024), lane l the 16 B at
-        // X = 1024 j + 16 l = row X / 288, byte X % 288 (pad bytes and rows past the batch: a valid dummy)
-        uint32_t va[5], vw[3];
+        // X = 1024 j + 16 l = row X / FCH_ROW, byte X % FCH_ROW (pad bytes and rows past the batch: a valid dummy)
+        uint32_t va[FCH_PA], vw[FCH_PW];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
+        for (int j = 0; j < FCH_PA; ++j) {
             const int X = 1024 * j + 16 * lane, r = X / FCH_ROW, off = X - (X / FCH_ROW) * FCH_ROW;
             va[j] = (r < FCH_S && off < FCH_CK * 4) ? (uint32_t)(min(r, ns - 1) * P_SAMPLE * 4 + off) : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < FCH_PW; ++j) {
             const int X = 1024 * j + 16 * lane, r = X / FCH_ROW, off = X - (X / FCH_ROW) * FCH_ROW;
             vw[j] = (r < NCLS && off < FCH_CK * 4) ? (uint32_t)(r * P_SAMPLE * 4 + off) : 0u;
         }
-        auto issue = [&](int c) {  // 8 DMA instructions per chunk (the fifth A piece: lanes 0-31)
-            const uint32_t la = lds_u32(slots + (c & 1) * FCH_SLOT);
+        auto issue = [&](int c) {  // FCH_NDMA DMA instructions per chunk (the last A piece: lanes < FCH_ALAST / 16)
+            const uint32_t la = lds_u32(slots + (c % FCH_NS) * FCH_SLOT);
             const float* pa = pooled + (size_t)s0 * P_SAMPLE + kb + c * FCH_CK;
             const float* pw = W3 + kb + c * FCH_CK;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) glds16_so(pa, va[j], la + 1024 * j);
-            if (lane < (FCH_A - 4096) / 16) glds16_so(pa, va[4], la + 4096);
+            for (int j = 0; j < FCH_PA - 1; ++j) glds16_so(pa, va[j], la + 1024 * j);
+            if (lane < FCH_ALAST / 16) glds16_so(pa, va[FCH_PA - 1], la + 1024 * (FCH_PA - 1));
 #pragma unroll
-            for (int j = 0; j < 3; ++j) glds16_so(pw, vw[j], la + FCH_A + 1024 * j);
+            for (int j = 0; j < FCH_PW; ++j) glds16_so(pw, vw[j], la + FCH_A + 1024 * j);
         };
-        issue(0);
-        issue(1);
+#pragma unroll
+        for (int c = 0; c < FCH_NS; ++c) issue(c);
         // A fragment: lane (sample s16, group kg) holds features 16 blk + 4 kg + i; B: lane (class, kg) the
-        // same features of W3 row min(class, 9) (classes 10-15: duplicates, never stored)
+        // same features of W3 row min(class, 9) (classes 10-15: duplicates, never stored). Accumulator
+        // (feature / 16) % 4 for every chunk size, so the sum order (and the result) does not depend on FCH_CK.
         const int s16 = lane & 15, kg = lane >> 4, nrow = min(s16, NCLS - 1);
         f32x4 acc[4];
 #pragma unroll
@@ -579,22 +597,30 @@ __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
             slk_keep(acc[blk]);
         }
 #pragma unroll 2
-        for (int c = 0; c < FCH_NCH; ++c) {
-            if (c + 1 < FCH_NCH) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // chunk c landed, c + 1 in flight
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const char* sl = slots + (c & 1) * FCH_SLOT;
-            f32x4 a[4], w[4];
+        for (int cc = 0; cc < FCH_NCH; cc += FCH_U) {
 #pragma unroll
-            for (int blk = 0; blk < 4; ++blk) {
-                a[blk] = *reinterpret_cast<const f32x4*>(sl + s16 * FCH_ROW + 64 * blk + 16 * kg);
-                w[blk] = *reinterpret_cast<const f32x4*>(sl + FCH_A + nrow * FCH_ROW + 64 * blk + 16 * kg);
+            for (int u = 0; u < FCH_U; ++u) {
+                const int c = cc + u, left = FCH_NCH - 1 - c;  // chunks issued after c
+                if (left >= FCH_NS - 1) fch_vmwait<FCH_NDMA * (FCH_NS - 1)>();  // chunk c landed
+                else if (FCH_NS > 3 && left == 2) fch_vmwait<FCH_NDMA * 2>();
+                else if (FCH_NS > 2 && left == 1) fch_vmwait<FCH_NDMA>();
+                else fch_vmwait<0>();
+                const char* sl = slots + (c % FCH_NS) * FCH_SLOT;
+                f32x4 a[FCH_CK / 16], w[FCH_CK / 16];
+#pragma unroll
+                for (int blk = 0; blk < FCH_CK / 16; ++blk) {
+                    a[blk] = *reinterpret_cast<const f32x4*>(sl + s16 * FCH_ROW + 64 * blk + 16 * kg);
+                    w[blk] = *reinterpret_cast<const f32x4*>(sl + FCH_A + nrow * FCH_ROW + 64 * blk + 16 * kg);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before chunk c + FCH_NS overwrites it
+                if (c + FCH_NS < FCH_NCH) issue(c + FCH_NS);
+#pragma unroll
+                for (int blk = 0; blk < FCH_CK / 16; ++blk)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        acc[u * (FCH_CK / 16) + blk] =
+                            __builtin_amdgcn_mfma_f32_16x16x4f32(a[blk][i], w[blk][i], acc[u * (FCH_CK / 16) + blk], 0, 0, 0);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before chunk c + 2 overwrites it
-            if (c + 2 < FCH_NCH) issue(c + 2);
-#pragma unroll
-            for (int blk = 0; blk < 4; ++blk)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[blk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[blk][i], w[blk][i], acc[blk], 0, 0, 0);
         }
         // D[4 (lane >> 4) + r][lane & 15] = (sample, class) partial over this wave's features
         red[wave * 64 + lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
