@@ -302,7 +302,7 @@ int slk_wide_conv3_fwd(const uint16_t* p2, const uint16_t* w3f, const float* b3,
  * scaled by keep_scale), fc forward, cross-entropy forward+backward (dlogits scaled by grad_scale), the
  * cut gradient dcut = keep * keep_scale * dlogits @ Wf (bf16, C8) and the fc weight-gradient slabs
  * [slk_wide_head_nslab(B)][163850] = [dWf (torch layout) | dbf]. wf8 = slk_wide_fc_shadow(Wf);
- * work = slk_wide_head_work(B) floats of scratch; b0 = global index of sample 0 (micro-batches and
+ * work = slk_wide_head_work(B) floats of scratch (the step's dropout bits); b0 = global index of sample 0 (micro-batches and
  * SplitFed slices of one step draw the dropout mask of the concatenated batch). Replaces
  * server_part.py:48-51 + the cut-gradient return (:57) for the widened model. */
 int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels, const int* step,
@@ -312,8 +312,8 @@ int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const 
 int slk_wide_head_nslab(int B);
 int slk_wide_head_work(int B);
 /* slk_wide_head split at the loss, for the module path (WideModelPartB.forward -> criterion ->
- * loss.backward(), server_part.py:48-51): _fwd writes the logits (dropout + fc, same arithmetic and
- * partial order as slk_wide_head); _bwd takes dlogits from any loss and writes dcut and the fc slabs
+ * loss.backward(), server_part.py:48-51): _fwd writes the logits (dropout + fc, the same kernel and
+ * sum order as slk_wide_head, so bit-identical logits); _bwd takes dlogits from any loss and writes dcut and the fc slabs
  * exactly as slk_wide_head's last stage. */
 int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step, unsigned seed,
                       unsigned keep_threshold, float keep_scale, float* logits, float* work, int b0, int B,

@@ -54,29 +54,21 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
-// The head as three launches over a (feature slice x sample group) grid, so every fc weight is read
-// into registers once per workgroup and reused over 64 samples (the weight matrix is 655 KB: re-read
-// per handful of samples it, not the cut, was the traffic):
-//   head_logits : thread = one 8-feature chunk of a 2048-feature slice, weights in registers; per
-//                 sample: dropout, 80 FMAs, wave reduction -> partial logits [B][32][10] (workspace)
-//   head_ce     : thread = sample; fixed-order sum of the 32 partials + bias, cross-entropy fwd/bwd
-//   head_back   : same grid; per sample the cut gradient chunk (bf16) and the fc weight-gradient
-//                 accumulation (80 registers) -> one slab per sample group [dWf | dbf]
+// The training step's head is two launches: wide_head16_kernel (logits on the f32 MFMA, cross-entropy
+// and the cut gradient, 16 samples per workgroup) and wide_head_back_kernel<false> (the fc weight
+// gradient over a (feature slice x sample group) grid: thread = one 8-feature chunk of a 2048-feature
+// slice accumulating 80 products over HSG samples -> one slab per sample group [dWf | dbf]).
+// The module path's backward (slk_wide_head_bwd) is wide_head_back_kernel<true>, which also writes
+// the cut gradient with the same per-element formula (dcut_chunk).
 constexpr int HSLICE = 8;            // 2048-feature slices (256 chunks each)
 #ifndef SLK_HSG
 #define SLK_HSG 64
 #endif
 constexpr int HSG = SLK_HSG;         // samples per group (= per fc weight-gradient slab)
-constexpr int HPART = HSLICE * 4;    // partial logits per sample (slices x waves)
-#ifndef SLK_HSG_L
-#define SLK_HSG_L 32
-#endif
 #ifndef SLK_HEAD_PF
 #define SLK_HEAD_PF 1
 #endif
 constexpr int HPF = SLK_HEAD_PF;     // samples' cut chunks in flight ahead of the one in use (A/B: 2 and 4 no gain)
-constexpr int HSG_L = SLK_HSG_L;     // samples per group of the logits pass (no slab: free to differ;
-                                     // A/B via bench: 64 -> 0.193 ms head, 32 -> 0.177, 16 -> 0.175 but a slower step)
 
 __device__ __forceinline__ void load_w(const float* __restrict__ wf8, int fc, float (&w)[NC][8]) {
 #pragma unroll
@@ -101,106 +93,174 @@ __device__ __forceinline__ uint4 cut_chunk(const uint16_t* __restrict__ cut, int
     return b < B ? *reinterpret_cast<const uint4*>(cut + ((size_t)b * NCH + fc) * 8) : make_uint4(0, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256) void wide_head_logits_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
-                                                               const int* __restrict__ step_ptr, uint32_t seed,
-                                                               uint32_t thresh, float keep_scale,
-                                                               float* __restrict__ part, int b0, int B) {
-    const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int fc = slice * 256 + threadIdx.x;
+// cut gradient of one 8-feature chunk: (dlogits @ Wf) masked and scaled like the forward's dropout
+__device__ __forceinline__ uint4 dcut_chunk(const float (&w)[NC][8], const float (&dlr)[NC], uint32_t kb, float keep_scale) {
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) a = __builtin_fmaf(dlr[j], w[j][k], a);
+        o[k] = (kb >> k) & 1 ? a * keep_scale : 0.f;
+    }
+    return make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+}
+
+// The training step's head in ONE pass over the cut for 16 samples per workgroup (then
+// wide_head_back_kernel<false> for the fc weight gradient): logits on v_mfma_f32_16x16x4_f32
+// (A = 16 samples x 4 features, B = 4 features x 16 classes, 10 used), cross-entropy, and the cut
+// gradient from the dropout bits the logits phase left in LDS. Replaces head_logits (10 wave
+// reductions per sample and chunk slice) + head_ce + the cut-gradient half of head_back.
+// Wave w owns chunks [256 w, 256 w + 256); lane (s16, kg) loads chunk 256 w + 4 blk + kg of sample
+// s16 (16 contiguous bytes; 4 kg lanes = 64 B of a row) and the same chunk of Wf row min(s16, 9) (an
+// L2 hit: Wf is 655 KB for all workgroups); MFMA i of a block takes feature i of each lane's chunk.
+constexpr int WH_S = 16, WH_T = 512, WH_W = WH_T / 64;
+constexpr int WH_CPW = NCH / WH_W;  // 256 chunks per wave = 64 blocks of 4
+constexpr int WH_KBS = NCH + 16;    // LDS row stride of the dropout bits (16 rows x 4 dwords: 64 distinct banks)
+#ifndef SLK_WH_PF
+#define SLK_WH_PF 8
+#endif
+constexpr int WH_PF = SLK_WH_PF;    // blocks in flight per lane (cut + Wf registers)
+static_assert(NCH % WH_W == 0 && (WH_CPW / 4) % WH_PF == 0 && NCH % WH_T == 0, "head16 tiling");
+
+template <bool TRAIN>  // false: logits only (WideModelPartB.forward; labels .. dcut unused)
+__global__ __launch_bounds__(WH_T) void wide_head16_kernel(
+    const uint16_t* __restrict__ cut, const float* __restrict__ wf8, const float* __restrict__ bf,
+    const int64_t* __restrict__ labels, const int* __restrict__ step_ptr, uint32_t seed, uint32_t thresh,
+    float keep_scale, float grad_scale, float* __restrict__ logits, float* __restrict__ loss_i,
+    float* __restrict__ dlogits, uint16_t* __restrict__ dcut, uint8_t* __restrict__ kbits, int* __restrict__ err_flag,
+    int b0, int B) {
+    __shared__ __attribute__((aligned(16))) uint8_t kbl[WH_S * WH_KBS];
+    __shared__ __attribute__((aligned(16))) f32x4 red[WH_W * 64];
+    __shared__ float zl[WH_S][NC];
+    __shared__ float dls[WH_S][NC];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int s0 = blockIdx.x * WH_S, ns = min(WH_S, B - s0);
     const uint32_t step = (uint32_t)*step_ptr;
-    float w[NC][8];
-    load_w(wf8, fc, w);
-    const int b1 = min(B, (grp + 1) * HSG_L);
-    uint4 ring[HPF];
+    {
+        const int s16 = lane & 15, kg = lane >> 4, sl = min(s16, ns - 1);  // rows past the batch: never stored
+        const uint4* crow = reinterpret_cast<const uint4*>(cut + (size_t)(s0 + sl) * CUTF);
+        const float4* wrow = reinterpret_cast<const float4*>(wf8 + (size_t)min(s16, NC - 1) * CUTF);
+        const int cb = wave * WH_CPW + kg;
+        const int bs = b0 + s0 + sl;
+        uint4 cv[WH_PF];
+        float4 wv[WH_PF][2];
 #pragma unroll
-    for (int i = 0; i < HPF; ++i) ring[i] = cut_chunk(cut, grp * HSG_L + i, fc, b1);
+        for (int p = 0; p < WH_PF; ++p) {
+            cv[p] = crow[cb + 4 * p];
+            wv[p][0] = wrow[2 * (cb + 4 * p)];
+            wv[p][1] = wrow[2 * (cb + 4 * p) + 1];
+        }
+        f32x4 acc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            slk_keep(acc[q]);
+        }
 #pragma unroll 1
-    for (int b = grp * HSG_L; b < b1; ++b) {
-        const uint4 v = ring[0];
+        for (int blk = 0; blk < WH_CPW / 4; blk += WH_PF) {
 #pragma unroll
-        for (int i = 0; i + 1 < HPF; ++i) ring[i] = ring[i + 1];
-        ring[HPF - 1] = cut_chunk(cut, b + HPF, fc, b1);  // later samples' chunks in flight during this one
-        float d[8];
-        dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
-        float pj[NC];
+            for (int p = 0; p < WH_PF; ++p) {
+                const int ch = cb + 4 * (blk + p);
+                const uint4 v = cv[p];
+                const float wf[8] = {wv[p][0].x, wv[p][0].y, wv[p][0].z, wv[p][0].w,
+                                     wv[p][1].x, wv[p][1].y, wv[p][1].z, wv[p][1].w};
+                if (blk + WH_PF < WH_CPW / 4) {
+                    cv[p] = crow[ch + 4 * WH_PF];
+                    wv[p][0] = wrow[2 * (ch + 4 * WH_PF)];
+                    wv[p][1] = wrow[2 * (ch + 4 * WH_PF) + 1];
+                }
+                float d[8];
+                const uint32_t kb = dropped(v, bs, ch, step, seed, thresh, keep_scale, d);
+                if constexpr (TRAIN) kbl[s16 * WH_KBS + ch] = (uint8_t)kb;
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            float a = 0.f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a = __builtin_fmaf(d[k], w[j][k], a);
-            pj[j] = wave_sum(a);
+                for (int i = 0; i < 8; ++i) acc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(d[i], wf[i], acc[i & 3], 0, 0, 0);
+            }
         }
-        if (lane < NC) {
-            float v = pj[0];
+        // D[4 (lane >> 4) + r][lane & 15] = (sample, class) partial over this wave's chunks
+        red[wave * 64 + lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+    __syncthreads();
+    if (tid < 256) {
+        const int l = tid & 63, r = tid >> 6, n = l & 15, s = 4 * (l >> 4) + r;
+        float v = 0.f;
 #pragma unroll
-            for (int j = 1; j < NC; ++j) v = lane == j ? pj[j] : v;
-            part[((size_t)b * HPART + slice * 4 + wave) * NC + lane] = v;
+        for (int w = 0; w < WH_W; ++w) v += red[w * 64 + l][r];
+        if (n < NC) {
+            zl[s][n] = v + bf[n];
+            if (!TRAIN && s < ns) logits[(size_t)(s0 + s) * NC + n] = v + bf[n];
+        }
+    }
+    if constexpr (!TRAIN) return;
+    __syncthreads();
+    if (tid < WH_S) {  // cross-entropy of sample tid (wide_head_ce_kernel's formula)
+        const int s = tid;
+        if (s < ns) {
+            const int b = s0 + s;
+            float z[NC], m = -__builtin_inff();
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                z[j] = zl[s][j];
+                m = fmaxf(m, z[j]);
+            }
+            float se = 0.f;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) se += expf(z[j] - m);
+            const float lse = m + logf(se);
+            const int64_t y = labels[b];
+            const bool ok = y >= 0 && y < NC;
+            if (!ok && err_flag) atomicOr(err_flag, 1);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const float g = ok ? (expf(z[j] - lse) - (j == y ? 1.f : 0.f)) * grad_scale : __builtin_nanf("");
+                logits[(size_t)b * NC + j] = z[j];
+                dlogits[(size_t)b * NC + j] = g;
+                dls[s][j] = g;
+            }
+            loss_i[b] = ok ? lse - z[(int)y] : __builtin_nanf("");
+        }
+    }
+    __syncthreads();
+    // the dropout bits for wide_head_back_kernel<false> (kbits [B][2048]: 8 MB at B = 4096, so the
+    // weight-gradient pass reads them instead of re-hashing 8 features per chunk)
+#pragma unroll
+    for (int i = tid; i < WH_S * NCH / 16; i += WH_T) {
+        const int s = i / (NCH / 16), q = i - s * (NCH / 16);
+        if (s < ns)
+            reinterpret_cast<uint4*>(kbits + (size_t)(s0 + s) * NCH)[q] =
+                *reinterpret_cast<const uint4*>(kbl + s * WH_KBS + 16 * q);
+    }
+    // cut gradient: thread = chunk (4 per thread), Wf's 80 floats of it in registers, every sample's
+    // chunk stored as 1-KiB-contiguous wave stores
+#pragma unroll 1
+    for (int ch = tid; ch < NCH; ch += WH_T) {
+        float w[NC][8];
+        load_w(wf8, ch, w);
+#pragma unroll 1
+        for (int s = 0; s < ns; ++s) {
+            asm volatile("" ::: "memory");  // keeps the 16 x 10 dls reads from being hoisted out of the chunk loop
+            float dlr[NC];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) dlr[j] = dls[s][j];
+            *reinterpret_cast<uint4*>(dcut + ((size_t)(s0 + s) * NCH + ch) * 8) =
+                dcut_chunk(w, dlr, kbl[s * WH_KBS + ch], keep_scale);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void wide_head_ce_kernel(const float* __restrict__ part, const float* __restrict__ bf,
-                                                           const int64_t* __restrict__ labels, float grad_scale,
-                                                           float* __restrict__ logits, float* __restrict__ loss_i,
-                                                           float* __restrict__ dlogits, int* __restrict__ err_flag, int B) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    // partials of this sample: 32 x 10 contiguous floats, read 8 partials (20 float4) at a time so
-    // the loads are in flight together; summed per logit in partial order q = 0..31 from 0, then + bias
-    float z[NC], m = -__builtin_inff();
-#pragma unroll
-    for (int j = 0; j < NC; ++j) z[j] = 0.f;
-    const float4* p4 = reinterpret_cast<const float4*>(part + (size_t)b * HPART * NC);
-#pragma unroll
-    for (int q0 = 0; q0 < HPART; q0 += 8) {
-        float pv[8 * NC];
-#pragma unroll
-        for (int i = 0; i < 2 * NC; ++i) {
-            const float4 t = p4[q0 * NC / 4 + i];
-            pv[4 * i] = t.x; pv[4 * i + 1] = t.y; pv[4 * i + 2] = t.z; pv[4 * i + 3] = t.w;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-            for (int j = 0; j < NC; ++j) z[j] += pv[q * NC + j];
-    }
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        z[j] = z[j] + bf[j];
-        m = fmaxf(m, z[j]);
-    }
-    float se = 0.f;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) se += expf(z[j] - m);
-    const float lse = m + logf(se);
-    if (!labels) {  // forward only (the module path: WideModelPartB.forward, the loss comes later)
-#pragma unroll
-        for (int j = 0; j < NC; ++j) logits[(size_t)b * NC + j] = z[j];
-        return;
-    }
-    const int64_t y = labels[b];
-    const bool ok = y >= 0 && y < NC;
-    if (!ok && err_flag) atomicOr(err_flag, 1);
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        logits[(size_t)b * NC + j] = z[j];
-        dlogits[(size_t)b * NC + j] = ok ? (expf(z[j] - lse) - (j == y ? 1.f : 0.f)) * grad_scale : __builtin_nanf("");
-    }
-    loss_i[b] = ok ? lse - z[(int)y] : __builtin_nanf("");
-}
-
+template <bool DCUT>
 __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __restrict__ cut, const float* __restrict__ wf8,
                                                              const float* __restrict__ dlogits,
                                                              const int* __restrict__ step_ptr, uint32_t seed,
                                                              uint32_t thresh, float keep_scale,
-                                                             uint16_t* __restrict__ dcut, float* __restrict__ slabs, int b0,
-                                                             int B) {
+                                                             uint16_t* __restrict__ dcut, float* __restrict__ slabs,
+                                                             const uint8_t* __restrict__ kbits, int b0, int B) {
     const int slice = blockIdx.x % HSLICE, grp = blockIdx.x / HSLICE;
     const int fc = slice * 256 + threadIdx.x;
     const uint32_t step = (uint32_t)*step_ptr;
     float w[NC][8], acc[NC][8];
-    load_w(wf8, fc, w);
+    if constexpr (DCUT) load_w(wf8, fc, w);
 #pragma unroll
     for (int j = 0; j < NC; ++j)
 #pragma unroll
@@ -217,26 +277,25 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
         for (int i = 0; i + 1 < HPF; ++i) ring[i] = ring[i + 1];
         ring[HPF - 1] = cut_chunk(cut, b + HPF, fc, b1);
         float d[8];
-        const uint32_t kb = dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
+        uint32_t kb;
+        if constexpr (DCUT) {
+            kb = dropped(v, b0 + b, fc, step, seed, thresh, keep_scale, d);
+        } else {  // the forward's bits (wide_head16_kernel<true>), same formula as dropped()
+            kb = kbits[(size_t)b * NCH + fc];
+            unpack8(v, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = (kb >> k) & 1 ? d[k] * keep_scale : 0.f;
+        }
         const float* dl = dlogits + (size_t)b * NC;
         float dlr[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) dlr[j] = dl[j];
-        float o[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            float a = 0.f;
-#pragma unroll
-            for (int j = 0; j < NC; ++j) a = __builtin_fmaf(dlr[j], w[j][k], a);
-            o[k] = (kb >> k) & 1 ? a * keep_scale : 0.f;
-        }
 #pragma unroll
         for (int j = 0; j < NC; ++j)
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[j][k] = __builtin_fmaf(dlr[j], d[k], acc[j][k]);
         if (slice == 0 && threadIdx.x < NC) accb += dl[threadIdx.x];
-        const uint32_t ow[4] = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
-        *reinterpret_cast<uint4*>(dcut + ((size_t)b * NCH + fc) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        if constexpr (DCUT) *reinterpret_cast<uint4*>(dcut + ((size_t)b * NCH + fc) * 8) = dcut_chunk(w, dlr, kb, keep_scale);
     }
     float* slab = slabs + (size_t)grp * (NC * CUTF + NC);
     const int plane = fc >> 6, pix = fc & 63;
@@ -426,11 +485,7 @@ __global__ __launch_bounds__(256) void wide_fc_shadow_kernel(const float* __rest
 __global__ void tick_kernel(int* __restrict__ ctr) { *ctr += 1; }
 
 extern "C" int slk_wide_head_nslab(int B) { return B > 0 ? (B + HSG - 1) / HSG : 0; }
-extern "C" int slk_wide_head_work(int B) { return B > 0 ? B * HPART * NC : 0; }
-// CE: one sample per thread in 64-thread blocks, so B = 4096 spreads over 64 CUs instead of 16
-// (0.0168 -> 0.0074 ms per launch, rocprofv3). (Storing the forward's dropout bits for the backward
-// instead of re-hashing: back -8.7 us, logits +5 us — not kept.)
-constexpr int HCE_T = 64;
+extern "C" int slk_wide_head_work(int B) { return B > 0 ? B * (NCH / 4) : 0; }  // the dropout bits, B x 2048 B
 extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float* bf, const int64_t* labels,
                              const int* step, unsigned seed, unsigned keep_threshold, float keep_scale,
                              float grad_scale, float* logits, float* loss_i, float* dlogits, uint16_t* dcut,
@@ -441,12 +496,11 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
     if (B == 0) return 0;
     const int ng = slk_wide_head_nslab(B);
     hipStream_t st = slk_stream(stream);
-    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ((B + HSG_L - 1) / HSG_L)), dim3(256), 0, st, cut, wf8, step, seed,
-                       keep_threshold, keep_scale, work, b0, B);
-    hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + HCE_T - 1) / HCE_T), dim3(HCE_T), 0, st, work, bf, labels, grad_scale,
-                       logits, loss_i, dlogits, err_flag, B);
-    hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, dlogits, step, seed,
-                       keep_threshold, keep_scale, dcut, slabs, b0, B);
+    hipLaunchKernelGGL(wide_head16_kernel<true>, dim3((B + WH_S - 1) / WH_S), dim3(WH_T), 0, st, cut, wf8, bf, labels, step, seed,
+                       keep_threshold, keep_scale, grad_scale, logits, loss_i, dlogits, dcut, (uint8_t*)work, err_flag,
+                       b0, B);
+    hipLaunchKernelGGL(wide_head_back_kernel<false>, dim3(HSLICE * ng), dim3(256), 0, st, cut, wf8, dlogits, step, seed,
+                       keep_threshold, keep_scale, dcut, slabs, (const uint8_t*)work, b0, B);
     return slk_launch_status();
 }
 extern "C" int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step,
@@ -456,10 +510,8 @@ extern "C" int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const fl
     SLK_CHECK_ARG(((uintptr_t)work & 15) == 0);
     if (B == 0) return 0;
     hipStream_t st = slk_stream(stream);
-    hipLaunchKernelGGL(wide_head_logits_kernel, dim3(HSLICE * ((B + HSG_L - 1) / HSG_L)), dim3(256), 0, st, cut, wf8, step, seed,
-                       keep_threshold, keep_scale, work, b0, B);
-    hipLaunchKernelGGL(wide_head_ce_kernel, dim3((B + HCE_T - 1) / HCE_T), dim3(HCE_T), 0, st, work, bf, nullptr, 0.f, logits,
-                       nullptr, nullptr, nullptr, B);
+    hipLaunchKernelGGL(wide_head16_kernel<false>, dim3((B + WH_S - 1) / WH_S), dim3(WH_T), 0, st, cut, wf8, bf, nullptr, step,
+                       seed, keep_threshold, keep_scale, 0.f, logits, nullptr, nullptr, nullptr, nullptr, nullptr, b0, B);
     return slk_launch_status();
 }
 
@@ -468,8 +520,8 @@ extern "C" int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const fl
                                  int b0, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && dlogits && step && dcut && slabs);
     if (B == 0) return 0;
-    hipLaunchKernelGGL(wide_head_back_kernel, dim3(HSLICE * slk_wide_head_nslab(B)), dim3(256), 0, slk_stream(stream), cut,
-                       wf8, dlogits, step, seed, keep_threshold, keep_scale, dcut, slabs, b0, B);
+    hipLaunchKernelGGL(wide_head_back_kernel<true>, dim3(HSLICE * slk_wide_head_nslab(B)), dim3(256), 0, slk_stream(stream), cut,
+                       wf8, dlogits, step, seed, keep_threshold, keep_scale, dcut, slabs, nullptr, b0, B);
     return slk_launch_status();
 }
 

@@ -12,6 +12,7 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--cases", default="", help="comma-separated subset of the cases (default: all)")
 args = ap.parse_args()
 B = args.batch
 dev = torch.device("cuda:0")
@@ -65,7 +66,13 @@ for path in args.libs:
     L.slk_wide_head_bwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] * 2 + [ctypes.c_int] * 2 + [P]
     L._hwork = torch.empty(L.slk_wide_head_work(B), device=dev)
     L._hslabs = torch.empty(L.slk_wide_head_nslab(B), 163850, device=dev)
+    L.slk_wide_head.argtypes = [P] * 5 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float, ctypes.c_float] + [P] * 7 + [ctypes.c_int] * 2 + [P]
+    L._hout = {"logits": torch.empty(B, 10, device=dev), "loss_i": torch.empty(B, device=dev),
+               "dlogits": torch.empty(B, 10, device=dev), "dcut": torch.empty_like(cut),
+               "slabs": torch.empty(L.slk_wide_head_nslab(B), 163850, device=dev)}
     libs.append(L)
+hlab = torch.randint(0, 10, (B,), device=dev, generator=g)
+herr = torch.zeros(1, dtype=torch.int32, device=dev)
 
 
 def calls(L):
@@ -83,6 +90,10 @@ def calls(L):
                                                 p(L._hwork), 0, B, P(s)),
         "head_bwd": lambda: L.slk_wide_head_bwd(p(cut), p(wf8), p(hdl), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hdcut),
                                                 p(L._hslabs), 0, B, P(s)),
+        # the training step's head (forward + CE + cut gradient + fc weight-gradient slabs)
+        "head": lambda: L.slk_wide_head(p(cut), p(wf8), p(bfc), p(hlab), p(stepc), 7, 1 << 30, 4.0 / 3.0, 1.0 / B,
+                                        *(p(L._hout[k]) for k in ("logits", "loss_i", "dlogits", "dcut", "slabs")),
+                                        p(L._hwork), p(herr), 0, B, P(s)),
     }
 
 
@@ -90,6 +101,8 @@ res = {i: {} for i in range(len(libs))}
 for r in range(args.rounds):
     for i, L in enumerate(libs):
         for name, fn in calls(L).items():
+            if args.cases and name not in args.cases.split(","):
+                continue
             assert fn() == 0, name
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -99,7 +112,15 @@ for r in range(args.rounds):
             e1.record()
             torch.cuda.synchronize()
             res[i].setdefault(name, []).append(e0.elapsed_time(e1) / args.reps)
-out = {}
+torch.cuda.synchronize()
+chk = {}
+for i, L in enumerate(libs[1:], 1):  # the fused head's outputs vs the first library's
+    for k, t in L._hout.items():
+        ref = libs[0]._hout[k].float()
+        if k == "slabs":
+            t, ref = t.sum(0), ref.sum(0)
+        chk[f"{args.libs[i]}:{k}"] = float((t.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+out = {"check_vs_lib0": chk}
 for i, path in enumerate(args.libs):
     d = {}
     for name, v in res[i].items():
