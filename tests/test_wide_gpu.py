@@ -435,3 +435,35 @@ def test_pooled_gradient_routing_random_codes(gpu):
     dW1, db1 = W.conv3x3p1_wgrad(bf(f(x)), da1m)
     grad_close(g1[:1728].reshape(64, 3, 3, 3), dW1)
     grad_close(g1[1728:], db1)
+
+
+def test_wide_head_ragged_batch_vs_oracle(gpu):
+    """The step's head (wide_head16_kernel<true> + wide_head_back_kernel<false>) at a ragged B = 1000
+    (62.5 sixteen-sample workgroups, 15.6 weight-gradient groups) as micro-batch b0 = 3 of step 2, seed 5:
+    logits / loss / dlogits vs the fp64 oracle, the cut gradient within one bf16 ulp, the fc slabs' sum
+    vs the oracle's weight gradient, and the dropout bits the head hands the weight-gradient pass in
+    `work` equal to the oracle's mask (bit k of byte [b][chunk] = feature (plane * 8 + k) * 64 + pixel)."""
+    from splitcnn.wide import WideServerStage, _q, init_wide_models, nchw_to_c8
+    _, Bm = init_wide_models(seed=0)
+    s = WideServerStage(Bm, device=gpu, seed=5)
+    B, b0, step = 1000, 3, 2
+    gen = torch.Generator().manual_seed(9)
+    cut_nchw = torch.randn(B, 256, 8, 8, generator=gen).clamp_min(0).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), generator=gen)
+    s.step_ctr.fill_(step)
+    dcut, loss_i, sf = s.forward_backward(nchw_to_c8(cut_nchw).to(gpu), y.to(gpu), 1.0 / B, b0=b0)
+    work = s._b("work", (_q("slk_wide_head_work", B),), torch.float32)
+    torch.cuda.synchronize()
+    P = {k: _np(v) for k, v in s.model.state_dict().items()}
+    keep = W.dropout_keep(5, step, B, b0=b0)
+    sv = W.server_step(P, _np(cut_nchw), y.numpy(), keep)
+    grad_close(_np(s._logits), sv["logits"], rtol=1e-5)
+    np.testing.assert_allclose(_np(loss_i), sv["loss_i"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(_np(s._dlogits), sv["dlogits"], rtol=0, atol=2e-7)
+    bf16_close(_nchw(dcut), sv["dcut"])
+    g = _np(sf.sum(0))
+    grad_close(g[:163840].reshape(10, -1), sv["grads"]["fc.weight"])
+    grad_close(g[163840:], sv["grads"]["fc.bias"])
+    bits = work.view(torch.uint8)[:B * 2048].cpu().numpy().reshape(B, 2048)
+    want = np.packbits(keep.reshape(B, 32, 8, 64).transpose(0, 1, 3, 2), axis=-1, bitorder="little")
+    assert np.array_equal(bits, want.reshape(B, 2048))
