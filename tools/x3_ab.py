@@ -120,6 +120,29 @@ def main():
             cases[f"fc1 {tag}"] = (lambda L=L, lg=lg3: L.slk_fc_fwd(p(pooled), p(W3), p(b3), p(lg), B, st))
             cases[f"fc4 {tag}"] = (lambda L=L, dl=dl3, dpo=dpo3: L.slk_fc_dgrad(p(dl), p(W3), p(dpo), B, st))
             outs[f"fc {tag}3"] = dpo3
+        if "fcord" in args.ops.split(","):
+            # launch order of the server head + fc weight gradient: A = the step's (fused head, then
+            # fc_wgrad: pooled evicted by the head's own 151 MB dpooled write); B = logits, CE, fc_wgrad
+            # (pooled re-read while still in the Infinity Cache), dpooled last
+            for n in ("slk_fc_fwd", "slk_xent_fwd_bwd", "slk_fc_dgrad", "slk_fc_wgrad", "slk_fc_xent_amax",
+                      "slk_fc_wgrad_nslab"):
+                getattr(L, n).restype = ctypes.c_int
+            L.slk_fc_fwd.argtypes = [P] * 4 + [ctypes.c_int, P]
+            L.slk_xent_fwd_bwd.argtypes = [P] * 4 + [ctypes.c_float, P, ctypes.c_int, P]
+            L.slk_fc_dgrad.argtypes = [P] * 3 + [ctypes.c_int, P]
+            L.slk_fc_wgrad.argtypes = [P] * 3 + [ctypes.c_int, P]
+            L.slk_fc_xent_amax.argtypes = [P] * 9 + [ctypes.c_float, P, ctypes.c_int, P]
+            yo = y.to(dev)
+            oA = [torch.empty(B, 10, device=dev), torch.empty(B, device=dev), torch.empty(B, 10, device=dev),
+                  torch.empty_like(dp), torch.empty(B, device=dev), torch.empty(L.slk_fc_wgrad_nslab(B), 92170, device=dev)]
+            oB = [torch.empty_like(t) for t in oA]
+            cases[f"fcA {tag}"] = (lambda L=L, o=oA: L.slk_fc_xent_amax(
+                p(pooled), p(W3), p(b3), p(yo), p(o[0]), p(o[1]), p(o[2]), p(o[3]), p(o[4]), 1.0 / B, None, B, st)
+                | L.slk_fc_wgrad(p(o[2]), p(pooled), p(o[5]), B, st))
+            cases[f"fcB {tag}"] = (lambda L=L, o=oB: L.slk_fc_fwd(p(pooled), p(W3), p(b3), p(o[0]), B, st)
+                | L.slk_xent_fwd_bwd(p(o[0]), p(yo), p(o[1]), p(o[2]), 1.0 / B, None, B, st)
+                | L.slk_fc_wgrad(p(o[2]), p(pooled), p(o[5]), B, st) | L.slk_fc_dgrad(p(o[2]), p(W3), p(o[3]), B, st))
+            cases[f"fcwA {tag}"] = (lambda L=L, o=oA: L.slk_fc_wgrad(p(o[2]), p(pooled), p(o[5]), B, st))
         if "fcw" in args.ops.split(","):
             L.slk_fc_wgrad_nslab.restype = ctypes.c_int
             L.slk_fc_wgrad.restype = ctypes.c_int
