@@ -108,6 +108,9 @@ int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, float* loss_i, 
 /* dpooled = dlogits @ W3 (fc1 input gradient). Replaces the fc1 part of loss.backward()
  * (src/server_part.py:51). */
 int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpooled, int B, void* stream);
+/* slk_fc_dgrad that also writes dp_amax[b] = max |dpooled[b]|: the split head of the x3 step (logits,
+ * cross-entropy, fc1 weight gradient while pooled is still in the Infinity Cache, then this). */
+int slk_fc_dgrad_amax(const float* dlogits, const float* W3, float* dpooled, float* dp_amax, int B, void* stream);
 
 /* Fused server head: fc1 forward, cross-entropy forward+backward and fc1 input gradient in one
  * launch (pooled is read from HBM once for the logits and once, L2-hot, for nothing else).

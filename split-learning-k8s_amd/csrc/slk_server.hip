@@ -854,6 +854,18 @@ extern "C" int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpoole
     return slk_launch_status();
 }
 
+// slk_fc_dgrad + the per-sample max |dpooled| the x3 conv2 kernels scale by (fused, as slk_fc_xent_amax)
+extern "C" int slk_fc_dgrad_amax(const float* dlogits, const float* W3, float* dpooled, float* dp_amax, int B,
+                                 void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(dlogits && W3 && dpooled && dp_amax);
+    fc_head16_kernel<4><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
+        nullptr, W3, nullptr, nullptr, nullptr, nullptr, const_cast<float*>(dlogits), dpooled, 0.f,
+        nullptr, B, dp_amax);
+    return slk_launch_status();
+}
+
 extern "C" int slk_fc_xent(const float* pooled, const float* W3, const float* b3,
                            const int64_t* labels, float* logits, float* loss_i, float* dlogits,
                            float* dpooled, float grad_scale, int* err_flag, int B, void* stream) {

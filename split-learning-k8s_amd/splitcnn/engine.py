@@ -274,6 +274,11 @@ class ServerStage:
         # just read by it), conv2 wgrad before the dgrad. Defaults: the measured fastest order.
         self.fc_wgrad_early = False
         self.wgrad_first = False
+        # the head as logits + cross-entropy, fc1 wgrad, then dpooled (+ dp_amax): fc1 wgrad re-reads
+        # pooled while it is still in the Infinity Cache (the fused head's own 151 MB dpooled write
+        # evicts it); same kernels, bit-identical results (tools/x3_ab.py --ops fcord --flush: 0.1010 ->
+        # 0.0970 ms for head + fc1 wgrad from cold caches)
+        self.fc_split = True
         self._buf = _Buffers()
 
     def bind_grads(self, view: torch.Tensor):
@@ -320,13 +325,25 @@ class ServerStage:
             with TIMER("conv2_fwd_pool"):
                 pooled, code = ops.conv2_fwd_pool(act, W2, b2, pooled=pooled_b, code=code_b, impl=fi,
                                                   act_amax=act_amax, act16=act16)
-        with TIMER("fc_xent"):
-            _, loss_i, dlogits, dpooled = ops.fc_xent(
-                pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
-                loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
-                dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
+        split = self.fc_split and dp_amax is not None
+        if split:
+            with TIMER("fc_xent"):
+                logits = ops.fc_fwd(pooled, W3, b3, out=self._b("logits", (B, 10)))
+                loss_i, dlogits = ops.xent_fwd_bwd(logits, labels, grad_scale, loss_i=self._b("loss_i", (B,)),
+                                                   dlogits=self._b("dlogits", (B, 10)), err_flag=self.err_flag)
+            with TIMER("fc_wgrad"):
+                s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
+            dpooled = self._b("dpooled", (B, 64, 12, 12))
+            with TIMER("fc_dgrad"):
+                ops.fc_dgrad(dlogits, W3, out=dpooled.view(B, 9216), dp_amax=dp_amax)
+        else:
+            with TIMER("fc_xent"):
+                _, loss_i, dlogits, dpooled = ops.fc_xent(
+                    pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
+                    loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)),
+                    dpooled=self._b("dpooled", (B, 64, 12, 12)), err_flag=self.err_flag, dp_amax=dp_amax)
         # launch order dgrad -> wgrad -> fc wgrad (measured fastest: DESIGN.md §3a "Launch order")
-        if self.fc_wgrad_early:
+        if self.fc_wgrad_early and not split:
             with TIMER("fc_wgrad"):
                 s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
 
@@ -351,7 +368,7 @@ class ServerStage:
                 ops.conv2_dgrad(dpooled, code, W2, out=cut_grad, impl=di, dp_amax=dp_amax)
         if not self.wgrad_first:
             s2 = wgrad()
-        if not self.fc_wgrad_early:
+        if not self.fc_wgrad_early and not split:
             with TIMER("fc_wgrad"):
                 s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
         return cut_grad, loss_i, s2, s3

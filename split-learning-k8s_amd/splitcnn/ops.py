@@ -230,11 +230,16 @@ def xent_fwd_bwd(logits, labels, grad_scale, loss_i=None, dlogits=None, err_flag
     return loss_i, dlogits
 
 
-def fc_dgrad(dlogits, W3, out=None):
+def fc_dgrad(dlogits, W3, out=None, dp_amax=None):
+    """dp_amax (a [B] f32 tensor): also write the per-sample max |dpooled|, fused."""
     B = batch_of(dlogits, (10,), "dlogits")
     dpooled = _out(out, (B, 9216), dlogits, name="dpooled")
-    _lib.call("slk_fc_dgrad", _dev(dlogits, "dlogits"), _dev(W3, "fc1.weight", (10, 9216)),
-              _dev(dpooled, "dpooled"), B, _stream(dlogits))
+    if dp_amax is None:
+        _lib.call("slk_fc_dgrad", _dev(dlogits, "dlogits"), _dev(W3, "fc1.weight", (10, 9216)),
+                  _dev(dpooled, "dpooled"), B, _stream(dlogits))
+    else:
+        _lib.call("slk_fc_dgrad_amax", _dev(dlogits, "dlogits"), _dev(W3, "fc1.weight", (10, 9216)),
+                  _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)), B, _stream(dlogits))
     return dpooled
 
 

@@ -28,8 +28,10 @@ def main():
     X, Y = make_pool(B, 4, dev)
     variants = {}
     configs = {"x3": {}, "x3_unfused": {"fuse_client_backward": False}, "x3w": {"conv": "x3w"}, "f32": {"conv": "f32"}}
-    server_attrs = {"x3_fcw_early": {"fc_wgrad_early": True}, "x3_wgrad_first": {"wgrad_first": True},
-                    "x3_both": {"fc_wgrad_early": True, "wgrad_first": True}}
+    # the default splits the head (fc_split); the fused-head orders set it off
+    server_attrs = {"x3_fused_head": {"fc_split": False},
+                    "x3_fcw_early": {"fc_split": False, "fc_wgrad_early": True},
+                    "x3_wgrad_first": {"wgrad_first": True}}
     if args.order:
         configs = {"x3": {}, **{k: {} for k in server_attrs}}
     for name, kw in configs.items():
@@ -53,6 +55,12 @@ def main():
     for k, v in times.items():
         v.sort()
         print(f"{k:10s} median {v[len(v) // 2]:.4f} ms/step  min {v[0]:.4f}", flush=True)
+    if args.order:  # every order ran the same steps on the same batches: parameters must be bit-identical
+        ref = variants["x3"]
+        for k, tr in variants.items():
+            same = (torch.equal(tr.server.params, ref.server.params)
+                    and torch.equal(tr.client.params, ref.client.params))
+            print(f"{k:10s} parameters bit-identical to x3: {same}", flush=True)
 
 
 if __name__ == "__main__":
