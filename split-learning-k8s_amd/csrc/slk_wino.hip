@@ -19,12 +19,6 @@
 
 using namespace slk;
 
-// Profiling-only ablation bits (tools/build_variant.sh -DSLK_WINO_ABL=...): 1 = skip the input
-// transform (B operand = raw patch), 2 = skip the output transform (y = 4 raw accumulators).
-#ifndef SLK_WINO_ABL
-#define SLK_WINO_ABL 0
-#endif
-
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -204,162 +198,6 @@ constexpr int WF_CHUNKS = (WF_PIECES + 63) / 64;
 constexpr int WF_BSTR = WF_CHUNKS * 256;       // buffer stride: the last chunk writes a full KiB
 constexpr int WF_GRID = 256;                   // one workgroup per CU
 
-// The one-M-block-per-wave forward (round 1's v1, superseded by conv2_fwd_pool_wino2_kernel below)
-// is kept only as a profiling variant: tools/build_variant.sh NAME -DSLK_WINO_V1=1 (tools/ab_wino.py).
-#if SLK_WINO_V1
-__device__ __forceinline__ void wf_dma_band(const float* __restrict__ act, int u, const float* dst, int wave, int lane) {
-    const int b = u / 3, band = u - 3 * (u / 3);
-    const float* src = act + (size_t)b * A_SAMPLE + band * 8 * A_HW;
-    const uint32_t base = (uint32_t)(uintptr_t)dst;
-#pragma unroll 1
-    for (int c = wave; c < WF_CHUNKS; c += WF_WAVES) {
-        // lanes past the band end (last chunk) re-read the band's last piece into the pad
-        const int p = min(c * 64 + lane, WF_PIECES - 1);
-        const int ci = p / 65, k = p - 65 * (p / 65);
-        glds16(src + ci * A_PIX + 4 * k, __builtin_amdgcn_readfirstlane(base + c * 1024));
-    }
-}
-
-__global__ __launch_bounds__(WF_THREADS, 1) void conv2_fwd_pool_wino_kernel(
-    const float* __restrict__ act, const float* __restrict__ W2, const float* __restrict__ b2,
-    float* __restrict__ pooled, uint8_t* __restrict__ code, int B) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * WF_BSTR + C2];
-    float* bias_s = smem + 2 * WF_BSTR;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int li = lane & 15, lk = lane >> 4;
-    const int nunit = 3 * B;
-
-    int u = blockIdx.x;
-    if (u < nunit) wf_dma_band(act, u, smem, wave, lane);
-
-    // transformed filters of this lane's (co, ci) pairs
-    float uw[8][16];
-    {
-        const int co = 16 * wave + li;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const float* gp = W2 + (size_t)co * K2 + (4 * s + lk) * 9;
-            float g[9];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) g[k] = gp[k];
-            wino_filter(g, uw[s]);
-        }
-    }
-    if (tid < C2) bias_s[tid] = b2[tid];
-    wg_wait_vmcnt<0>();  // first band + filters landed
-
-    int buf = 0;
-#pragma unroll 1
-    for (; u < nunit; u += gridDim.x) {
-        // this unit's band has landed: its DMA was issued before the previous unit's 24 epilogue
-        // stores of this wave — and every wave is done reading the other buffer
-        wg_wait_vmcnt<16>();
-        lds_barrier();
-        const int nu = u + gridDim.x;
-        if (nu < nunit) wf_dma_band(act, nu, smem + (buf ^ 1) * WF_BSTR, wave, lane);
-        const float* img = smem + buf * WF_BSTR;
-        const float4 bv = reinterpret_cast<const float4*>(bias_s)[4 * wave + lk];
-        const int b = u / 3, band = u - 3 * (u / 3);
-        const auto prs = __builtin_amdgcn_make_buffer_rsrc(pooled + (size_t)b * P_SAMPLE, 0, P_SAMPLE * 4, 0x00020000);
-        const auto crs = __builtin_amdgcn_make_buffer_rsrc(code + (size_t)b * P_SAMPLE, 0, P_SAMPLE, 0x00020000);
-#pragma unroll 1
-        for (int g = 0; g < 3; ++g) {
-            const int t = 48 * band + 16 * g + li;       // tile = pooling window index
-            const int ty = t / P_HW, tx = t - P_HW * (t / P_HW);
-            const float* pp = img + lk * WF_CSTR + (2 * ty - 8 * band) * A_HW + 2 * tx;
-            f32x4 acc[16];  // written first by the C = 0 MFMAs of k step 0
-            f2 Rlo[4], Rhi[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                Rlo[r] = *reinterpret_cast<const f2*>(pp + r * A_HW);
-                Rhi[r] = *reinterpret_cast<const f2*>(pp + r * A_HW + 2);
-            }
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                f2 v01[4], v23[4];
-                if (SLK_WINO_ABL & 1) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { v01[r] = Rlo[r]; v23[r] = Rhi[r]; }
-                } else {
-                    pk_wino_in(Rlo, Rhi, v01, v23);
-                }
-                if (s < 7) {  // next step's patch: in flight under this step's 16 MFMAs
-                    const float* ps = pp + 4 * (s + 1) * WF_CSTR;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        Rlo[r] = *reinterpret_cast<const f2*>(ps + r * A_HW);
-                        Rhi[r] = *reinterpret_cast<const f2*>(ps + r * A_HW + 2);
-                    }
-                }
-                // pin the order (hipcc otherwise sinks the prefetch next to its use and exposes the
-                // LDS latency twice per step at one wave per SIMD)
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (s == 0) {
-                        mfma_a0(acc[4 * i + 0], uw[s][4 * i + 0], v01[i].x);
-                        mfma_a0(acc[4 * i + 1], uw[s][4 * i + 1], v01[i].y);
-                        mfma_a0(acc[4 * i + 2], uw[s][4 * i + 2], v23[i].x);
-                        mfma_a0(acc[4 * i + 3], uw[s][4 * i + 3], v23[i].y);
-                    } else {
-                        mfma_a(acc[4 * i + 0], uw[s][4 * i + 0], v01[i].x);
-                        mfma_a(acc[4 * i + 1], uw[s][4 * i + 1], v01[i].y);
-                        mfma_a(acc[4 * i + 2], uw[s][4 * i + 2], v23[i].x);
-                        mfma_a(acc[4 * i + 3], uw[s][4 * i + 3], v23[i].y);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            mfma_drain();
-            // output transform, two rows (co = 16w + 4lk + r, r = 2h, 2h+1) per packed op; + bias
-            f2 z[2][4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                f2 m[16];
-#pragma unroll
-                for (int ij = 0; ij < 16; ++ij) m[ij] = h ? acc[ij].zw : acc[ij].xy;
-                if (SLK_WINO_ABL & 4) {  // cheapest use of every accumulator
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) z[h][q] = (m[q] + m[q + 4]) + (m[q + 8] + m[q + 12]);
-                } else {
-                    pk_wino_out(m, z[h]);
-                }
-                const f2 bb = h ? f2{bv.z, bv.w} : f2{bv.x, bv.y};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) z[h][q] += bb;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int h = r >> 1;
-                float yq[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) yq[q] = (r & 1) ? z[h][q].y : z[h][q].x;
-                // max over the raw window, first max wins; = torch's relu-then-pool scan
-                const float mx = fmaxf(fmaxf(yq[0], yq[1]), fmaxf(yq[2], yq[3]));
-                const int idx = yq[0] == mx ? 0 : yq[1] == mx ? 1 : yq[2] == mx ? 2 : 3;
-                const bool pos = mx > 0.f;
-                const int o = (16 * wave + 4 * lk + r) * P_WIN + t;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pos ? mx : 0.f), prs, 4 * o, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pos ? idx : CODE_NONE), crs, o, 0, 0);
-            }
-        }
-        buf ^= 1;
-    }
-}
-
-extern "C" int slk_conv2_fwd_pool_v1(const float* act, const float* W2, const float* b2, float* pooled,
-                                  uint8_t* code, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0);
-    if (B == 0) return 0;
-    SLK_CHECK_ARG(act && W2 && b2 && pooled && code);
-    const int nunit = 3 * B;
-    conv2_fwd_pool_wino_kernel<<<nunit < WF_GRID ? nunit : WF_GRID, WF_THREADS, 0, slk_stream(stream)>>>(
-        act, W2, b2, pooled, code, B);
-    return slk_launch_status();
-}
-
-#endif  // SLK_WINO_V1
 // ============================================================================ shared helpers
 // 4x4 patch of a row-major LDS image (row stride A_HW floats) as 8 ds_read_b64, as row pairs
 __device__ __forceinline__ void lds_patch_pk(const float* ps, f2 (&lo)[4], f2 (&hi)[4]) {
@@ -594,11 +432,6 @@ constexpr int WD_CD_CH = P_SAMPLE / 1024;      // 9 KiB chunks of code
 constexpr int WD_BSTR = WD_CD_OFF + P_SAMPLE / 4 + 64;   // 11648 floats = 46,592 B per buffer
 constexpr int WD_XCH = 2 * 2 * 4 * 64 * 4;     // per parity: [group slot][writer kh][r][lane] float4
 constexpr int WD_GRID = 256;
-// Profiling-only ablation bits (tools/build_variant.sh -DSLK_WD_ABL=...; outputs wrong): 1 = no sample
-// DMA after the first two, 2 = no exchange barrier, 4 = no cut-gradient stores, 8 = no LUT reads.
-#ifndef SLK_WD_ABL
-#define SLK_WD_ABL 0
-#endif
 
 __device__ __forceinline__ void wd_dma_sample(const float* __restrict__ dpool, const uint8_t* __restrict__ code, int b,
                                               const float* dst, int wave, int lane) {
@@ -671,8 +504,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
         // every tile before this iteration was read before the previous iteration's exchange
         // barrier: sample next_dma - 2 is free once its last tile is behind us
         if (next_dma < nloc && WD_NT * (next_dma - 1) <= 32 * it) {
-            if (!(SLK_WD_ABL & 1))
-                wd_dma_sample(dpool, code, b + next_dma * (int)gridDim.x, smem + (next_dma & 1) * WD_BSTR, wu, lane);
+            wd_dma_sample(dpool, code, b + next_dma * (int)gridDim.x, smem + (next_dma & 1) * WD_BSTR, wu, lane);
             ++next_dma;
         }
         const int p = it;
@@ -713,7 +545,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             // earlier), so the dependent LDS read is not exposed in front of the expansion
             auto lutload = [&](const int (&c)[4], float4 (&E)[4]) {
 #pragma unroll
-                for (int w = 0; w < 4; ++w) E[w] = (SLK_WD_ABL & 8) ? make_float4((float)c[w], 0.f, 1.f, 0.f) : lutw[w][c[w]];
+                for (int w = 0; w < 4; ++w) E[w] = lutw[w][c[w]];
             };
             auto expand = [&](const float (&v)[4], const float4 (&E)[4], f2 (&v01)[4], f2 (&v23)[4]) {
                 f2 Rlo[4], Rhi[4];
@@ -781,10 +613,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
             // kh = 1 ci 16..31 — slot 0 is always the wave's own block: no selects on kh)
 #pragma unroll
             for (int r = 0; r < 4; ++r) xw[r * 64] = row(y[1], r);
-            if (SLK_WD_ABL & 2)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            else
-                lds_barrier();
+            lds_barrier();
             auto finish = [&](const f2 (&ym)[2][4], int mb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -792,7 +621,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void conv2_dgrad_wino_kernel(
                     const float4 tot = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
                     const int ci = 16 * mb + 4 * lk + r;
                     float* op = gsm + ci * A_PIX + 2 * ty * A_HW + 2 * tx;
-                    if (valid && !((SLK_WD_ABL & 4) && tot.x != 12345.f)) {
+                    if (valid) {
                         *reinterpret_cast<f2*>(op) = f2{tot.x, tot.y};
                         *reinterpret_cast<f2*>(op + A_HW) = f2{tot.z, tot.w};
                     }
