@@ -25,10 +25,13 @@ pickle, B = 64, timed on this host — oracle/cpu_loop.py).
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
+import statistics
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +74,8 @@ def parse():
     ap.add_argument("--no-kernel-pass", action="store_true")
     ap.add_argument("--no-exchange-phase", action="store_true")
     ap.add_argument("--exchange-steps", type=int, default=10, help="steps of the N > 1 side objects")
+    ap.add_argument("--trial-steps", type=int, default=5,
+                    help="timed steps per exchange trial at N > 1 (at least 5; the trial picks the lowest median)")
     ap.add_argument("--config", default="k2", choices=["k2", "k5"],
                     help="k2 = reference split CNN fp32 (headline); k5 = widened bf16 split CNN")
     ap.add_argument("--no-k5", action="store_true", help="skip the widened-config side measurement")
@@ -252,6 +257,18 @@ def roofline_from(kern, B, impls=None, variants=None):
             r["rocprof_source"] = src
             r["rocprof_build_id"] = bid[:16] if bid else None
             r["hip_event_avg_ms"] = r["avg_ms"]
+            if same and ms:
+                # the same launch priced on the profiler's duration, next to `frac` (this process's events)
+                r["frac_rocprof"] = round(r["flop_per_launch"] / (ms * 1e-3) / 1e12 / r["peak"], 4)
+                # the profiled process's own JSON line (written beside the summary by tools/gpu_profile_all.sh):
+                # its step time and its own HIP-event average of this kernel, so the two clocks are comparable
+                try:
+                    pj = json.load(open(os.path.join(ROOT, "profiles", "rocprof_kernel_stats_k2.bench.json")))
+                    r["rocprof_process"] = {"ms_per_step": round(pj["ms_per_step"], 4),
+                                            "graph": pj.get("config", {}).get("graph"),
+                                            "hip_event_avg_ms": (pj.get("roofline") or {}).get("avg_ms")}
+                except (OSError, ValueError, KeyError, TypeError):
+                    pass
     r["per_kernel"] = {k: {kk: conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino"))[kk]
                            for kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops")}
                        for k, v in conv.items()}
@@ -270,6 +287,8 @@ def run_single(args, out):
     conv = args.conv or CONV_DEFAULT
     a, b = init_models(seed=0)
     tr = SplitTrainer(a, b, device=dev, graph=not args.no_graph, conv=conv)
+    for i in range(4):   # the pool is the loader's ring: one graph per buffer pair, captured before timing
+        tr.register_inputs(X[i], Y[i])
     step = lambda i: tr.step(X[i % 4], Y[i % 4])  # noqa: E731
     dt = timed(step, args.steps, args.warmup, dev)
     losses = tr.loss_log.flush()
@@ -314,6 +333,8 @@ def run_single(args, out):
                 continue
             try:
                 tro = SplitTrainer(*init_models(seed=0), device=dev, graph=not args.no_graph, conv=other)
+                for i in range(4):
+                    tro.register_inputs(X[i], Y[i])
                 dto = timed(lambda i: tro.step(X[i % 4], Y[i % 4]), args.steps, args.warmup, dev)
                 out["conv_presets"][other] = round(args.steps * B / dto, 1)
                 del tro
@@ -447,6 +468,8 @@ def run_wide(args, B, steps, warmup, kernel_pass_on=True):
     xs, ys = zip(*(data.batch(B) for _ in range(4)))
     X, Y = torch.stack(xs).to(dev), torch.stack(ys).to(dev)
     tr = WideTrainer(*init_wide_models(seed=0), device=dev, graph=not args.no_graph)
+    for i in range(4):
+        tr.register_inputs(X[i], Y[i])
     dt = timed(lambda i: tr.step(X[i % 4], Y[i % 4]), steps, warmup, dev)
     losses = tr.loss_log.flush()
     r = {"metric": "training samples/sec, widened split CNN (BASELINE config 5)", "value": steps * B / dt,
@@ -490,55 +513,145 @@ def predict_exchange(nc, B, p2p_gbps):
     return out
 
 
-def run_distributed(args, out, rank, world, local):
+def timed_steps(fn, K, W, device, group=None):
+    """W warm-up calls, then K calls each timed on its own between a synchronize + barrier; returns the K
+    per-step times (s), each the max over ranks (one all-reduce at the end). The exchange trials choose
+    by the median of these."""
+    import torch
+    import torch.distributed as dist
+    for i in range(W):
+        fn(i)
+    ts = []
+    for i in range(K):
+        torch.cuda.synchronize(device)
+        if dist.is_initialized():
+            dist.barrier(group=group)
+        t0 = time.perf_counter()
+        fn(W + i)
+        torch.cuda.synchronize(device)
+        ts.append(time.perf_counter() - t0)
+    if dist.is_initialized():
+        t = torch.tensor(ts, dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        ts = [float(v) for v in t.cpu()]
+    return ts
+
+
+# executed f16 MFMA FLOPs per sample of the server GPU's three x3 conv2 kernels (forward, dgrad, wgrad; each
+# does 3 f16 products per direct-conv multiply-add): what the server GPU's step-level roofline prices
+SERVER_X3_FLOP_PER_SAMPLE = 9 * CONV2_FLOP_PER_SAMPLE
+
+
+def server_kernel_pass(t, B, dev, steps=3):
+    """Hub / Pipeline server rank, after the headline: `steps` eager passes over the step's chunks on the
+    data already in the receive buffers (no exchange), HIP events around each launch on the launch
+    stream; the dominant conv2 kernel priced per launch (one launch = one chunk of nc*B/m samples)."""
+    from splitcnn.engine import TIMER
+    codec = t._use_codec(dev)
+    TIMER.reset()
+    TIMER.enabled = True
+    try:
+        for _ in range(steps):
+            for k in range(t.micro):
+                t._chunk(k, B, dev, codec)
+        kern = TIMER.summary()
+    finally:
+        TIMER.enabled = False
+    s = t.stage
+    CH = t.nclients * B // t.micro
+    r = roofline_from(kern, CH, {"conv2_fwd_pool": s.impl_fwd, "conv2_dgrad": s.impl_dgrad, "conv2_wgrad": s.impl_wgrad})
+    if r is not None:
+        r["launch_batch"] = CH
+        r["measured_on"] = "server rank, eager chunk passes after the timed region (HIP events on the launch stream)"
+        r["kernels_ms"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["avg_ms"])}
+    return r
+
+
+def step_roofline(samples_per_s_per_server, ms_per_step, global_batch):
+    """Step-level roofline of the server GPU at N > 1: the executed f16 MFMA FLOPs of its x3 conv2 kernels
+    over the step time, against the dense f16 peak."""
+    ach = samples_per_s_per_server * SERVER_X3_FLOP_PER_SAMPLE / 1e12
+    return {"scope": "server GPU over the whole step (x3 conv2 forward + dgrad + wgrad: 9 x 21,233,664 executed "
+                     "f16 MFMA FLOP per sample)", "bound": "mfma", "achieved": round(ach, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+            "flop_per_step": SERVER_X3_FLOP_PER_SAMPLE * global_batch, "ms_per_step": round(ms_per_step, 4),
+            "step_direct_equivalent_tflops": round(samples_per_s_per_server * FLOP_PER_SAMPLE / 1e12, 2)}
+
+
+# watchdog limits (s) per phase of the N > 1 bench; SLK_BENCH_WATCHDOG_SCALE multiplies them
+PHASE_LIMIT_S = {"setup": 300, "p2p": 120, "trial": 150, "roofline": 120, "replicated": 240, "k5": 300, "teardown": 120}
+
+
+def run_distributed(args, out, rank, world, local, wd=None):
     """N > 1, BASELINE's own topologies. Headline `value`: N = 2 -> K3 (client GPU <-> server GPU,
     micro-batched RCCL send/recv, dist.Pipeline); N >= 3 -> K4 (SplitFed: N-1 client GPUs feeding 1
     server GPU, client all-reduce, dist.Hub). Before timing: the RCCL p2p rate client 0 -> server is
-    measured, the exchange (dense fp32 or the lossless sparse codec) is predicted from it, and a short
-    trial of both on the real topology decides. Side objects: "replicated_dp" (data-parallel
-    SplitFed-V1 replicas of the fused K2 step — NOT a BASELINE config) and "k5_splitfed" (config 5's
-    widened model on the hub topology), with cut-exchange GB/s against the measured p2p peak and the
-    vendor link figure."""
+    measured, the exchange (dense fp32 or the lossless sparse codec) is predicted from it, and a trial of
+    both on the real topology decides (median of >= 5 timed steps). `roofline`: the server GPU's
+    executed f16 FLOPs per step over the step time, with its dominant kernel (HIP events on the server
+    rank) and the link beside it. Side objects: "replicated_dp" (data-parallel SplitFed-V1 replicas of the
+    fused K2 step — NOT a BASELINE config) and "k5_splitfed" (config 5's widened model on the hub
+    topology), with cut-exchange GB/s against the measured p2p peak and the vendor link figure. Every
+    phase runs under the watchdog `wd`; every HIP graph of a phase is captured after a synchronize +
+    barrier and before that phase's first exchange (capture mode thread_local besides)."""
     import torch
     import torch.distributed as dist
 
     from splitcnn import dist as sd
     from splitcnn.data import init_models
     from splitcnn.engine import ClientStage, ServerStage
+    wd = wd or Watchdog(out, rank, enabled=False)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     B = args.batch
     topo = args.topology if args.topology != "auto" else ("pipeline" if world == 2 else "hub")
+    wd.phase("setup", PHASE_LIMIT_S["setup"])
     X, Y = make_pool(B, 4, dev, seed=42 + rank)
     grp = sd.client_group_for(world)   # every rank creates it (collective), used by hub topologies
     groups = sd.exchange_groups()      # one process group per exchange direction (see its docstring)
     nc = world - 1
 
+    def settle():
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+
     def build(topology, micro, codec):
+        """Construct this rank's side of `topology`, then capture its graphs between two settle()s."""
         a, b = init_models(seed=0)
+        images = not codec and not args.no_images
         if topology == "replicated":
             t = sd.Replicated(ClientStage(a, device=dev), ServerStage(b, device=dev), graph=not args.no_graph)
-            return (lambda i: t.step(X[i % 4], Y[i % 4])), t, world * B
-        # the dense exchange ships the client's x3 split images (the f32 cut's bytes) unless --no-images
-        images = not codec and not args.no_images
-        if topology == "pipeline":
+            fn, gb = (lambda i: t.step(X[i % 4], Y[i % 4])), world * B
+        elif topology == "pipeline":
             assert world == 2
             if rank == 0:
                 t = sd.Pipeline(ClientStage(a, device=dev), "client", 1, micro=micro, compress=codec, groups=groups,
                                 graph=not args.no_graph, images=images)
-                return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, B
-            t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec, groups=groups,
-                            graph=not args.no_graph, images=images)
-            return (lambda i: t.server_step(B, dev)), t, B
-        if topology == "hub":
+                fn = lambda i: t.client_step(X[i % 4], Y[i % 4])  # noqa: E731
+            else:
+                t = sd.Pipeline(ServerStage(b, device=dev), "server", 0, micro=micro, compress=codec, groups=groups,
+                                graph=not args.no_graph, images=images)
+                fn = lambda i: t.server_step(B, dev)  # noqa: E731
+            gb = B
+        elif topology == "hub":
             if rank < world - 1:
                 t = sd.Hub(ClientStage(a, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
                            groups=groups, graph=not args.no_graph, images=images)
-                return (lambda i: t.client_step(X[i % 4], Y[i % 4])), t, (world - 1) * B
-            t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
-                       groups=groups, graph=not args.no_graph, images=images)
-            return (lambda i: t.server_step(B, dev)), t, (world - 1) * B
-        raise ValueError(topology)
+                fn = lambda i: t.client_step(X[i % 4], Y[i % 4])  # noqa: E731
+            else:
+                t = sd.Hub(ServerStage(b, device=dev), rank, world, client_group=grp, micro=micro, compress=codec,
+                           groups=groups, graph=not args.no_graph, images=images)
+                fn = lambda i: t.server_step(B, dev)  # noqa: E731
+            gb = (world - 1) * B
+        else:
+            raise ValueError(topology)
+        settle()
+        if topology == "replicated":
+            t.prepare(B)
+        else:
+            t.prepare(B, dev)
+        settle()
+        return fn, t, gb
 
     labels = {
         "replicated": "data-parallel SplitFed-V1 replicas (NOT a BASELINE config): every GPU hosts one client + "
@@ -563,8 +676,8 @@ def run_distributed(args, out, rank, world, local):
 
     # 1. the link: RCCL p2p client 0 -> server, one direction, one cut's worth of bytes
     peak = None
+    wd.phase("p2p peak", PHASE_LIMIT_S["p2p"])
     try:
-        progress("p2p peak")
         p = sd.measure_p2p(CUT_BYTES * B, 0, world - 1, dev)
         pk = torch.tensor([p or 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(pk, op=dist.ReduceOp.MAX)
@@ -573,34 +686,38 @@ def run_distributed(args, out, rank, world, local):
     except Exception as e:
         out["p2p_peak_GBps_measured"] = {"error": repr(e)[:300]}
 
-    # 2. the exchange: predicted from the link, decided by a short trial of both on this topology
+    # 2. the exchange: predicted from the link, decided by a trial of both on this topology
     exch = {"vendor_link_GBps": XGMI_LINK_GBPS}
     if topo == "replicated":
+        wd.phase("replicated: build + capture", PHASE_LIMIT_S["trial"])
         fn, t, global_batch = build(topo, args.micro, False)
     else:
         forced = {"dense": False, "codec": True}.get("dense" if args.dense_exchange else args.exchange)
         exch["prediction_ms_per_step"] = predict_exchange(nc if topo == "hub" else 1, B, peak)
-        trials = {}
+        trials, spread = {}, {}
         built = {}
         # micro-batch counts tried: a link-bound pipeline takes ~(1 + 1/m) x its link time, while each
         # micro-batch adds fixed costs (p2p op latency, the codec's count round trip), so the link decides
         micros = [args.micro] + ([2 * args.micro] if not args.no_micro_trial and B % (2 * args.micro) == 0 else [])
+        Kt = max(5, args.trial_steps)
         for name, codec in (("dense", False), ("codec", True)):
             if forced is not None and codec != forced:
                 continue
             for m in micros:
                 key = f"{name}/m{m}"
-                progress(f"{topo} x{world}: {key} exchange trial")
+                wd.phase(f"{topo} x{world}: {key} exchange trial", PHASE_LIMIT_S["trial"])
                 f, tt, gb = build(topo, m, codec)
-                dtt = timed(f, 3, 2, dev)
-                trials[key] = round(dtt / 3 * 1e3, 3)
+                ts = timed_steps(f, Kt, 2, dev)
+                trials[key] = round(statistics.median(ts) * 1e3, 3)
+                spread[key] = [round(min(ts) * 1e3, 3), round(max(ts) * 1e3, 3)]
                 built[key] = (f, tt, gb, m)
         best = min(trials, key=trials.get)
         choice, micro = best.split("/")[0], built[best][3]
-        exch.update(choice=choice, micro_batches=micro, trial_ms_per_step=trials,
+        exch.update(choice=choice, micro_batches=micro, trial_ms_per_step=trials, trial_min_max_ms=spread,
                     rule=("exchange forced by flag; " if forced is not None else "") +
-                         "the fastest of a 3-step trial (after 2 warm-up steps) of each exchange x micro-batch count "
-                         "on this topology",
+                         f"the lowest median step time of a {Kt}-step trial (after 2 warm-up steps; each step timed "
+                         "between a synchronize + barrier, max over ranks) of each exchange x micro-batch count on "
+                         "this topology",
                     prediction_agrees=(min(exch["prediction_ms_per_step"], key=exch["prediction_ms_per_step"].get)
                                        == choice) if peak else None)
         fn, t, global_batch, _ = built[best]
@@ -610,19 +727,20 @@ def run_distributed(args, out, rank, world, local):
         torch.cuda.empty_cache()
 
     # 3. the headline
-    progress(f"{topo} x{world}: timing {args.steps} steps")
+    wd.phase(f"{topo} x{world}: timing {args.steps} steps",
+             PHASE_LIMIT_S["trial"] + 5.0 * (args.steps + args.warmup))
     dt = timed(fn, args.steps, args.warmup, dev)
     out.update(value=args.steps * global_batch / dt, ms_per_step=dt / args.steps * 1e3)
     out["config"] = {"workload": labels[topo], "global_batch": global_batch, "per_gpu_batch": B, "topology": topo,
                      "parallelism": {"pipeline": "k3-client-server", "hub": f"k4-{nc}clients-1server"}.get(topo, f"dp{world}"),
                      "graph": bool(getattr(t, "graph", False))}
     out["scaling"] = "weak"
+    step_s = dt / args.steps
     if topo != "replicated":
         out["config"]["micro_batches"] = exch["micro_batches"]
         out["config"]["per_client_batch"] = B
         out["config"]["cut_exchange"] = codec_label[exch["choice"] == "codec"]
         moved, dense = wire(t)
-        step_s = dt / args.steps
         per_dir_dense = B * CUT_BYTES
         wgbps = moved / 2 / step_s / 1e9
         exch.update(link_bytes_per_step_moved=moved, link_bytes_per_step_dense=dense,
@@ -634,19 +752,36 @@ def run_distributed(args, out, rank, world, local):
         if topo == "hub":
             exch["server_inbound_wire_GBps_all_links"] = round(wgbps * nc, 2)
         out["exchange"] = exch
+        # the server GPU's roofline over the step, its dominant kernel, and the link beside them
+        roof = step_roofline(global_batch / step_s, step_s * 1e3, global_batch)
+        roof["link"] = {k: exch[k] for k in ("wire_GBps_per_link_per_direction", "wire_frac_of_measured_p2p_peak",
+                                             "wire_frac_of_vendor_link")}
+        out["roofline"] = roof
+        wd.phase("roofline: server kernel pass", PHASE_LIMIT_S["roofline"])
+        try:
+            settle()
+            dk = [server_kernel_pass(t, B, dev) if rank == world - 1 else None]
+            settle()
+        except Exception as e:  # noqa: BLE001 (the headline stands on its own)
+            dk = [{"error": repr(e)[:300]}]
+        dist.broadcast_object_list(dk, src=world - 1)
+        out["roofline"]["dominant_kernel"] = dk[0]
     else:
         out["config"]["replica_step"] = ("fused single-GPU step kernels (x3 conv2, client images, client backward "
                                          "in the dgrad epilogue) captured in a HIP graph; bucket all-reduce "
                                          "outside the graph; one launch steps both stages" if t.fused else "unfused")
+        roof = step_roofline(B / step_s, step_s * 1e3, B)
+        roof["scope"] = "each GPU (replica) over the whole step: " + roof["scope"].split("(", 1)[1].rstrip(")")
+        out["roofline"] = roof
     del fn, t
     torch.cuda.empty_cache()
 
     if topo != "replicated" and not args.no_exchange_phase:
         # side object: data-parallel replicas of the fused K2 step on every GPU (not a BASELINE config)
+        wd.phase(f"replicated x{world}: build + {args.exchange_steps} steps", PHASE_LIMIT_S["replicated"])
         try:
             fn2, t2, gb2 = build("replicated", args.micro, False)
             K2 = args.exchange_steps
-            progress(f"replicated x{world}: timing {K2} steps")
             dt2 = timed(fn2, K2, 2, dev)
             out["replicated_dp"] = {"workload": labels["replicated"], "samples_per_s": round(K2 * gb2 / dt2, 1),
                                     "ms_per_step": round(dt2 / K2 * 1e3, 3), "global_batch": gb2,
@@ -657,6 +792,7 @@ def run_distributed(args, out, rank, world, local):
             out["replicated_dp"] = {"error": repr(e)[:300]}
     if not args.no_k5:
         # BASELINE config 5 SplitFed: N-1 client GPUs run the widened conv stack, GPU N-1 the head
+        wd.phase(f"k5_splitfed x{world}", PHASE_LIMIT_S["k5"])
         try:
             from splitcnn.wide import SyntheticCIFAR, WideClientStage, WideServerStage, init_wide_models
             Bk = args.k5_batch
@@ -673,7 +809,6 @@ def run_distributed(args, out, rank, world, local):
                                 groups=groups)
                 wfn = lambda i: wt.server_step(Bk, dev, WideClientStage.cut_shape, WideClientStage.cut_dtype)  # noqa: E731
             Kw = max(3, min(args.steps, 10))
-            progress(f"k5_splitfed x{world}: timing {Kw} steps")
             dtw = timed(wfn, Kw, 2, dev)
             Gw = (world - 1) * Bk
             per_dir = Bk * 32768
@@ -694,6 +829,79 @@ def progress(msg):
     """Phase marker on stderr (long multi-rank runs stay visibly alive; stdout keeps the one JSON line)."""
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
+class Watchdog:
+    """Per-phase hang guard of the multi-rank bench (armed by default at N > 1; SLK_BENCH_WATCHDOG=0 turns
+    it off, =1 arms it at N = 1 too; SLK_BENCH_WATCHDOG_SCALE multiplies every limit). `phase(name, s)`
+    starts a phase that must end within s seconds (the next phase() or disarm() ends it). On expiry the
+    watchdog thread dumps every thread's stack to stderr; on rank 0 it prints the JSON line accumulated so
+    far (`out`: the headline once measured) with "error": "watchdog: <phase>"; then the process leaves
+    with os._exit(3) — no re-launch, and torch.distributed.run then stops the other ranks. Ranks other
+    than 0 wait `grace` seconds longer, so that rank 0 (which holds the JSON) reports first.
+    SLK_BENCH_STALL=<phase prefix> (+ SLK_BENCH_STALL_RANK, default 0) makes that rank sleep inside the
+    first matching phase: the test knob for this path."""
+
+    EXIT_CODE = 3
+
+    def __init__(self, out, rank=0, enabled=True, scale=None, grace=30.0, stream=None):
+        self.out, self.rank = out, rank
+        self.enabled = bool(enabled)
+        self.scale = float(os.environ.get("SLK_BENCH_WATCHDOG_SCALE", "1")) if scale is None else float(scale)
+        self.grace = 0.0 if rank == 0 else grace
+        self.stream = stream if stream is not None else sys.stdout
+        self.name = None
+        self.history = []
+        self._deadline = None
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._stall = os.environ.get("SLK_BENCH_STALL")
+        self._stall_rank = int(os.environ.get("SLK_BENCH_STALL_RANK", "0"))
+        if self.enabled:
+            threading.Thread(target=self._run, name="slk-bench-watchdog", daemon=True).start()
+
+    def phase(self, name, seconds):
+        progress(name)
+        with self._lock:
+            if self.name is not None:
+                self.history.append(self.name)
+            self.name = name
+            self._deadline = time.monotonic() + seconds * self.scale + self.grace
+        if self._stall and name.startswith(self._stall) and self.rank == self._stall_rank:
+            self._stall = None
+            print(f"[bench] SLK_BENCH_STALL: rank {self.rank} stalls in phase '{name}'", file=sys.stderr, flush=True)
+            time.sleep(1e7)
+
+    def disarm(self):
+        with self._lock:
+            self._deadline = None
+        self._stop.set()
+
+    def _run(self):
+        while not self._stop.wait(0.25):
+            with self._lock:
+                late = self._deadline is not None and time.monotonic() > self._deadline
+                name = self.name
+            if late:
+                self._fire(name)
+
+    def _fire(self, name):
+        try:
+            print(f"[bench] watchdog: phase '{name}' exceeded its limit on rank {self.rank}; all stacks:",
+                  file=sys.stderr, flush=True)
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            if self.rank == 0:
+                try:
+                    o = json.loads(json.dumps(self.out, default=str))   # a snapshot the main thread cannot change
+                except Exception:  # noqa: BLE001 (a nested value mutated mid-copy: keep the scalars)
+                    o = {k: v for k, v in dict(self.out).items() if isinstance(v, (int, float, str, type(None)))}
+                o["error"] = f"watchdog: {name}"
+                o["phases_completed"] = list(self.history)
+                print(json.dumps(o), file=self.stream, flush=True)
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(self.EXIT_CODE)
 
 
 def main():
@@ -721,13 +929,16 @@ def main():
         cpu = cpu_baseline(args.cpu_baseline_seconds)  # before this process touches the GPU
     import torch
     import torch.distributed as dist
+    wd_env = os.environ.get("SLK_BENCH_WATCHDOG")
+    wd = Watchdog(out, rank, enabled=(wd_env != "0") if world > 1 else (wd_env == "1"))
     if world > 1:
+        wd.phase("init_process_group", PHASE_LIMIT_S["setup"])
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)
-        run_distributed(args, out, rank, world, local)
+        run_distributed(args, out, rank, world, local, wd)
     elif args.config == "k5":
         w = run_wide(args, args.k5_batch, args.steps, args.warmup, not args.no_kernel_pass)
         out.update({k: v for k, v in w.items() if k != "metric"})
@@ -778,10 +989,13 @@ def main():
         out["build"] = {"slk_build_id": _lib.build_id()[:16], "variant_defines": _lib.VARIANT_DEFINES}
     except Exception as e:  # noqa: BLE001
         out["build"] = {"error": repr(e)[:200]}
+    if world > 1:
+        wd.phase("teardown", PHASE_LIMIT_S["teardown"])
+        dist.barrier()
+    wd.disarm()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
         dist.destroy_process_group()
 
 

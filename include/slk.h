@@ -319,8 +319,7 @@ int slk_wide_head_work(int B);
  * sum order as slk_wide_head, so bit-identical logits); _bwd takes dlogits from any loss and writes dcut and the fc slabs
  * exactly as slk_wide_head's last stage. */
 int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step, unsigned seed,
-                      unsigned keep_threshold, float keep_scale, float* logits, float* work, int b0, int B,
-                      void* stream);
+                      unsigned keep_threshold, float keep_scale, float* logits, int b0, int B, void* stream);
 int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogits, const int* step, unsigned seed,
                       unsigned keep_threshold, float keep_scale, uint16_t* dcut, float* slabs, int b0, int B,
                       void* stream);

@@ -504,10 +504,9 @@ extern "C" int slk_wide_head(const uint16_t* cut, const float* wf8, const float*
     return slk_launch_status();
 }
 extern "C" int slk_wide_head_fwd(const uint16_t* cut, const float* wf8, const float* bf, const int* step,
-                                 unsigned seed, unsigned keep_threshold, float keep_scale, float* logits, float* work,
+                                 unsigned seed, unsigned keep_threshold, float keep_scale, float* logits,
                                  int b0, int B, void* stream) {
-    SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && bf && step && logits && work);
-    SLK_CHECK_ARG(((uintptr_t)work & 15) == 0);
+    SLK_CHECK_ARG(B >= 0 && b0 >= 0 && cut && wf8 && bf && step && logits);
     if (B == 0) return 0;
     hipStream_t st = slk_stream(stream);
     hipLaunchKernelGGL(wide_head16_kernel<false>, dim3((B + WH_S - 1) / WH_S), dim3(WH_T), 0, st, cut, wf8, bf, nullptr, step,

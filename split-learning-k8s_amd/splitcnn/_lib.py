@@ -78,7 +78,7 @@ _SIGS = {
     "slk_wide_conv3_fwd": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_head": [_P, _P, _P, _P, _P, _U, _U, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "slk_wide_head_nslab": [_I],
-    "slk_wide_head_fwd": [_P, _P, _P, _P, _U, _U, _F, _P, _P, _I, _I, _P],
+    "slk_wide_head_fwd": [_P, _P, _P, _P, _U, _U, _F, _P, _I, _I, _P],
     "slk_wide_head_bwd": [_P, _P, _P, _P, _U, _U, _F, _P, _P, _I, _I, _P],
     "slk_wide_head_work": [_I],
     "slk_wide_conv3_wgrad": [_P, _P, _P, _P, _I, _P],

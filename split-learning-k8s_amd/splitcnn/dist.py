@@ -185,11 +185,19 @@ class Replicated:
             self._compute_fused(x, y)
         torch.cuda.current_stream(dev).wait_stream(st)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture mode: ProcessGroupNCCL's watchdog thread queries the events of earlier
+        # collectives while this thread captures; in the default global mode that query invalidates it
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._compute_fused(x, y)
         g = {"graph": graph, "x": x, "y": y}
         self._graphs[B] = g
         return g
+
+    def prepare(self, B: int) -> None:
+        """Capture the replica's graph for batch size B now (bench.py does this after a synchronize +
+        barrier and before the phase's first collective); otherwise the first step() captures it."""
+        if self.fused and self.graph:
+            self._graph_for(B)
 
     def _step_fused(self, x, y):
         from . import ops
@@ -318,6 +326,16 @@ class Hub:
         self._codec = None
         # the server passes the shipped max on only to stages whose compute takes it (engine stages)
         self._amax_kw = "act_amax" in inspect.signature(stage.compute).parameters if hasattr(stage, "compute") else False
+        if self.images and self.is_server:
+            # fail here, not inside the first forward_backward while the clients block in their sends
+            # (engine stages declare their conv kernels; a stage without impl_* — the CPU protocol tests'
+            # oracle stage — only has to take the image bytes)
+            takes = inspect.signature(stage.compute).parameters if hasattr(stage, "compute") else {}
+            engine = hasattr(stage, "impl_fwd")
+            impls = (getattr(stage, "impl_fwd", "x3"), getattr(stage, "impl_wgrad", "x3"))
+            if "act16" not in takes or impls != ("x3", "x3") or (engine and not self._amax_kw):
+                raise ValueError(f"Hub(images=True) needs a server stage on the x3 forward and wgrad whose compute "
+                                 f"takes act16 and act_amax (got impl_fwd/impl_wgrad={impls}, act_amax={self._amax_kw})")
 
     @property
     def is_server(self):
@@ -377,7 +395,12 @@ class Hub:
         """Receive a 1-element int32 count from `src` and return it on the host, without waiting for
         the compute queued on the current stream (side stream + pinned copy)."""
         w = self._p2p(irecv, head, src, self.groups[0], side)
-        if side is None or _host_staged(head, self.groups[0]):
+        if isinstance(w, _Staged):
+            # gloo: the count is already on the host; copying it to the device and reading it back
+            # would wait for everything queued on the current stream (the previous chunk's graph)
+            w.work.wait()
+            return int(w.host.item())
+        if side is None:
             w.wait()
             return int(head.item())
         with torch.cuda.stream(side):
@@ -532,10 +555,17 @@ class Hub:
                 self._chunk(k, B, device, codec)
             torch.cuda.current_stream(device).wait_stream(st)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):   # see Replicated._graph_for
                 self._chunk(k, B, device, codec)
             self._graphs[k, B, codec is not None] = g
         torch.cuda.current_stream(device).synchronize()
+
+    def prepare(self, B: int, device) -> None:
+        """Server rank: capture the chunk graphs for per-client batch B now (bench.py does this after a
+        synchronize + barrier and before the phase's first exchange); otherwise the first server_step
+        captures them. No-op on client ranks (they run eagerly)."""
+        if self.is_server:
+            self._prepare(B, device, self._use_codec(device))
 
     def _run_chunk(self, k, B, device, codec):
         if self._graphed(device):

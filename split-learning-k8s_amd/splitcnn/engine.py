@@ -437,6 +437,52 @@ class ServerStage:
             raise IndexError("splitcnn: a label was out of range [0, 10)")
 
 
+def _n_caller_graphs(tr, B: int) -> int:
+    return sum(1 for k in tr._graphs if isinstance(k, tuple) and k[0] == B)
+
+
+def _is_static(tr, x, y) -> bool:
+    st = tr._graphs.get(x.shape[0])
+    return st is not None and x.data_ptr() == st["x"].data_ptr() and y.data_ptr() == st["y"].data_ptr()
+
+
+def register_graph_inputs(tr, x, y) -> bool:
+    """Capture trainer `tr`'s step graph on the caller's own (x, y) buffers now — a loader declaring its
+    ring of batch buffers — so step() on them replays with no copy and no capture later. Counts toward
+    `tr.graph_inputs`; False (nothing captured) when the buffers do not qualify or that budget is spent.
+    Shared by SplitTrainer and wide.WideTrainer (`_graphs`, `_graph_for`, `_own_buffers_ok`)."""
+    if not tr.graph or not tr._own_buffers_ok(x, y):
+        return False
+    B = x.shape[0]
+    if _is_static(tr, x, y) or (B, x.data_ptr(), y.data_ptr()) in tr._graphs:
+        return True
+    if _n_caller_graphs(tr, B) >= tr.graph_inputs:
+        return False
+    tr._graph_for(B, x, y)
+    return True
+
+
+def select_graph(tr, x, y):
+    """The graph step() replays directly on (x, y), or None (then it copies into the static inputs).
+    The static inputs handed back (static_inputs(B)) replay their own graph; a caller buffer pair gets a
+    graph of its own the SECOND time it is seen (a loader's ring), so a one-off fresh tensor goes
+    through the static-input copy and is not kept alive by a graph."""
+    if not tr._own_buffers_ok(x, y):
+        return None
+    if _is_static(tr, x, y):
+        return tr._graphs[x.shape[0]]
+    B = x.shape[0]
+    key = (B, x.data_ptr(), y.data_ptr())
+    g = tr._graphs.get(key)
+    if g is None:
+        n = tr._seen.get(key, 0) + 1
+        tr._seen[key] = n
+        if n >= 2 and _n_caller_graphs(tr, B) < tr.graph_inputs:
+            g = tr._graph_for(B, x, y)
+            del tr._seen[key]
+    return g
+
+
 class SplitTrainer:
     """Both stages fused on ONE GPU (BASELINE config 2): the cut tensor is handed over in place.
 
@@ -464,6 +510,7 @@ class SplitTrainer:
         # one reads its inputs where they already are, with no copy into the static inputs; at most
         # `graph_inputs` such buffer pairs per batch size, any others go through the static inputs
         self.graph_inputs = graph_inputs
+        self._seen = {}   # (B, x ptr, y ptr) -> times a caller buffer pair went through the static inputs
         self.global_step = 0
 
     @property
@@ -512,7 +559,8 @@ class SplitTrainer:
             self._eager(x, y)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture: another thread's CUDA calls (a process group's watchdog) cannot void it
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._eager(x, y)
         self.client.params.copy_(saved_c)
         self.server.params.copy_(saved_s)
@@ -526,15 +574,15 @@ class SplitTrainer:
                 and y.dtype == torch.int64 and x.is_contiguous() and y.is_contiguous()
                 and tuple(x.shape[1:]) == (1, 28, 28) and y.shape == (x.shape[0],))
 
+    def register_inputs(self, x: torch.Tensor, y: torch.Tensor) -> bool:
+        """Capture a graph on the caller's own (x, y) buffers now (see `register_graph_inputs`)."""
+        return register_graph_inputs(self, x, y)
+
     def step(self, x: torch.Tensor, y: torch.Tensor):
         B = x.shape[0]
         if self.graph:
-            key = (B, x.data_ptr(), y.data_ptr())
-            g = self._graphs.get(key)
-            if g is None and self._own_buffers_ok(x, y) and \
-                    sum(1 for k in self._graphs if isinstance(k, tuple) and k[0] == B) < self.graph_inputs:
-                g = self._graph_for(B, x, y)
-            if g is not None and self._own_buffers_ok(x, y):
+            g = select_graph(self, x, y)
+            if g is not None:
                 g["graph"].replay()
                 self.server.loss_log.note_step(self.global_step)
                 self.global_step += 1

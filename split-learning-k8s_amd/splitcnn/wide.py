@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .engine import TIMER, LossLog, _Buffers
+from .engine import TIMER, LossLog, _Buffers, register_graph_inputs, select_graph
 from .ops import _dev, _stream
 
 P_DROP = 0.25
@@ -305,9 +305,8 @@ class _WideHeadFn(torch.autograd.Function):
         s = _stream(cut)
         _k("wide_fc_shadow", _f32p(Wf, "fc.weight", 163840), wf8.data_ptr(), s)
         logits = torch.empty((B, 10), dtype=_F32, device=dev)
-        work = torch.empty((_q("slk_wide_head_work", B),), dtype=_F32, device=dev)
         _k("wide_head_fwd", cut.data_ptr(), wf8.data_ptr(), _f32p(bf, "fc.bias", 10), step.data_ptr(), int(seed),
-           int(thresh), float(scale), logits.data_ptr(), work.data_ptr(), 0, B, s)
+           int(thresh), float(scale), logits.data_ptr(), 0, B, s)
         ctx.save_for_backward(cut, wf8, step)
         ctx.drop = (int(seed), int(thresh), float(scale))
         ctx.in_dtype = cut_nchw.dtype
@@ -561,6 +560,7 @@ class WideTrainer:
         self.graph = graph
         self._graphs = {}
         self.graph_inputs = 4   # caller input buffers captured directly (as engine.SplitTrainer)
+        self._seen = {}
         self.global_step = 0
 
     @property
@@ -592,7 +592,7 @@ class WideTrainer:
             self._eager(x, y)
         torch.cuda.current_stream(self.device).wait_stream(st)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._eager(x, y)
         for t, v in zip(self._state(), saved):
             t.copy_(v)
@@ -607,6 +607,10 @@ class WideTrainer:
                 and x.is_contiguous() and y.is_contiguous() and tuple(x.shape[1:]) == (3, 32, 32)
                 and y.shape == (x.shape[0],))
 
+    def register_inputs(self, x, y) -> bool:
+        """Capture a graph on the caller's own (x, y) buffers now (engine.register_graph_inputs)."""
+        return register_graph_inputs(self, x, y)
+
     def static_inputs(self, B):
         g = self._graph_for(B)
         return g["x"], g["y"]
@@ -614,12 +618,8 @@ class WideTrainer:
     def step(self, x, y):
         B = x.shape[0]
         if self.graph:
-            key = (B, x.data_ptr(), y.data_ptr())
-            g = self._graphs.get(key)
-            if g is None and self._own_buffers_ok(x, y) and \
-                    sum(1 for k in self._graphs if isinstance(k, tuple) and k[0] == B) < self.graph_inputs:
-                g = self._graph_for(B, x, y)
-            if g is not None and self._own_buffers_ok(x, y):
+            g = select_graph(self, x, y)
+            if g is not None:
                 g["graph"].replay()
                 self.server.loss_log.note_step(self.global_step)
                 self.global_step += 1

@@ -62,3 +62,48 @@ def test_fc_xent_bad_label_sets_flag(gpu):
     assert torch.isnan(loss_i[17]) and torch.isnan(dlogits[17]).all()
     assert torch.isfinite(loss_i[:17]).all() and torch.isfinite(loss_i[18:]).all()
 
+
+
+@pytest.mark.parametrize("B", [1, 7, 15, 16, 17, 33, 100, 4096])
+def test_split_head_bitwise_vs_fused_head_with_amax(gpu, B):
+    """The server's default split head (engine.ServerStage.fc_split: slk_fc_fwd -> slk_xent_fwd_bwd ->
+    slk_fc_dgrad_amax) against the fused slk_fc_xent_amax: every output bit-identical, dp_amax included."""
+    from splitcnn import ops
+    g = torch.Generator().manual_seed(1000 + B)
+    pooled = torch.relu(torch.randn(B, 64, 12, 12, generator=g)).to(gpu)
+    W3 = (torch.randn(10, 9216, generator=g) * 0.01).to(gpu)
+    b3 = (torch.randn(10, generator=g) * 0.1).to(gpu)
+    y = torch.randint(0, 10, (B,), generator=g).to(gpu)
+    dpa = torch.empty(B, device=gpu)
+    logits, loss_i, dlogits, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+    lg2 = ops.fc_fwd(pooled, W3, b3)
+    l2, dl2 = ops.xent_fwd_bwd(lg2, y, 1.0 / B)
+    dpa2 = torch.full((B,), float("nan"), device=gpu)
+    dp2 = ops.fc_dgrad(dl2, W3, dp_amax=dpa2)
+    assert torch.equal(lg2, logits)
+    assert torch.equal(l2, loss_i)
+    assert torch.equal(dl2, dlogits)
+    assert torch.equal(dp2.reshape(dp.shape), dp)
+    assert torch.equal(dpa2, dpa)
+
+
+@pytest.mark.parametrize("B", [17, 4096])
+def test_server_stage_split_head_bitwise_vs_fused_head(gpu, B):
+    """ServerStage.forward_backward with fc_split True (default) and False: the same cut gradient,
+    conv2 slabs (s2) and fc1 slabs (s3), bit for bit (src/server_part.py:48-51)."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    a, b = init_models(seed=0)
+    cl = ClientStage(a, device=gpu)
+    cl.emit_amax = True
+    x, y = SyntheticMNIST(5).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    act = cl.forward(x)
+    outs = []
+    for split in (True, False):
+        s = ServerStage(init_models(seed=0)[1], device=gpu)
+        s.fc_split = split
+        cut, loss_i, s2, s3 = s.forward_backward(act, y, 1.0 / B, act_amax=cl._act_amax)
+        outs.append([t.clone() for t in (cut, loss_i, s2, s3)])
+    for u, v, name in zip(outs[0], outs[1], ("cut_grad", "loss_i", "s2", "s3")):
+        assert torch.equal(u, v), name

@@ -412,3 +412,37 @@ def test_graphs_on_caller_buffers_bitwise_vs_static_inputs(gpu):
     assert torch.equal(own.client.params, cpy.client.params)
     assert torch.equal(own.server.params, cpy.server.params)
     assert [l for _, l in own.loss_log.flush()] == [l for _, l in cpy.loss_log.flush()]
+
+
+def test_graph_inputs_static_buffers_and_register(gpu):
+    """The static inputs handed back (static_inputs(B)) replay their own graph (no second capture on
+    the same memory); register_inputs() captures on a declared buffer pair at once; an undeclared pair
+    is captured only the second time it is seen. All bit-identical to the always-copy trainer."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import SplitTrainer
+    data = SyntheticMNIST(13)
+    B = 64
+    xs, ys = zip(*(data.batch(B) for _ in range(3)))
+    X, Y = torch.stack(xs).to(gpu), torch.stack(ys).to(gpu)
+    own = SplitTrainer(*init_models(seed=6), device=gpu, graph=True, graph_inputs=4)
+    cpy = SplitTrainer(*init_models(seed=6), device=gpu, graph=True, graph_inputs=0)
+    sx, sy = own.static_inputs(B)
+    assert own.register_inputs(X[0], Y[0])
+    n_caller = lambda: sum(1 for k in own._graphs if isinstance(k, tuple))  # noqa: E731
+    assert n_caller() == 1
+    sx.copy_(X[2])
+    sy.copy_(Y[2])
+    own.step(sx, sy)
+    cpy.step(X[2], Y[2])
+    assert n_caller() == 1                       # no graph captured on the static buffers
+    own.step(X[1], Y[1])
+    cpy.step(X[1], Y[1])
+    assert n_caller() == 1                       # first sight of X[1]: static-input copy
+    for i in range(4):
+        own.step(X[i % 2], Y[i % 2])
+        cpy.step(X[i % 2], Y[i % 2])
+    assert n_caller() == 2                       # X[1] captured on its second sight
+    torch.cuda.synchronize()
+    assert torch.equal(own.client.params, cpy.client.params)
+    assert torch.equal(own.server.params, cpy.server.params)
+    assert [l for _, l in own.loss_log.flush()] == [l for _, l in cpy.loss_log.flush()]

@@ -424,3 +424,16 @@ def test_widehub_drains_under_rccl_semantics(monkeypatch):
         done.append("server")
     fab.run([client(r) for r in range(world - 1)] + [server])
     assert sorted(map(str, done)) == ["0", "1", "server"]
+
+
+def test_hub_images_rejects_a_server_stage_that_cannot_take_images():
+    """Hub(images=True) on the server rank raises at construction (not inside the first step, with the
+    clients blocked in their sends) unless the stage runs the x3 forward and wgrad."""
+    sd, *_ = _setup()
+    from splitcnn.engine import ServerStage
+    for conv in ("f32", "x3w"):
+        with pytest.raises(ValueError, match="images=True"):
+            sd.Hub(ServerStage(device="cpu", conv=conv), 1, 2, compress=False, images=True, groups=(None, None))
+    sd.Hub(ServerStage(device="cpu", conv="x3"), 1, 2, compress=False, images=True, groups=(None, None))
+    # a client rank is not checked (its stage is a client stage)
+    sd.Hub(ServerStage(device="cpu", conv="f32"), 0, 2, compress=False, images=True, groups=(None, None))

@@ -62,7 +62,7 @@ for path in args.libs:
     L = ctypes.CDLL(path)
     L.slk_wide_head_work.restype = ctypes.c_int
     L.slk_wide_head_nslab.restype = ctypes.c_int
-    L.slk_wide_head_fwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] * 2 + [ctypes.c_int] * 2 + [P]
+    L.slk_wide_head_fwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] + [ctypes.c_int] * 2 + [P]
     L.slk_wide_head_bwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] * 2 + [ctypes.c_int] * 2 + [P]
     L._hwork = torch.empty(L.slk_wide_head_work(B), device=dev)
     L._hslabs = torch.empty(L.slk_wide_head_nslab(B), 163850, device=dev)
@@ -87,7 +87,7 @@ def calls(L):
         "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1), p(out_da1m), B, P(s)),
         "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
         "head_fwd": lambda: L.slk_wide_head_fwd(p(cut), p(wf8), p(bfc), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hlog),
-                                                p(L._hwork), 0, B, P(s)),
+                                                0, B, P(s)),
         "head_bwd": lambda: L.slk_wide_head_bwd(p(cut), p(wf8), p(hdl), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hdcut),
                                                 p(L._hslabs), 0, B, P(s)),
         # the training step's head (forward + CE + cut gradient + fc weight-gradient slabs)

@@ -20,6 +20,8 @@ for cfg in k2 k5; do
   rc=$?; echo "rocprof $cfg rc=$rc"; stop_if_fatal $rc rocprof
   # the library build this profile belongs to (bench.py reports rocprof_avg_ms only for a matching build)
   python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_$cfg.build_id
+  # the profiled process's own JSON line (bench.py reads it as roofline.rocprof_process)
+  grep '^{' gpurun_out/prof_$cfg.log | tail -1 > gpurun_out/prof_$cfg.bench.json || true
   OUT=gpurun_out/pmc_$cfg KARGS="--config $cfg --steps 3" bash tools/pmc.sh || exit $?
   python tools/pmc_summary.py --dir gpurun_out/pmc_$cfg --out gpurun_out/pmc_${cfg}_summary.json > /dev/null
 done
