@@ -19,7 +19,7 @@ linear_wgrad, cross_entropy_grad.
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -27,6 +27,44 @@ from torch import Tensor
 from . import ops
 
 _NS = "splitcnn"
+
+
+class _Memo:
+    """A by-product one op's kernel wrote next to its output, remembered for the op that consumes that
+    output in the same autograd pass: linear_dgrad's fused per-sample max |dpooled| (slk_fc_dgrad_amax)
+    for the conv2 backward's x3 scales, cross_entropy's dlogits for its backward. A hit requires the very
+    same storage (data pointer, element count) at the same version counter (views share it; any in-place
+    write bumps it), so the by-product describes exactly the bytes the consumer sees; anything else (a
+    miss, fake tensors under tracing) falls back to the op that recomputes it. One entry per kind; a hit
+    consumes it."""
+
+    def __init__(self):
+        self._e = {}
+
+    @staticmethod
+    def _key(t):
+        try:
+            return (t.device, t.data_ptr(), t.numel(), t._version)
+        except Exception:  # noqa: BLE001 (fake / functional tensors under tracing have no storage)
+            return None
+
+    def put(self, kind, t, value):
+        k = self._key(t)
+        if k is None:
+            self._e.pop(kind, None)
+        else:
+            self._e[kind] = (k, t, value)   # t held until consumed or replaced (the next step's put)
+
+    def take(self, kind, t) -> Optional[Tensor]:
+        e = self._e.get(kind)
+        k = self._key(t)
+        if e is None or k is None or e[0] != k:
+            return None
+        del self._e[kind]
+        return e[2]
+
+
+_MEMO = _Memo()
 
 
 # ----------------------------------------------------------------------------------- conv1 + ReLU
@@ -41,28 +79,32 @@ def _(x, W1, b1):
 
 
 @torch.library.custom_op(f"{_NS}::conv1_wgrad", mutates_args=())
-def conv1_wgrad(x: Tensor, act: Tensor, g: Tensor) -> Tensor:
-    """[dW1 (288) | db1 (32)] of relu(conv1(x)) for the output gradient g (mask act > 0)."""
-    return ops.reduce_slabs(ops.conv1_wgrad_slabs(x.contiguous(), act.contiguous(), g.contiguous()))
+def conv1_wgrad(x: Tensor, W1: Tensor, b1: Tensor, g: Tensor) -> Tensor:
+    """[dW1 (288) | db1 (32)] of relu(conv1(x)) for the output gradient g. The ReLU mask act > 0 is
+    recomputed from x, W1, b1 in conv1's own FMA order (bit-identical to the forward's), so act is neither
+    saved nor read: x + g only (slk_conv1_wgrad_remask)."""
+    return ops.reduce_slabs(ops.conv1_wgrad_remask_slabs(x.contiguous(), W1.contiguous(), b1.contiguous(),
+                                                         g.contiguous()))
 
 
 @conv1_wgrad.register_fake
-def _(x, act, g):
+def _(x, W1, b1, g):
     return x.new_empty((ops.CLIENT_NPARAM,))
 
 
 def _conv1_setup(ctx, inputs, output):
-    x, _W1, _b1 = inputs
-    ctx.save_for_backward(x, output)
+    x, W1, b1 = inputs
+    # W1 / b1 are saved for the mask: autograd's version check raises if they change before the backward
+    ctx.save_for_backward(x, W1, b1)
 
 
 def _conv1_backward(ctx, g):
-    x, act = ctx.saved_tensors
+    x, W1, b1 = ctx.saved_tensors
     if ctx.needs_input_grad[0]:
         raise NotImplementedError(
             "splitcnn: gradient w.r.t. the client INPUT images is not part of the split step "
             "(the reference's data never requires grad, src/client_part.py:110-114)")
-    flat = torch.ops.splitcnn.conv1_wgrad(x, act, g)
+    flat = torch.ops.splitcnn.conv1_wgrad(x, W1, b1, g)
     return None, flat[:288].view(32, 1, 3, 3), flat[288:].view(32)
 
 
@@ -181,7 +223,12 @@ def _conv2_setup(ctx, inputs, output):
 def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16):
     code, W2, *kept = ctx.saved_tensors
     _fi, di, wi = ctx.impls
-    dpa = torch.ops.splitcnn.row_amax(dpooled) if "x3" in (di, wi) else None
+    dpa = None
+    if "x3" in (di, wi):
+        # fc1's input gradient comes with its per-sample max (linear_dgrad, fused); recomputed otherwise
+        dpa = _MEMO.take("dp_amax", dpooled)
+        if dpa is None:
+            dpa = torch.ops.splitcnn.row_amax(dpooled)
     gact = None
     if ctx.needs_input_grad[0]:
         gact = (torch.ops.splitcnn.conv2_dgrad_x3(dpooled, code, W2, dpa) if di == "x3"
@@ -210,7 +257,13 @@ def _(flat, W3, b3):
 
 @torch.library.custom_op(f"{_NS}::linear_dgrad", mutates_args=())
 def linear_dgrad(dlogits: Tensor, W3: Tensor) -> Tensor:
-    return ops.fc_dgrad(dlogits.contiguous(), W3.contiguous())
+    """fc1's input gradient; the kernel also writes its per-sample max |.| (slk_fc_dgrad_amax), kept for
+    the conv2 backward's x3 scales (no separate row_amax pass over dpooled)."""
+    dlogits = dlogits.contiguous()
+    amax = dlogits.new_empty((dlogits.shape[0],))
+    dflat = ops.fc_dgrad(dlogits, W3.contiguous(), dp_amax=amax)
+    _MEMO.put("dp_amax", dflat, amax)
+    return dflat
 
 
 @linear_dgrad.register_fake
@@ -251,8 +304,9 @@ linear.register_autograd(_linear_backward, setup_context=_linear_setup)
 @torch.library.custom_op(f"{_NS}::cross_entropy", mutates_args=())
 def cross_entropy(logits: Tensor, labels: Tensor) -> Tensor:
     """Mean cross-entropy (nn.CrossEntropyLoss(), integer labels) as a 0-d tensor."""
-    logits = logits.contiguous()
-    loss_i, _ = ops.xent_fwd_bwd(logits, labels.contiguous(), 1.0 / logits.shape[0])
+    logits, labels = logits.contiguous(), labels.contiguous()
+    loss_i, dlogits = ops.xent_fwd_bwd(logits, labels, 1.0 / logits.shape[0])
+    _MEMO.put("dlogits", logits, (labels, labels._version, dlogits))   # the backward's (softmax - onehot) / B
     return ops.loss_mean(loss_i).view(())
 
 
@@ -264,8 +318,12 @@ def _(logits, labels):
 @torch.library.custom_op(f"{_NS}::cross_entropy_grad", mutates_args=())
 def cross_entropy_grad(logits: Tensor, labels: Tensor, gloss: Tensor) -> Tensor:
     """d loss / d logits = (softmax - onehot) / B * gloss (the fused kernel, then the upstream scale)."""
-    logits = logits.contiguous()
-    _, dlogits = ops.xent_fwd_bwd(logits, labels.contiguous(), 1.0 / logits.shape[0])
+    logits, labels = logits.contiguous(), labels.contiguous()
+    hit = _MEMO.take("dlogits", logits)
+    if hit is not None and hit[0].data_ptr() == labels.data_ptr() and hit[1] == labels._version:
+        dlogits = hit[2]
+    else:
+        _, dlogits = ops.xent_fwd_bwd(logits, labels, 1.0 / logits.shape[0])
     return dlogits * gloss
 
 

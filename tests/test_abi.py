@@ -167,7 +167,7 @@ def test_custom_op_fake_kernels_shapes():
                "loss": O.cross_entropy(logits, y), "dlogits": O.cross_entropy_grad(logits, y, logits.new_ones(())),
                "dflat": O.linear_dgrad(logits, torch.empty(10, 9216, device="cuda")),
                "g3": O.linear_wgrad(logits, flat), "cut": O.conv2_dgrad(pooled, code, torch.empty(64, 32, 3, 3, device="cuda")),
-               "g2": O.conv2_wgrad(act, pooled, code), "g1": O.conv1_wgrad(x, act, act),
+               "g2": O.conv2_wgrad(act, pooled, code), "g1": O.conv1_wgrad(x, torch.empty(32, 1, 3, 3, device="cuda"), torch.empty(32, device="cuda"), act),
                "amax": amax, "a16": a16, "dpa": O.row_amax(pooled),
                "cut_x3": O.conv2_dgrad_x3(pooled, code, torch.empty(64, 32, 3, 3, device="cuda"), amax),
                "g2_x3": O.conv2_wgrad_x3(a16, amax, pooled, amax, code)}

@@ -446,3 +446,39 @@ def test_graph_inputs_static_buffers_and_register(gpu):
     assert torch.equal(own.client.params, cpy.client.params)
     assert torch.equal(own.server.params, cpy.server.params)
     assert [l for _, l in own.loss_log.flush()] == [l for _, l in cpy.loss_log.flush()]
+
+
+@pytest.mark.parametrize("B", [13, 4096])
+def test_dropin_fused_byproducts_bitwise_vs_recomputed(gpu, monkeypatch, B):
+    """The drop-in modules' backward takes linear_dgrad's fused per-sample max |dpooled| and the cross
+    entropy's forward dlogits (library._MEMO) instead of re-running row_amax / the CE kernel: every gradient
+    of the reference's step is bit-identical to the path that recomputes them, and the memo is hit."""
+    from splitcnn import library
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.model_def import CrossEntropyLoss
+    x, y = SyntheticMNIST(21).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    hits = []
+    take = library._Memo.take
+
+    def counting_take(self, kind, t):
+        v = take(self, kind, t)
+        hits.append((kind, v is not None))
+        return v
+
+    def run(use_memo):
+        client, server = (m.to(gpu) for m in init_models(seed=2))
+        with monkeypatch.context() as mp:
+            mp.setattr(library._Memo, "take", counting_take if use_memo else (lambda self, kind, t: None))
+            act = client(x)
+            ca = act.clone().detach().requires_grad_(True)
+            loss = CrossEntropyLoss()(server(ca), y)
+            loss.backward()
+            act.backward(ca.grad.clone())
+        return [loss.detach(), ca.grad] + [p.grad for p in (*client.parameters(), *server.parameters())]
+
+    got = run(True)
+    assert sorted(hits) == [("dlogits", True), ("dp_amax", True)], hits
+    want = run(False)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
