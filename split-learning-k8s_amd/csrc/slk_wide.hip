@@ -312,13 +312,19 @@ __device__ __forceinline__ void exp_store(char* slot, int i, uint4 v, uint2 cw) 
     const uint32_t cA = __builtin_amdgcn_perm(0u, cw.x, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw.x, 0x03030202u);
     const uint32_t cC = __builtin_amdgcn_perm(0u, cw.y, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw.y, 0x03030202u);
     char* base = slot + (c * C::NPP + 2 * px + 1) * 16;
+    // an 8-lane group of ds_write_b128 (banks = dword % 32) holds 8 consecutive px, whose pieces sit 32 B
+    // apart: storing the same column everywhere hit only 4 of the 8 16-B slots of 128 B (2-way on every
+    // store, 10.5 M conflict cycles per conv2-dgrad launch); lanes with px & 4 store the other column first
+    const int f = (px >> 2) & 1;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
         const int ry = 2 * pr + dy - 1;
         if (ry < 0 || ry > C::TR + 1) continue;
 #pragma unroll
-        for (int dx = 0; dx < 2; ++dx)
-            lds_store16(base + (ry * C::PW + dx) * 16, route_chunk(v, cA, cB, cC, cD, 2 * dy + dx));
+        for (int dx = 0; dx < 2; ++dx) {
+            const int ddx = dx ^ f;
+            lds_store16(base + (ry * C::PW + ddx) * 16, route_chunk(v, cA, cB, cC, cD, 2 * dy + ddx));
+        }
     }
 }
 
@@ -1077,9 +1083,14 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         const uint32_t cA = __builtin_amdgcn_perm(0u, c0, 0x01010000u), cB = __builtin_amdgcn_perm(0u, c0, 0x03030202u);
         const uint32_t cC = __builtin_amdgcn_perm(0u, c1, 0x01010000u), cD = __builtin_amdgcn_perm(0u, c1, 0x03030202u);
         char* base = buf + (c * C::NPXP + 2 * pr * C::HW + 2 * px) * 16;
+        // lanes with px & 4 walk the window's columns in the other order: the 8 lanes of a ds_write_b128
+        // group then fill all 8 16-B slots of 128 B (same order: 2-way on every store, 8.4 M cycles a launch)
+        const int f = (px >> 2) & 1;
 #pragma unroll
-        for (int pos = 0; pos < 4; ++pos)
+        for (int pos0 = 0; pos0 < 4; ++pos0) {
+            const int pos = pos0 ^ f;
             *reinterpret_cast<uint4*>(base + ((pos >> 1) * C::HW + (pos & 1)) * 16) = route_chunk(v, cA, cB, cC, cD, pos);
+        }
     };
     auto issue_tile = [&](int t, char* buf) {
         int n, rb;

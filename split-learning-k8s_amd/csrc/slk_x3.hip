@@ -500,6 +500,9 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 // fragments for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its <= 4 accumulators live
 // across the part's two co halves.
 // ReLU bitmap of the cut (written by conv1_fwd_x3_kernel, layout there): u32 words per (ci, u), per sample
+#ifndef SLK_X3D_DUP
+#define SLK_X3D_DUP 0
+#endif
 constexpr int RB_SAMPLE = 4 * (A_PIX / 4);  // 676 u32 = 2,704 B per sample: [channel group 4][169]
 constexpr int X3D_THREADS = 512;
 constexpr int X3D_REC = 160;                       // bytes per image pixel: h 64 | l 64 | pad 32
@@ -815,13 +818,18 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 acc[i] = mfma_f16(fh[st & 3], wh[h][tap], acc[i]);
                 ct = mfma_f16(fh[st & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
                 ct = mfma_f16(fl[st & 3], wh[h][tap], ct);
+#if SLK_X3D_DUP  // timing-only probe: every A read feeds 6 MFMAs (outputs wrong)
+                acc[i] = mfma_f16(fh[st & 3], wh[h ^ 1][tap], acc[i]);
+                ct = mfma_f16(fh[st & 3], wl[h ^ 1][tap], ct);
+                ct = mfma_f16(fl[st & 3], wh[h ^ 1][tap], ct);
+#endif
                 if (tap == 8) acc[i] += ct;
             }
             // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
             __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
             for (int st = 0; st < NS; ++st) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, SLK_X3D_DUP ? 6 : 3, 0);
                 if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
             if (!sfirst) {
@@ -837,12 +845,17 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     acc[3] = mfma_f16(fh[tap & 3], wh[h][tap], acc[3]);
                     ct = mfma_f16(fh[tap & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
                     ct = mfma_f16(fl[tap & 3], wh[h][tap], ct);
+#if SLK_X3D_DUP
+                    acc[3] = mfma_f16(fh[tap & 3], wh[h ^ 1][tap], acc[3]);
+                    ct = mfma_f16(fh[tap & 3], wl[h ^ 1][tap], ct);
+                    ct = mfma_f16(fl[tap & 3], wh[h ^ 1][tap], ct);
+#endif
                 }
                 acc[3] += ct;
                 __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
+                    __builtin_amdgcn_sched_group_barrier(0x008, SLK_X3D_DUP ? 6 : 3, 1);
                     if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
                 }
             }

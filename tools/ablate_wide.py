@@ -120,6 +120,24 @@ for i, L in enumerate(libs[1:], 1):  # the fused head's outputs vs the first lib
         if k == "slabs":
             t, ref = t.sum(0), ref.sum(0)
         chk[f"{args.libs[i]}:{k}"] = float((t.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+# conv kernels: every library's output bitwise against the first library's (same operands)
+outs = {"conv2_fwd": [out_p2, out_c2], "conv3_fwd": [out_cut, out_c3], "conv3_dgrad": [out_dp2],
+        "conv2_dgrad": [out_da1m], "conv3_wgrad": [slabs], "conv2_wgrad": [slabs], "conv1_fwd": [out_a1],
+        "conv1_wgrad": [slabs]}
+for name, ts in outs.items():
+    if args.cases and name not in args.cases.split(","):
+        continue
+    for t in ts:
+        t.zero_()
+    assert calls(libs[0])[name]() == 0
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in ts]
+    for i, L in enumerate(libs[1:], 1):
+        for t in ts:
+            t.zero_()
+        assert calls(L)[name]() == 0
+        torch.cuda.synchronize()
+        chk[f"{args.libs[i]}:{name}:bitwise"] = all(torch.equal(a, b) for a, b in zip(ts, ref))
 out = {"check_vs_lib0": chk}
 for i, path in enumerate(args.libs):
     d = {}
