@@ -293,8 +293,12 @@ int slk_cut_unpack(const float* vals, int64_t n, const uint32_t* mask, const int
 #define SLK_WIDE_SERVER_NPARAM 163850
 
 /* a1 = bf16(relu(conv1(bf16(x)) + b1)), x f32 NCHW [B,3,32,32]; one bf16 MFMA K-step (K = 27 -> 32);
- * w1b [64][32] bf16 from slk_wide_shadows. */
-int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, int B, void* stream);
+ * w1b [64][32] bf16 from slk_wide_shadows. a1bits (may be NULL): the ReLU word of every pixel, [B][1024]
+ * u64, bit c = (a1[c] > 0) — what slk_wide_conv2_dgrad masks with (8 KB a sample instead of a1's 128 KB). */
+int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, uint64_t* a1bits, int B,
+                       void* stream);
+/* The same ReLU words from a stored a1 (callers that hold a1 but not its words). */
+int slk_wide_relu_bits(const uint16_t* a1, uint64_t* a1bits, int B, void* stream);
 /* p2, code2 = pool(relu(conv2(a1) + b2)) — bf16 MFMA implicit GEMM, f32 accumulation. */
 int slk_wide_conv2_fwd(const uint16_t* a1, const uint16_t* w2f, const float* b2, uint16_t* p2, uint8_t* code2,
                        int B, void* stream);
@@ -328,7 +332,7 @@ int slk_wide_head_bwd(const uint16_t* cut, const float* wf8, const float* dlogit
  * dcut while staging it; conv3 wgrad slabs [nslab][294912 + 256]; dp2 = conv3 dgrad = the gradient of
  * p2 at its own 16 x 16 resolution (bf16, C8); conv2's dgrad and wgrad apply conv2's max-pool backward
  * (code2) to dp2 the same way; conv2 wgrad slabs [nslab][73728 + 128]; da1m = conv2 dgrad masked by
- * a1 > 0; conv1 wgrad slabs [nslab][1728 + 64] (bf16(x) operand). Slabs are [dW (torch layout) | db],
+ * a1 > 0 (its ReLU words a1bits, slk_wide_conv1_fwd); conv1 wgrad slabs [nslab][1728 + 64] (bf16(x) operand). Slabs are [dW (torch layout) | db],
  * reduced in fixed order. */
 int slk_wide_conv3_wgrad(const uint16_t* dcut, const uint8_t* code3, const uint16_t* p2, float* slabs, int B,
                          void* stream);
@@ -338,7 +342,7 @@ int slk_wide_conv3_dgrad(const uint16_t* dcut, const uint8_t* code3, const uint1
 int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
                          void* stream);
 int slk_wide_conv2_wgrad_nslab(int B);
-int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint16_t* a1,
+int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint64_t* a1bits,
                          uint16_t* da1m, int B, void* stream);
 int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream);
 int slk_wide_conv1_wgrad_nslab(int B);

@@ -117,6 +117,13 @@ __device__ __forceinline__ uint32_t mask_pos_bf16x2(uint32_t w, uint32_t a1w) {
     return w & k;
 }
 
+// the a1 > 0 bits of 4 consecutive channels (a nibble of a pixel's 64-bit ReLU word, slk_wide_conv1_fwd)
+// as bf16-half masks of the packed pairs (channels 0,1 | 2,3): bit b -> 0xFFFF in half b
+__device__ __forceinline__ uint2 relu_nibble_masks(uint32_t nib) {
+    return make_uint2((nib & 1u) * 0xFFFFu + (nib & 2u) * 0x7FFF8000u,
+                      ((nib >> 2) & 1u) * 0xFFFFu + ((nib >> 2) & 2u) * 0x7FFF8000u);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 // vmcnt is 6 bits: an allowance above 63 saturates (waiting for more than needed is always safe)
@@ -162,7 +169,7 @@ struct ConvCfg {
     // VMEM instructions per lane in the epilogue: stores (pooled value + code, plain or masked value)
     // and the a1 words loaded at tile start. Must never over-count.
     static constexpr int EPI_ST = 4 * FW;
-    static constexpr int EPI_LD = MODE == 2 ? 4 * FW : 0;
+    static constexpr int EPI_LD = MODE == 2 ? FW : 0;       // dgrad-mask: one 8-B a1 ReLU word per pixel fragment
     // EXP: the input is the max-pool backward of a POOLED gradient (HW/2 x HW/2, bf16 C8) and its
     // routing code: both move by LDS-DMA into a raw staging area (values [XR*THREADS][16 B], code
     // dwords 2 x [XR*THREADS][4 B]) and are expanded from there into the tile (exp_expand), so the
@@ -315,7 +322,8 @@ __device__ __forceinline__ void exp_store(char* slot, int i, uint4 v, uint2 cw) 
     // an 8-lane group of ds_write_b128 (banks = dword % 32) holds 8 consecutive px, whose pieces sit 32 B
     // apart: storing the same column everywhere hit only 4 of the 8 16-B slots of 128 B (2-way on every
     // store, 10.5 M conflict cycles per conv2-dgrad launch); lanes with px & 4 store the other column first
-    const int f = (px >> 2) & 1;
+    // (measured: conv3 dgrad, HW = 16, 0.5105 -> 0.5032 ms; conv2 dgrad, HW = 32, 0.5828 -> 0.6168: kept for HW = 16)
+    const int f = C::HW == 16 ? (px >> 2) & 1 : 0;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
         const int ry = 2 * pr + dy - 1;
@@ -377,21 +385,19 @@ __device__ __forceinline__ void issue_weight(const uint16_t* __restrict__ wsh, i
 
 // Epilogue operands of a tile (dgrad-mask: a1 words), loaded when the tile
 // starts so their latency hides under its main loop instead of draining the DMA queue at the epilogue.
+// dgrad-mask: the ReLU word of each of the lane's FW pixels ([B][HW*HW] u64, bit c = a1[c] > 0 for the
+// 64 channels: slk_wide_conv1_fwd writes it beside a1), 8 B per pixel instead of the 4 x 8 B of a1 words
+// the mask once read (32 VGPRs held across the main loop, and 537 MB of a1 per launch at B = 4096)
 template <class C>
 __device__ __forceinline__ void epi_prefetch(const void* __restrict__ aux, const TileState& s, int wm, int wn,
-                                             int lane, uint2 (&em)[4][C::FW]) {
+                                             int lane, uint2 (&em)[C::FW]) {
     if constexpr (C::MODE == wide::MODE_DGRAD_MASK) {
-        const int ch_base = s.cob * C::MT + wm * 64 + 4 * (lane >> 4);
+        static_assert(C::CO == 64 && C::MT == 64, "one 64-bit ReLU word covers the tile's channels");
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ch0 = ch_base + i * 16;
-#pragma unroll
-            for (int f = 0; f < C::FW; ++f) {
-                const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
-                const int y = s.rb * C::TR + q / C::HW, x = q % C::HW;
-                const size_t o = (((size_t)(s.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
-                em[i][f] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + o);
-            }
+        for (int f = 0; f < C::FW; ++f) {
+            const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
+            const int y = s.rb * C::TR + q / C::HW, x = q % C::HW;
+            em[f] = reinterpret_cast<const uint2*>(aux)[((size_t)s.n * C::HW + y) * C::HW + x];
         }
     }
 }
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
     int wslot = 0;   // ring slot of the current step
     int islot = 0;   // input slot of the current group
     bool post = false;   // a previous tile's epilogue stores may be in flight
-    uint2 em[4][C::FW];
+    uint2 em[C::FW];
 #pragma unroll 1
     while (true) {
         const bool tail = !nxt.valid;
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                 }
             }
         } else {
-            const uint16_t* a1 = reinterpret_cast<const uint16_t*>(aux);
+            // channels ch0 .. ch0 + 3 = bits 16 i + 4 (lane >> 4) .. + 3 of the pixel's ReLU word
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int ch0 = ch_base + i * 16;
@@ -645,19 +651,10 @@ __global__ __launch_bounds__(C::THREADS, C::NWV == 4 ? 2 : 1) void wide_conv_ker
                     const int q = wn * 16 * C::FW + f * 16 + (lane & 15);
                     const int y = cur.rb * C::TR + q / C::HW, x = q % C::HW;
                     const size_t o = (((size_t)(cur.n * (C::CO / 8) + (ch0 >> 3)) * C::HW + y) * C::HW + x) * 8 + (ch0 & 7);
-                    const uint2 m = em[i][f];
-                    if (SLK_WIDE_EPI2) {
-                        *reinterpret_cast<uint2*>(out + o) =
-                            make_uint2(mask_pos_bf16x2(pack_bf16x2(acc[i][f][0], acc[i][f][1]), m.x),
-                                       mask_pos_bf16x2(pack_bf16x2(acc[i][f][2], acc[i][f][3]), m.y));
-                        continue;
-                    }
-                    // a1 > 0 (bf16): sign bit clear and not +0
-                    const float v0 = (int)(m.x << 16) > 0 ? acc[i][f][0] : 0.f;
-                    const float v1 = (int)(m.x & 0xFFFF0000u) > 0 ? acc[i][f][1] : 0.f;
-                    const float v2 = (int)(m.y << 16) > 0 ? acc[i][f][2] : 0.f;
-                    const float v3 = (int)(m.y & 0xFFFF0000u) > 0 ? acc[i][f][3] : 0.f;
-                    *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                    const uint32_t word = (i < 2) ? em[f].x : em[f].y;
+                    const uint2 m = relu_nibble_masks(word >> (16 * (i & 1) + 4 * (lane >> 4)));
+                    *reinterpret_cast<uint2*>(out + o) = make_uint2(pack_bf16x2(acc[i][f][0], acc[i][f][1]) & m.x,
+                                                                    pack_bf16x2(acc[i][f][2], acc[i][f][3]) & m.y);
                 }
             }
         }
@@ -960,10 +957,10 @@ extern "C" int slk_wide_conv3_dgrad(const uint16_t* dcut, const uint8_t* code3, 
     SLK_CHECK_ARG(code3 != nullptr);
     return launch_conv<CfgConv3Dgrad>(dcut, w3d, nullptr, dp2, const_cast<uint8_t*>(code3), B, stream);
 }
-extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint16_t* a1,
+extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint64_t* a1bits,
                                     uint16_t* da1m, int B, void* stream) {
-    SLK_CHECK_ARG(code2 != nullptr);
-    return launch_conv<CfgConv2Dgrad>(dp2, w2d, a1, da1m, const_cast<uint8_t*>(code2), B, stream);
+    SLK_CHECK_ARG(code2 != nullptr && a1bits != nullptr);
+    return launch_conv<CfgConv2Dgrad>(dp2, w2d, a1bits, da1m, const_cast<uint8_t*>(code2), B, stream);
 }
 
 // ============================================================================ conv3x3 weight gradient
@@ -1263,8 +1260,13 @@ __device__ __forceinline__ int im2col_off(int k) {
 // Forward: a1[co][px] = relu(sum_k W1b[co][k] * bf16(x)[k][px] + b1[co]); A = W1b (4 fragments in
 // registers for the whole launch), B = the im2col fragment of 16 pixels. Wave w of a workgroup takes
 // pixel fragments w, w+4, ... of its image; grid-strided over images.
+// a1bits (optional): the ReLU word of every pixel, [B][1024] u64, bit c = (the stored bf16 a1[c] != 0), i.e.
+// a1[c] > 0 (relu output: +0 or positive) — conv2's dgrad masks with it instead of re-reading a1. Lane
+// (col, q) holds channels 16 cf + 4 q + r of pixel col; the four q lanes' nibbles are OR-combined by two
+// lane swaps and lanes q = 0 store 16 consecutive pixels' words (128 B).
 __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ w1b,
-                                                             const float* __restrict__ b1, uint16_t* __restrict__ a1, int B) {
+                                                             const float* __restrict__ b1, uint16_t* __restrict__ a1, int B,
+                                                             uint2* __restrict__ a1bits = nullptr) {
     __shared__ float xs[3 * C1P * C1P];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int q = lane >> 4, col = lane & 15;
@@ -1299,6 +1301,7 @@ __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __rest
 #pragma unroll
             for (int j = 0; j < 8; ++j) bv[j] = (__bf16)g[j];
             uint16_t* dst = a1 + ((size_t)(n * 8) * 1024 + y * 32 + xx) * 8 + 4 * (q & 1);
+            uint32_t wlo = 0u, whi = 0u;
 #pragma unroll
             for (int cf = 0; cf < 4; ++cf) {
                 f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[cf], bv, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -1308,9 +1311,20 @@ __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __rest
                     const float t = acc[r] + bias[cf][r];
                     o[r] = t > 0.f ? t : 0.f;
                 }
+                const uint32_t p0 = pack_bf16x2(o[0], o[1]), p1 = pack_bf16x2(o[2], o[3]);
                 // channels cf*16 + 4q .. +3 = chunk 2cf + (q >> 1), offset 4 (q & 1)
-                *reinterpret_cast<uint2*>(dst + (size_t)(2 * cf + (q >> 1)) * 1024 * 8) =
-                    make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+                *reinterpret_cast<uint2*>(dst + (size_t)(2 * cf + (q >> 1)) * 1024 * 8) = make_uint2(p0, p1);
+                const uint32_t nib = ((p0 & 0xFFFFu) ? 1u : 0u) | ((p0 >> 16) ? 2u : 0u) | ((p1 & 0xFFFFu) ? 4u : 0u) |
+                                     ((p1 >> 16) ? 8u : 0u);
+                if (cf < 2) wlo |= nib << (16 * cf + 4 * q);
+                else whi |= nib << (16 * (cf - 2) + 4 * q);
+            }
+            if (a1bits) {
+                wlo |= (uint32_t)__shfl_xor((int)wlo, 32);
+                whi |= (uint32_t)__shfl_xor((int)whi, 32);
+                wlo |= (uint32_t)__shfl_xor((int)wlo, 16);
+                whi |= (uint32_t)__shfl_xor((int)whi, 16);
+                if (q == 0) a1bits[(size_t)n * 1024 + y * 32 + xx] = make_uint2(wlo, whi);
             }
         }
     }
@@ -1423,11 +1437,42 @@ __global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __re
     }
 }
 
-extern "C" int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, int B, void* stream) {
+extern "C" int slk_wide_conv1_fwd(const float* x, const uint16_t* w1b, const float* b1, uint16_t* a1, uint64_t* a1bits,
+                                  int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && x && w1b && b1 && a1);
     if (B == 0) return 0;
     const int grid = B < 2048 ? B : 2048;
-    hipLaunchKernelGGL(wide_conv1_fwd_kernel, dim3(grid), dim3(256), 0, slk_stream(stream), x, w1b, b1, a1, B);
+    hipLaunchKernelGGL(wide_conv1_fwd_kernel, dim3(grid), dim3(256), 0, slk_stream(stream), x, w1b, b1, a1, B,
+                       reinterpret_cast<uint2*>(a1bits));
+    return slk_launch_status();
+}
+
+// the ReLU words of a1 (as slk_wide_conv1_fwd writes them) from a stored a1: thread = pixel, its 8 chunks
+__global__ __launch_bounds__(256) void wide_relu_bits_kernel(const uint4* __restrict__ a1, uint2* __restrict__ bits,
+                                                             int npix) {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // global pixel (sample * 1024 + p)
+    if (i >= npix) return;
+    const int n = i >> 10, p = i & 1023;
+    uint32_t w[2] = {0u, 0u};
+#pragma unroll
+    for (int c8 = 0; c8 < 8; ++c8) {
+        const uint4 v = a1[((size_t)n * 8 + c8) * 1024 + p];
+        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t h = (d[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            const int c = 8 * c8 + k;
+            w[c >> 5] |= ((int16_t)h > 0 ? 1u : 0u) << (c & 31);   // a1 > 0 (sign clear, not +0)
+        }
+    }
+    bits[i] = make_uint2(w[0], w[1]);
+}
+extern "C" int slk_wide_relu_bits(const uint16_t* a1, uint64_t* a1bits, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && a1 && a1bits);
+    if (B == 0) return 0;
+    const int npix = B * 1024;
+    hipLaunchKernelGGL(wide_relu_bits_kernel, dim3((npix + 255) / 256), dim3(256), 0, slk_stream(stream),
+                       reinterpret_cast<const uint4*>(a1), reinterpret_cast<uint2*>(a1bits), npix);
     return slk_launch_status();
 }
 extern "C" int slk_wide_conv1_wgrad_nslab(int B) { return B >= 0 ? C1W_GRID : 0; }

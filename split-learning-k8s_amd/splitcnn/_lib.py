@@ -73,7 +73,8 @@ _SIGS = {
     "slk_sgd_multi_from_slabs": [_P, _P, _P, _P, _P, _I, _F, _P, _I, _F, _P, _I, _P, _P],
     "slk_mnist_batch": [_P, _P, _I, _P, _I, _F, _F, _P, _P, _P, _P],
     # widened split CNN (BASELINE config 5)
-    "slk_wide_conv1_fwd": [_P, _P, _P, _P, _I, _P],
+    "slk_wide_conv1_fwd": [_P, _P, _P, _P, _P, _I, _P],
+    "slk_wide_relu_bits": [_P, _P, _I, _P],
     "slk_wide_conv2_fwd": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_conv3_fwd": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_head": [_P, _P, _P, _P, _P, _U, _U, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],

@@ -211,13 +211,15 @@ def build_shadows(W1, W2, W3, sh, stream):
        sh["w3f"].data_ptr(), sh["w3d"].data_ptr(), stream)
 
 
-def client_forward_kernels(x, sh, b1, b2, b3, a1, p2, code2, cut, code3):
-    """conv1 + ReLU -> conv2 + ReLU + pool -> conv3 + ReLU + pool (the cut), C8 bf16."""
+def client_forward_kernels(x, sh, b1, b2, b3, a1, p2, code2, cut, code3, a1bits=None):
+    """conv1 + ReLU -> conv2 + ReLU + pool -> conv3 + ReLU + pool (the cut), C8 bf16. a1bits ([B, 1024]
+    int64): conv1 also writes the ReLU word of every pixel (bit c = a1[c] > 0), conv2's dgrad mask."""
     B = x.shape[0]
     _dev(x, "x", (B, 3, 32, 32))
     s = _stream(x)
     b1p, b2p, b3p = _f32p(b1, "conv1.bias", 64), _f32p(b2, "conv2.bias", 128), _f32p(b3, "conv3.bias", 256)
-    _k("wide_conv1_fwd", x.data_ptr(), sh["w1b"].data_ptr(), b1p, a1.data_ptr(), B, s)
+    bits = _dev(a1bits, "a1bits", (B, 1024), torch.int64) if a1bits is not None else None
+    _k("wide_conv1_fwd", x.data_ptr(), sh["w1b"].data_ptr(), b1p, a1.data_ptr(), bits, B, s)
     _k("wide_conv2_fwd", a1.data_ptr(), sh["w2f"].data_ptr(), b2p, p2.data_ptr(), code2.data_ptr(), B, s)
     _k("wide_conv3_fwd", p2.data_ptr(), sh["w3f"].data_ptr(), b3p, cut.data_ptr(), code3.data_ptr(), B, s)
 
@@ -229,18 +231,26 @@ def client_backward_slab_shapes(B):
 
 def client_backward_kernels(dcut, saved, w2d, w3d, scratch, s1, s2, s3):
     """activations.backward(dcut) of the client stack into three slab sets [dW | db] (conv1, conv2,
-    conv3). saved = (x, a1, p2, code2, code3) of the forward; scratch = (dp2, da1m). No unpooled
-    gradient is stored: conv3's kernels route the pooled dcut by code3 while staging it, conv3's dgrad
-    writes dp2 (the gradient of p2, 16 x 16) and conv2's kernels route dp2 by code2 the same way."""
-    x, a1, p2, code2, code3 = saved
+    conv3). saved = (x, a1, p2, code2, code3[, a1bits]) of the forward; scratch = (dp2, da1m). No
+    unpooled gradient is stored: conv3's kernels route the pooled dcut by code3 while staging it, conv3's
+    dgrad writes dp2 (the gradient of p2, 16 x 16) and conv2's kernels route dp2 by code2 the same way.
+    conv2's dgrad masks by a1 > 0 from a1's ReLU words (slk_wide_conv1_fwd writes them; computed from a1
+    here when the forward did not)."""
+    x, a1, p2, code2, code3 = saved[:5]
     dp2, da1m = scratch
     B = x.shape[0]
     s = _stream(dp2)
     _dev(dcut, "dcut", (B,) + CUT_SHAPE, _BF)
+    if len(saved) > 5 and saved[5] is not None:
+        _dev(saved[5], "a1bits", (B, 1024), torch.int64)
+        a1bits = saved[5]
+    else:
+        a1bits = torch.empty((B, 1024), dtype=torch.int64, device=dp2.device)
+        _k("wide_relu_bits", a1.data_ptr(), a1bits.data_ptr(), B, s)
     _k("wide_conv3_wgrad", dcut.data_ptr(), code3.data_ptr(), p2.data_ptr(), s3.data_ptr(), B, s)
     _k("wide_conv3_dgrad", dcut.data_ptr(), code3.data_ptr(), w3d.data_ptr(), dp2.data_ptr(), B, s)
     _k("wide_conv2_wgrad", dp2.data_ptr(), code2.data_ptr(), a1.data_ptr(), s2.data_ptr(), B, s)
-    _k("wide_conv2_dgrad", dp2.data_ptr(), code2.data_ptr(), w2d.data_ptr(), a1.data_ptr(), da1m.data_ptr(), B, s)
+    _k("wide_conv2_dgrad", dp2.data_ptr(), code2.data_ptr(), w2d.data_ptr(), a1bits.data_ptr(), da1m.data_ptr(), B, s)
     _k("wide_conv1_wgrad", x.data_ptr(), da1m.data_ptr(), s1.data_ptr(), B, s)
 
 
@@ -270,8 +280,9 @@ class _WideClientFn(torch.autograd.Function):
         code2 = torch.empty((B, 16, 16, 16, 8), dtype=_U8, device=dev)
         cut = torch.empty((B,) + CUT_SHAPE, dtype=_BF, device=dev)
         code3 = torch.empty((B,) + CUT_SHAPE, dtype=_U8, device=dev)
-        client_forward_kernels(x, sh, Ws[1], Ws[3], Ws[5], a1, p2, code2, cut, code3)
-        ctx.save_for_backward(x, a1, p2, code2, code3, sh["w2d"], sh["w3d"])
+        a1bits = torch.empty((B, 1024), dtype=torch.int64, device=dev)
+        client_forward_kernels(x, sh, Ws[1], Ws[3], Ws[5], a1, p2, code2, cut, code3, a1bits)
+        ctx.save_for_backward(x, a1, p2, code2, code3, a1bits, sh["w2d"], sh["w3d"])
         return c8_to_nchw(cut)
 
     @staticmethod
@@ -279,12 +290,12 @@ class _WideClientFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             raise NotImplementedError("splitcnn: gradient w.r.t. the client's input images is not part of the "
                                       "split step (src/client_part.py:110-114)")
-        x, a1, p2, code2, code3, w2d, w3d = ctx.saved_tensors
+        x, a1, p2, code2, code3, a1bits, w2d, w3d = ctx.saved_tensors
         B, dev = x.shape[0], x.device
         dcut = nchw_to_c8(g.to(_BF))
         scratch = client_backward_scratch(B, lambda n, sh_, dt: torch.empty(sh_, dtype=dt, device=dev))
         slabs = [torch.empty(sh_, dtype=_F32, device=dev) for sh_ in client_backward_slab_shapes(B)]
-        client_backward_kernels(dcut, (x, a1, p2, code2, code3), w2d, w3d, scratch, *slabs)
+        client_backward_kernels(dcut, (x, a1, p2, code2, code3, a1bits), w2d, w3d, scratch, *slabs)
         g1, g2, g3 = (_reduce(sl) for sl in slabs)
         return (None, g1[:1728].view(64, 3, 3, 3), g1[1728:], g2[:73728].view(128, 64, 3, 3), g2[73728:],
                 g3[:294912].view(256, 128, 3, 3), g3[294912:])
@@ -371,16 +382,17 @@ class WideClientStage:
         cut = out if out is not None else self._b(f"cut{tag}", (B,) + CUT_SHAPE, _BF)
         _dev(cut, "cut", (B,) + CUT_SHAPE, _BF)
         code3 = self._b(f"code3{tag}", (B,) + CUT_SHAPE, _U8)
+        a1bits = self._b(f"a1bits{tag}", (B, 1024), torch.int64)
         client_forward_kernels(x, self.sh, self._p("b1", 64), self._p("b2", 128), self._p("b3", 256),
-                               a1, p2, code2, cut, code3)
+                               a1, p2, code2, cut, code3, a1bits)
         self._x, self._a1, self._p2, self._code2, self._code3 = x, a1, p2, code2, code3
-        self._saved[tag] = (x, a1, p2, code2, code3)
+        self._saved[tag] = (x, a1, p2, code2, code3, a1bits)
         return cut
 
     def backward_slabs(self, dcut: torch.Tensor, tag=""):
         """Client backward into three slab sets (conv1, conv2, conv3); returns them."""
         B = self._saved[tag][0].shape[0]
-        self._x, self._a1, self._p2, self._code2, self._code3 = self._saved[tag]
+        self._x, self._a1, self._p2, self._code2, self._code3 = self._saved[tag][:5]
         scratch = client_backward_scratch(B, self._b)
         s1, s2, s3 = (self._b(n, shp, _F32) for n, shp in zip(("s1", "s2", "s3"), client_backward_slab_shapes(B)))
         client_backward_kernels(dcut, self._saved[tag], self.sh["w2d"], self.sh["w3d"], scratch, s1, s2, s3)

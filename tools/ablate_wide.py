@@ -58,8 +58,12 @@ hdl = torch.randn(B, 10, device=dev, generator=g) / B
 hdcut = torch.empty_like(cut)
 
 libs = []
+a1bits = torch.empty(B, 1024, dtype=torch.int64, device=dev)
 for path in args.libs:
     L = ctypes.CDLL(path)
+    L._bits = hasattr(L, "slk_wide_relu_bits")
+    if L._bits:
+        assert L.slk_wide_relu_bits(p(a1), p(a1bits), B, P(s)) == 0
     L.slk_wide_head_work.restype = ctypes.c_int
     L.slk_wide_head_nslab.restype = ctypes.c_int
     L.slk_wide_head_fwd.argtypes = [P] * 4 + [ctypes.c_uint, ctypes.c_uint, ctypes.c_float] + [P] + [ctypes.c_int] * 2 + [P]
@@ -77,14 +81,17 @@ herr = torch.zeros(1, dtype=torch.int32, device=dev)
 
 def calls(L):
     return {
-        "conv1_fwd": lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), B, P(s)),
+        # round 5 ABI: conv1 also writes the ReLU words, conv2's dgrad reads them instead of a1
+        "conv1_fwd": (lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), p(a1bits), B, P(s))) if L._bits
+        else (lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), B, P(s))),
         "conv2_fwd": lambda: L.slk_wide_conv2_fwd(p(a1), p(w2f), p(b2), p(out_p2), p(out_c2), B, P(s)),
         "conv3_fwd": lambda: L.slk_wide_conv3_fwd(p(p2), p(w3f), p(b3), p(out_cut), p(out_c3), B, P(s)),
         # pooled gradients + codes: conv3's kernels route dcut by code3, conv2's route dp2 by code2
         "conv3_wgrad": lambda: L.slk_wide_conv3_wgrad(p(dcut), p(code3), p(p2), p(slabs), B, P(s)),
         "conv3_dgrad": lambda: L.slk_wide_conv3_dgrad(p(dcut), p(code3), p(w3d), p(out_dp2), B, P(s)),
         "conv2_wgrad": lambda: L.slk_wide_conv2_wgrad(p(dp2), p(code2), p(a1), p(slabs), B, P(s)),
-        "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1), p(out_da1m), B, P(s)),
+        "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1bits if L._bits else a1),
+                                                      p(out_da1m), B, P(s)),
         "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
         "head_fwd": lambda: L.slk_wide_head_fwd(p(cut), p(wf8), p(bfc), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hlog),
                                                 0, B, P(s)),
