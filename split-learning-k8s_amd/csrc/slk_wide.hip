@@ -1320,10 +1320,16 @@ __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __rest
                 else whi |= nib << (16 * (cf - 2) + 4 * q);
             }
             if (a1bits) {
-                wlo |= (uint32_t)__shfl_xor((int)wlo, 32);
-                whi |= (uint32_t)__shfl_xor((int)whi, 32);
-                wlo |= (uint32_t)__shfl_xor((int)wlo, 16);
-                whi |= (uint32_t)__shfl_xor((int)whi, 16);
+                // OR over lanes l, l ^ 32, l ^ 16 (gfx950 lane swaps: a swap of a value with itself
+                // returns it with the partner half's copy in the other half)
+                auto s32 = __builtin_amdgcn_permlane32_swap(wlo, wlo, false, false);
+                wlo = s32[0] | s32[1];
+                s32 = __builtin_amdgcn_permlane32_swap(whi, whi, false, false);
+                whi = s32[0] | s32[1];
+                auto s16 = __builtin_amdgcn_permlane16_swap(wlo, wlo, false, false);
+                wlo = s16[0] | s16[1];
+                s16 = __builtin_amdgcn_permlane16_swap(whi, whi, false, false);
+                whi = s16[0] | s16[1];
                 if (q == 0) a1bits[(size_t)n * 1024 + y * 32 + xx] = make_uint2(wlo, whi);
             }
         }

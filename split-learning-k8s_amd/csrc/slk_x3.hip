@@ -500,8 +500,8 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 // fragments for both co halves (2 x 9 x (h, l) = 144 VGPRs) stay in registers, its <= 4 accumulators live
 // across the part's two co halves.
 // ReLU bitmap of the cut (written by conv1_fwd_x3_kernel, layout there): u32 words per (ci, u), per sample
-#ifndef SLK_X3D_DUP
-#define SLK_X3D_DUP 0
+#ifndef SLK_X3W_ROUND4
+#define SLK_X3W_ROUND4 0
 #endif
 constexpr int RB_SAMPLE = 4 * (A_PIX / 4);  // 676 u32 = 2,704 B per sample: [channel group 4][169]
 constexpr int X3D_THREADS = 512;
@@ -818,18 +818,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 acc[i] = mfma_f16(fh[st & 3], wh[h][tap], acc[i]);
                 ct = mfma_f16(fh[st & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
                 ct = mfma_f16(fl[st & 3], wh[h][tap], ct);
-#if SLK_X3D_DUP  // timing-only probe: every A read feeds 6 MFMAs (outputs wrong)
-                acc[i] = mfma_f16(fh[st & 3], wh[h ^ 1][tap], acc[i]);
-                ct = mfma_f16(fh[st & 3], wl[h ^ 1][tap], ct);
-                ct = mfma_f16(fl[st & 3], wh[h ^ 1][tap], ct);
-#endif
                 if (tap == 8) acc[i] += ct;
             }
             // hold the schedule to that order (hipcc otherwise sinks every read next to its MFMAs)
             __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
             for (int st = 0; st < NS; ++st) {
-                __builtin_amdgcn_sched_group_barrier(0x008, SLK_X3D_DUP ? 6 : 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
                 if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
             if (!sfirst) {
@@ -845,17 +840,12 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     acc[3] = mfma_f16(fh[tap & 3], wh[h][tap], acc[3]);
                     ct = mfma_f16(fh[tap & 3], wl[h][tap], tap == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ct);
                     ct = mfma_f16(fl[tap & 3], wh[h][tap], ct);
-#if SLK_X3D_DUP
-                    acc[3] = mfma_f16(fh[tap & 3], wh[h ^ 1][tap], acc[3]);
-                    ct = mfma_f16(fh[tap & 3], wl[h ^ 1][tap], ct);
-                    ct = mfma_f16(fl[tap & 3], wh[h ^ 1][tap], ct);
-#endif
                 }
                 acc[3] += ct;
                 __builtin_amdgcn_sched_group_barrier(0x100, 6, 1);
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, SLK_X3D_DUP ? 6 : 3, 1);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
                     if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
                 }
             }
@@ -1251,6 +1241,271 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3_kernel(
     }
 }
 
+// ============================================================================ conv2 wgrad, both co halves per workgroup
+// The act16-image form of the x3 wgrad (round 5) with one workgroup per K share owning ALL of dW2: the
+// unit is (sample, sixth) = output rows 4t .. 4t + 3 (K = 96 pixels = 3 K-steps), so both co halves' dY
+// planes (4 x 6 KiB) and the unit's input image (rows 4t .. 4t + 5, 2 x 9.75 KiB) fit twice into LDS
+// (the 8-row unit with both co halves needed 164,864 B, 1 KiB over): the input image is moved by LDS-DMA
+// once for the 64 co instead of once per co half by two workgroups (the DMA of that image was 11 % of the
+// round-4 kernel), and no K-parity partial sums are exchanged at the end. 8 waves = (tap group tg, co half
+// c, ci half h), wave = 4 tg + 2 c + h: the two waves of a SIMD (w, w + 4) carry one tap group each; per
+// unit a wave does all 3 K-steps x its taps x both M tiles of its co half — the same fragment reads and
+// MFMAs per unit as the round-4 wave. dY staging as conv2_wgrad_x3_kernel (register loads two units
+// ahead, routed one unit ahead), items (4-co group, co half, window) with the co half's planes offset by
+// 64 B so a 16-lane store group (8 groups x 2 co halves of one window) covers 32 distinct banks.
+constexpr int X3Q_ROWS = 4;                              // output rows per unit (6 units per sample)
+constexpr int X3Q_Q = X3Q_ROWS * 24;                     // 96 output pixels = K per unit
+constexpr int X3Q_DYP = X3Q_Q * 64;                      // 6,144 B per dY plane (32 co of one co half)
+constexpr int X3Q_DYC = 2 * X3Q_DYP + 64;                // co half stride: h | l planes + 64 B
+constexpr int X3Q_XPIX = (X3Q_ROWS + 2) * A_HW;          // 156 input pixels per unit
+constexpr int X3Q_XP = X3Q_XPIX * 64;                    // 9,984 B per input plane
+constexpr int X3Q_DYOFF = 2 * X3Q_XP;                    // dY planes after the input planes (1 KiB aligned start)
+constexpr int X3Q_BUF = (X3Q_DYOFF + 2 * X3Q_DYC + 1023) / 1024 * 1024;  // 45,056 B per buffer
+constexpr int X3Q_NKS = 256;                             // K shares (slabs): one workgroup per CU
+constexpr int X3Q_DYITEMS = 24 * 16;                     // (window, 4-co group, co half) items per unit
+constexpr int X3Q_XPIECES = X3Q_XP / 1024 + 1;           // 10 DMA pieces per input plane (the last 768 B)
+static_assert(2 * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
+
+// LDS-DMA of unit uu's input image (rows 4t .. 4t + 5 of both planes of the sample's act16 image)
+__device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
+    const int b = uu / 6, t = uu - (uu / 6) * 6;
+    const char* src = reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t * (X3Q_ROWS * A_HW * 64);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int k = wave + 8 * r;  // piece k of the 20: plane k / 10, piece k % 10
+        if (k < 2 * X3Q_XPIECES) {
+            const int pl = k >= X3Q_XPIECES ? 1 : 0, pp = k - X3Q_XPIECES * pl;
+            if (pp < X3Q_XPIECES - 1 || lane < (X3Q_XP % 1024) / 16)
+                glds16_so(src + pl * X3S_PLANE, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3Q_XP + pp * 1024);
+        }
+    }
+}
+
+__global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
+    const uint16_t* __restrict__ act16, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
+    const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3Q_BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = wave & 1, c = (wave >> 1) & 1, tg = wave >> 2;
+    const int ks = blockIdx.x, nks = gridDim.x;
+    const int U = 6 * B;
+    float* red = reinterpret_cast<float*>(smem);  // prologue scratch (buffer 0, before any staging)
+
+    // launch scales: max over the batch of the per-sample maxima (as conv2_wgrad_x3_kernel)
+    float ma = 0.f, md = 0.f;
+    for (int i = tid; i < B; i += X3W_THREADS) {
+        ma = fmaxf(ma, act_amax[i]);
+        md = fmaxf(md, dp_amax[i]);
+    }
+    ma = wave_max(ma);
+    md = wave_max(md);
+    if (lane == 0) {
+        red[wave] = ma;
+        red[8 + wave] = md;
+    }
+    __syncthreads();
+    ma = red[0];
+    md = red[8];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+        ma = fmaxf(ma, red[i]);
+        md = fmaxf(md, red[8 + i]);
+    }
+    __syncthreads();
+    const int sx = x3_exp(ma), sd = x3_exp(md);
+    int sb_ld = 0;
+
+    // dY items: i = tid < 384 -> 4-co group dg = i & 7 of co half ci2 = (i >> 3) & 1, window dw = i >> 4
+    // (24 windows: 2 window rows x 12); waves 6-7 hold none
+    const bool dstage = tid < X3Q_DYITEMS;
+    const int dg = tid & 7, dc = (tid >> 3) & 1, dw = min(tid >> 4, 23);
+    float dv[4];
+    uint32_t dcb[4];
+    auto load_dy = [&](int uu) {
+        const int b = uu / 6, t = uu - (uu / 6) * 6;
+        const int w = (2 * t + dw / 12) * P_HW + dw % 12;
+        const size_t o = (size_t)b * P_SAMPLE + (32 * dc + 4 * dg) * P_WIN + w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            dv[j] = dpooled[o + j * P_WIN];
+            dcb[j] = code[o + j * P_WIN];
+        }
+        sb_ld = max(x3_exp(act_amax[b]), sx);
+    };
+    float dbacc[4] = {0.f, 0.f, 0.f, 0.f};
+    auto store_dy = [&](char* img, bool real) {
+        const float dsc = ldexpf(1.f, sd + sx - sb_ld);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dbacc[j] = (real && dcb[j] != (uint32_t)CODE_NONE) ? dbacc[j] + dv[j] : dbacc[j];
+        uint32_t hv[2], lv[2];
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+            const float a = dv[j] * dsc, cc = dv[j + 1] * dsc;
+            const _Float16 ha = (_Float16)a, hc = (_Float16)cc;
+            const _Float16 la = (_Float16)(a - (float)ha), lc = (_Float16)(cc - (float)hc);
+            hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
+            lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
+        }
+        const uint32_t dcw = dcb[0] | (dcb[1] << 8) | (dcb[2] << 16) | (dcb[3] << 24);
+        const uint32_t cA = __builtin_amdgcn_perm(0u, dcw, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw, 0x03030202u);
+        const int wy = dw / 12, wx = dw % 12;
+        char* plane = img + X3Q_DYOFF + dc * X3Q_DYC;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos) {
+            const uint32_t T = 0xFFu << (8 * pos);
+            const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
+            const int q = (2 * wy + (pos >> 1)) * 24 + 2 * wx + (pos & 1);
+            // co tile (dg >> 2) sits in slot (dg >> 2) ^ ((q >> 3) & 1), as in conv2_wgrad_x3_kernel
+            char* o = plane + q * 64 + ((((dg >> 2) ^ (q >> 3)) & 1) * 32) + 8 * (dg & 3);
+            *reinterpret_cast<uint2*>(o) = make_uint2(hv[0] & mA, hv[1] & mB);
+            *reinterpret_cast<uint2*>(o + X3Q_DYP) = make_uint2(lv[0] & mA, lv[1] & mB);
+        }
+    };
+
+    // transposed-read bases (conv2_wgrad_x3_kernel's, every K-step j = 0..2 of the 4-row unit)
+    const int g4 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    int abase[3][2], xbase[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int idx = 2 * j + (g4 >> 1);
+        const int orow = 2 * (idx / 3) + (g4 & 1), seg = idx % 3;
+        const int q0 = 24 * orow + 8 * seg;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+            abase[j][mi] = X3Q_DYOFF + c * X3Q_DYC + (q0 + qq) * 64 + ((mi ^ ((q0 >> 3) & 1)) * 32) + pp * 8;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int x = 8 * seg + qq + kx;
+            xbase[j][kx] = ((orow * A_HW + x) * 64) + (h ^ ((x >> 1) & 1)) * 32 + pp * 8;
+        }
+    }
+    typedef __fp16 hf4 __attribute__((__vector_size__(8)));
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) hf4* lp4;
+    auto trr = [&](const char* p) -> f16x8 {
+        const f16x4 lo = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)p));
+        const f16x4 hi = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)(p + 4 * 64)));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+
+    f32x4 acc[2][5];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto unit_mfma = [&](const char* img, auto TG) {
+        constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
+        constexpr int N = 3 * NT;
+        f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
+        auto rdA = [&](int j, int slot) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                Ah[slot][mi] = trr(img + abase[j][mi]);
+                Al[slot][mi] = trr(img + X3Q_DYP + abase[j][mi]);
+            }
+        };
+        auto rdB = [&](int n, int slot) {
+            const int j = n / NT, tap = T0 + n % NT;
+            const int to = (tap / 3) * A_HW * 64;
+            Bh[slot] = trr(img + xbase[j][tap % 3] + to);
+            Bl[slot] = trr(img + X3Q_XP + xbase[j][tap % 3] + to);
+        };
+        rdA(0, 0);
+        rdB(0, 0);
+        rdB(1, 1);
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            if (n + 2 < N) {
+                rdB(n + 2, (n + 2) % 3);
+                if ((n + 2) % NT == 0) rdA((n + 2) / NT, ((n + 2) / NT) & 1);
+            }
+            const int j = n / NT, t = n % NT;
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+                acc[mi][t] = mfma_x3(Ah[j & 1][mi], Al[j & 1][mi], Bh[n % 3], Bl[n % 3], acc[mi][t]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            if (n + 2 < N) {
+                if ((n + 2) % NT == 0) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                else __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+            }
+        }
+    };
+
+    // a contiguous range of units per K share (the six parts of a sample back to back: shared halo rows
+    // and dY window rows come from L2)
+    const int per = (U + nks - 1) / nks;
+    const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
+    int u = u0;
+    if (u < u1) {
+        x3q_issue_img(act16, u, wave, lane, lds_u32(smem));
+        if (dstage) {
+            load_dy(u);
+            store_dy(smem, true);
+            load_dy(min(u + 1, u1 - 1));
+        }
+    }
+    int k = 0;
+#pragma unroll 1
+    for (; u < u1; ++u, ++k) {
+        // this unit's image DMA landed; the 8 dY loads (every staging wave's last memory instructions,
+        // issued after its DMA) may stay in flight
+        if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __syncthreads();  // buffer k&1 complete; buffer (k+1)&1 free
+        const int nx = u + 1, nx2 = u + 2;
+        const char* img = smem + (k & 1) * X3Q_BUF;
+        char* nimg = smem + ((k & 1) ^ 1) * X3Q_BUF;
+        // tap-group-1 waves (the lighter MFMA share) route dY before their MFMAs, tap-group-0 after:
+        // the two waves of a SIMD overlap routing with MFMAs; store_dy before the DMA issue (hipcc does
+        // not count the asm DMAs: its wait for the dY registers would also wait for them)
+        const bool dfirst = tg == 1;
+        if (dfirst && dstage) store_dy(nimg, nx < u1);
+        x3q_issue_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
+        if (dfirst && dstage) load_dy(min(nx2, u1 - 1));
+        if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
+        else unit_mfma(img, std::integral_constant<int, 1>{});
+        if (!dfirst && dstage) {
+            store_dy(nimg, nx < u1);
+            load_dy(min(nx2, u1 - 1));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped) image DMA lands before LDS reuse
+    __syncthreads();
+    // db partials of the staging items -> LDS; co = 32 dc + 4 dg + j summed over the 24 windows in order
+    float* dbs = reinterpret_cast<float*>(smem);
+    if (dstage)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dbs[tid * 4 + j] = dbacc[j];
+    __syncthreads();
+    float* slab = slabs + (size_t)ks * (W2_N + C2);
+    if (tid < C2) {
+        const int cc = tid >> 5, g = (tid >> 2) & 7, j = tid & 3;
+        float sum = 0.f;
+        for (int w = 0; w < 24; ++w) sum += dbs[(w * 16 + cc * 8 + g) * 4 + j];
+        slab[W2_N + tid] = sum;
+    }
+    const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
+    const int ci = 16 * h + (lane & 15);
+    const int nt = tg ? 4 : 5;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+            if (t < nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = 32 * c + 16 * mi + 4 * (lane >> 4) + r;
+                    slab[(co * C1 + ci) * 9 + 5 * tg + t] = x3_unscale(acc[mi][t][r], us1, us2);
+                }
+    }
+}
+
 // ============================================================================ conv1 -> x3 input images
 // The client's conv1 + ReLU (src/model_def.py:8-9, the per-pixel FMA order of slk_client.hip's
 // conv1_fwd_kernel: taps from 0, then + bias) writing the server's x3 operand directly: per sample, the
@@ -1445,13 +1700,15 @@ extern "C" int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax
     return slk_launch_status();
 }
 
-extern "C" int slk_conv2_wgrad_x3_nslab(int B) { return B <= 0 ? 0 : (3 * B < X3W_NKS ? 3 * B : X3W_NKS); }
+// round 5: the slab count of both x3 wgrad entries is the images kernel's (conv2_wgrad_x3q_kernel: 6 units a
+// sample, up to X3Q_NKS shares); the f32-act kernel runs nslab / 2 K shares x 2 co halves into the same slabs
+extern "C" int slk_conv2_wgrad_x3_nslab(int B) { return B <= 0 ? 0 : (6 * B < X3Q_NKS ? 6 * B : X3Q_NKS); }
 
 extern "C" int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
                                   const uint8_t* code, float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && act && act_amax && dpooled && dp_amax && code && slabs);
     if (B == 0) return 0;
-    const int nks = slk_conv2_wgrad_x3_nslab(B);
+    const int nks = slk_conv2_wgrad_x3_nslab(B);  // one slab per K share (both co-half workgroups write it)
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<false>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), act,
                        act_amax, dpooled, dp_amax, code, slabs, B, nullptr);
     return slk_launch_status();
@@ -1462,7 +1719,12 @@ extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax,
     SLK_CHECK_ARG(B >= 0 && act16 && act_amax && dpooled && dp_amax && code && slabs);
     if (B == 0) return 0;
     const int nks = slk_conv2_wgrad_x3_nslab(B);
+#if SLK_X3W_ROUND4  // profiling A/B: the round-4 kernel (one co half per workgroup, 8-row units)
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<true>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), nullptr,
                        act_amax, dpooled, dp_amax, code, slabs, B, act16);
+#else
+    hipLaunchKernelGGL(conv2_wgrad_x3q_kernel, dim3(nks), dim3(X3W_THREADS), 0, slk_stream(stream), act16, act_amax,
+                       dpooled, dp_amax, code, slabs, B);
+#endif
     return slk_launch_status();
 }

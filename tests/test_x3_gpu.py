@@ -131,7 +131,7 @@ def test_x3_wgrad_matches_oracle(gpu, B):
     act, p, y = _inputs(gpu, B, seed=B + 200)
     pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
     _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
-    assert ops.conv2_wgrad_nslab(B, impl="x3") == min(3 * B, 128)
+    assert ops.conv2_wgrad_nslab(B, impl="x3") == min(6 * B, 256)
     sx = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, impl="x3")).cpu().numpy()
     sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw)).cpu().numpy()
     codes = cw.cpu().numpy().astype(np.int64)
@@ -198,9 +198,11 @@ def test_trainer_conv_presets_match_fixture(gpu, conv):
 
 @pytest.mark.parametrize("B", [1, 7, 300])
 def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
-    """The forward's split input images (act16) fed to the wgrad by LDS-DMA give the same slabs bit for
-    bit as the wgrad that loads and splits act itself (same per-sample scales, same f16 values); the
-    forward in that mode is the plain x3 forward bit for bit and meets the oracle bar."""
+    """The forward's split input images (act16) fed to the wgrad by LDS-DMA give the weight gradient of
+    the wgrad that loads and splits act itself (same per-sample scales, same f16 values; since round 5 the
+    images kernel owns both co halves per workgroup over 4-row units, so the two differ only in summation
+    order: 2e-6 of max |ref|); the forward in that mode is the plain x3 forward bit for bit and meets the
+    oracle bar."""
     from oracle.split_step import conv3x3, relu, tie_discrepancies
     from splitcnn import ops
     act, p, y = _inputs(gpu, B, seed=B + 300)
@@ -210,7 +212,9 @@ def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
     _, _, _, dp = ops.fc_xent(ps, p["W3"], p["b3"], y, 1.0 / B)
     s1 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am)
     s2 = ops.conv2_wgrad_slabs(act, dp, cs, impl="x3", act_amax=am, act16=a16)
-    assert torch.equal(s1, s2)
+    assert s1.shape == s2.shape == (min(6 * B, 256), ops.CONV2_SLAB)
+    g1, g2 = (ops.reduce_slabs(s).double().cpu().numpy() for s in (s1, s2))
+    assert rel_err(g2, g1) <= 2e-6
     px, cx = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=am)
     assert torch.equal(px, ps) and torch.equal(cx, cs)
     r = relu(conv3x3(act.double().cpu().numpy(), p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
@@ -253,7 +257,11 @@ def test_conv1_x3_images_and_forward_from_images_bitwise(gpu, B):
     _, _, _, dp = ops.fc_xent(p0, W3, b3, y, 1.0 / B)
     s0 = ops.conv2_wgrad_slabs(act0, dp, c0, impl="x3", act_amax=am0)
     s1 = ops.conv2_wgrad_slabs(None, dp, c0, impl="x3", act_amax=am2, act16=i2)
-    assert torch.equal(s0, s1)
+    s1b = ops.conv2_wgrad_slabs(None, dp, c0, impl="x3", act_amax=am0, act16=i0)
+    assert torch.equal(s1, s1b)   # the same images -> the same slabs, bit for bit
+    # the f32-act kernel sums in another order (test_x3_wgrad_from_forward_images_bitwise)
+    g0, g1 = (ops.reduce_slabs(s).double().cpu().numpy() for s in (s0, s1))
+    assert rel_err(g1, g0) <= 2e-6
 
 
 def test_trainer_client_images_bitwise(gpu):

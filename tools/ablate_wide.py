@@ -59,6 +59,7 @@ hdcut = torch.empty_like(cut)
 
 libs = []
 a1bits = torch.empty(B, 1024, dtype=torch.int64, device=dev)
+out_bits = torch.empty_like(a1bits)
 for path in args.libs:
     L = ctypes.CDLL(path)
     L._bits = hasattr(L, "slk_wide_relu_bits")
@@ -82,7 +83,7 @@ herr = torch.zeros(1, dtype=torch.int32, device=dev)
 def calls(L):
     return {
         # round 5 ABI: conv1 also writes the ReLU words, conv2's dgrad reads them instead of a1
-        "conv1_fwd": (lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), p(a1bits), B, P(s))) if L._bits
+        "conv1_fwd": (lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), p(out_bits), B, P(s))) if L._bits
         else (lambda: L.slk_wide_conv1_fwd(p(x), p(w1b), p(b1), p(out_a1), B, P(s))),
         "conv2_fwd": lambda: L.slk_wide_conv2_fwd(p(a1), p(w2f), p(b2), p(out_p2), p(out_c2), B, P(s)),
         "conv3_fwd": lambda: L.slk_wide_conv3_fwd(p(p2), p(w3f), p(b3), p(out_cut), p(out_c3), B, P(s)),

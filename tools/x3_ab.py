@@ -155,6 +155,7 @@ def main():
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
             cases[f"wgrad {tag}"] = (lambda L=L, sl=sl, a16=a16: L.slk_conv2_wgrad_x3s(p(a16), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
+            outs[f"wgrad {tag}"] = sl
     times = {k: [] for k in cases}
     for _ in range(3):
         for f in cases.values():
@@ -183,7 +184,7 @@ def main():
             first[op] = t
             continue
         r = first[op]
-        red = (lambda z: z.sum(0)) if op in ("dgc1", "fcw") else (lambda z: z)
+        red = (lambda z: z.sum(0)) if op in ("dgc1", "fcw", "wgrad") else (lambda z: z)
         a, b_ = red(t.double()), red(r.double())
         print(f"check {k:18s} max|diff|/max|ref| {((a - b_).abs().max() / b_.abs().max()).item():.3e}", flush=True)
 
