@@ -38,7 +38,7 @@ class UServerStage:
         self.lr = lr
         self.params, self.grads = _flatten_params([self.conv2.weight, self.conv2.bias], self.device)
         self._buf = _Buffers()
-        self._act = self._code = None
+        self._act = self._code = self._act16 = None
 
     def _b(self, name, shape, dtype=torch.float32):
         return self._buf.get(name, shape, dtype, self.device)
@@ -49,12 +49,15 @@ class UServerStage:
         amax = None
         if "x3" in (self.impl_fwd, self.impl_wgrad):
             amax = ops.row_amax(act, out=self._b("act_amax", (B,)))
+        # x3 forward + x3 wgrad: the forward hands its split input images to the wgrad (as ServerStage)
+        act16 = (self._b("act16", (ops.conv2_act16_bytes(B),), torch.uint8)
+                 if (self.impl_fwd, self.impl_wgrad) == ("x3", "x3") else None)
         with TIMER("conv2_fwd_pool"):
             pooled, code = ops.conv2_fwd_pool(act, W2, b2,
                                               pooled=pooled if pooled is not None else self._b("pooled", (B, 64, 12, 12)),
                                               code=self._b("code", (B, 64, 12, 12), torch.uint8),
-                                              impl=self.impl_fwd, act_amax=amax)
-        self._act, self._code, self._amax = act, code, amax
+                                              impl=self.impl_fwd, act_amax=amax, act16=act16)
+        self._act, self._code, self._amax, self._act16 = act, code, amax, act16
         return pooled
 
     def backward_step(self, dpooled: torch.Tensor, cut_grad: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -71,7 +74,7 @@ class UServerStage:
         with TIMER("conv2_wgrad"):
             s2 = ops.conv2_wgrad_slabs(act, dpooled, code,
                                        slabs=self._b("s2", (ops.conv2_wgrad_nslab(B, impl=self.impl_wgrad), ops.CONV2_SLAB)),
-                                       impl=self.impl_wgrad, act_amax=self._amax, dp_amax=dpa)
+                                       impl=self.impl_wgrad, act_amax=self._amax, dp_amax=dpa, act16=self._act16)
         with TIMER("sgd_server"):
             ops.sgd_from_slabs(self.params, self.grads, s2, self.lr)
         return cut_grad
