@@ -25,7 +25,7 @@ __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restri
                                                              float* __restrict__ act,
                                                              float* __restrict__ act_amax) {
     __shared__ float xs[IN_HW * IN_HW];
-    __shared__ float amx[C1F4_T / 64];
+    __shared__ float amx[8];
     __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -35,11 +35,15 @@ __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restri
     for (int i = tid; i < C1 * 9; i += C1F4_T) ws[(i / 9) * 10 + i % 9] = W1[i];
     if (tid < C1) ws[tid * 10 + 9] = b1[tid];
     __syncthreads();
-    // act_amax (optional): the sample's max act, for the x3 conv2 kernels' per-sample scales; without
-    // it the idle threads leave here
+    // act_amax (optional): the x3 conv2 kernels' per-sample scale value of the cut — the bound of its max
+    // from max|x| (conv1_cut_bound, slk_common.h), as slk_conv1_fwd_x3 emits it; without it the idle
+    // threads leave here
     const bool active = tid < C1F4_G;
-    if (!active && !act_amax) return;
-    float am = 0.f;
+    if (act_amax) {
+        const float bnd = conv1_cut_bound(xs, W1, b1, amx);
+        if (tid == 0) act_amax[b] = bnd;
+    }
+    if (!active) return;
     if (active) {
         float xv[4][9];
 #pragma unroll
@@ -67,15 +71,7 @@ __global__ __launch_bounds__(C1F4_T) void conv1_fwd_kernel(const float* __restri
                 o[u] = s > 0.f ? s : 0.f;
             }
             out[c * C1F4_G] = make_float4(o[0], o[1], o[2], o[3]);
-            am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
         }
-    }
-    if (act_amax) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) am = fmaxf(am, __shfl_xor(am, off, 64));
-        if ((tid & 63) == 0) amx[tid >> 6] = am;
-        __syncthreads();
-        if (tid == 0) act_amax[b] = fmaxf(fmaxf(amx[0], amx[1]), amx[2]);
     }
 }
 

@@ -76,6 +76,40 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// The x3 scale value of the cut a = relu(conv1(x) + b1) of one sample, computed by the client's conv1
+// kernels (round 5): an upper bound of max a from the image's max |x| alone,
+//     bound = max_c fma(sum_k |W1[c][k]| (taps in order), max|x|, max(b1[c], 0)),
+// the same float expression in every kernel that emits it, so their act_amax outputs agree bit for bit.
+// Only the scale's power of two is derived from it (x3_exp: the value lands in [2^13, 2^14)), and the cut's
+// max sits at most a small factor below the bound (2 bits of f16 headroom remain above 2^14 either way),
+// so the image writer needs no first pass over its own outputs. Block-wide: every thread calls it after xs
+// (the 28 x 28 image in LDS) is complete; red holds >= 8 floats of scratch; returns the bound to all.
+__device__ __forceinline__ float conv1_cut_bound(const float* xs, const float* __restrict__ W1,
+                                                 const float* __restrict__ b1, float* red) {
+    const int tid = threadIdx.x, nw = (blockDim.x + 63) >> 6;
+    float m = 0.f;
+    for (int i = tid; i < slk::IN_HW * slk::IN_HW; i += blockDim.x) m = fmaxf(m, fabsf(xs[i]));
+    m = wave_max(m);
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    float xmax = red[0];
+    for (int w = 1; w < nw; ++w) xmax = fmaxf(xmax, red[w]);
+    float bc = 0.f;
+    if (tid < 64) {
+        if (tid < slk::C1) {
+            float ws = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) ws += fabsf(W1[tid * 9 + k]);
+            bc = fmaf(ws, xmax, fmaxf(b1[tid], 0.f));
+        }
+        bc = wave_max(bc);
+    }
+    __syncthreads();  // every wave has read red[]
+    if (tid == 0) red[0] = bc;
+    __syncthreads();
+    return red[0];
+}
+
 // ---------------------------------------------------------------------------- LDS-DMA as inline asm
 // global_load_lds issued through asm: hipcc then neither counts it nor inserts its own vmcnt(0) in
 // front of LDS reads and writes it cannot prove disjoint from a DMA in flight (it cannot tell a

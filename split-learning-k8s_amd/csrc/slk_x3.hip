@@ -1519,16 +1519,23 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
 // sample [4 channel groups cg][169 threads t] u32, bit 4 (c & 7) + u of (cg = c >> 3, t) = (act[c][4t + u]
 // > 0) — pass 1's thread t packs its own 4 pixels of 8 channels into one word (act >= 0, so its bit
 // pattern is nonzero iff act > 0: min(bits, 1) is the mask bit) and writes 4 coalesced words.
-constexpr int C1X_T = 192;
-constexpr int C1X_G = A_PIX / 4;  // 169 active threads
+constexpr int C1X_T = 256;
+constexpr int C1X_G = A_PIX / 4;  // 169 pixel quads
 static_assert(RB_SAMPLE == 4 * C1X_G, "bit map layout");
+// Round 5: ONE pass. The per-sample scale comes from conv1_cut_bound (max |x| and the weights: no pass
+// over the outputs first; act_amax = that bound), so each (pixel, 8-channel chunk) item is computed once:
+// conv1 (taps in order from 0, + bias — the FMA order of slk_client.hip's conv1_fwd_kernel), split, one
+// 16-B store per plane (lanes on consecutive items: 1 KiB contiguous per store instruction), the optional
+// f32 act (the 8 channel planes' words of the pixel), and the ReLU bit map: lane (pixel 4 t + u, chunk cg)
+// spreads its 8 bits to 4 cc + u and the four u lanes of a 16-lane row OR them with two swizzles (items
+// start at pixel quads: 256 threads per pass, 16 items per row); 2,704 items over 256 threads.
 template <bool BITS, bool ACT>
-__global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
+__global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __restrict__ x, const float* __restrict__ W1,
                                                              const float* __restrict__ b1, float* __restrict__ act,
                                                              float* __restrict__ act_amax, uint16_t* __restrict__ act16,
                                                              uint32_t* __restrict__ relu_bits) {
     __shared__ float xs[IN_HW * IN_HW];
-    __shared__ float amx[C1X_T / 64];
+    __shared__ float red[8];
     __shared__ float ws[C1 * 10];  // [c][9 taps | bias]
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1538,58 +1545,11 @@ __global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __r
     for (int i = tid; i < C1 * 9; i += C1X_T) ws[(i / 9) * 10 + i % 9] = W1[i];
     if (tid < C1) ws[tid * 10 + 9] = b1[tid];
     __syncthreads();
-    const bool active = tid < C1X_G;
-    float xv[4][9];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int p = active ? 4 * tid + u : 0;
-        const int y = p / A_HW, xx = p - (p / A_HW) * A_HW;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) xv[u][k] = xs[(y + k / 3) * IN_HW + xx + k % 3];
-    }
-    float am = 0.f;
-    if (active) {
-        float4* out = ACT ? reinterpret_cast<float4*>(act + (size_t)b * A_SAMPLE) + tid : nullptr;
-#pragma unroll
-        for (int cg = 0; cg < 4; ++cg) {
-            uint32_t bw = 0;
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) {
-                const int c = 8 * cg + cc;
-                // the channel's weights are wave-uniform: scalar loads issued ahead, no LDS round trip
-                // (and no wait on one) per channel
-                float wk[10];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) wk[k] = W1[c * 9 + k];
-                wk[9] = b1[c];
-                float o[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    float sum = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) sum = fmaf(xv[u][k], wk[k], sum);
-                    sum += wk[9];
-                    o[u] = sum > 0.f ? sum : 0.f;
-                }
-                if constexpr (ACT) out[c * C1X_G] = make_float4(o[0], o[1], o[2], o[3]);
-                am = fmaxf(am, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
-                if constexpr (BITS) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) bw |= min(__float_as_uint(o[u]), 1u) << (4 * cc + u);
-                }
-            }
-            if constexpr (BITS) relu_bits[(size_t)b * RB_SAMPLE + cg * C1X_G + tid] = bw;
-        }
-    }
-    am = wave_max(am);
-    if ((tid & 63) == 0) amx[tid >> 6] = am;
-    __syncthreads();
-    am = fmaxf(fmaxf(amx[0], amx[1]), amx[2]);
+    const float am = conv1_cut_bound(xs, W1, b1, red);
     if (tid == 0) act_amax[b] = am;
     const float sc = ldexpf(1.f, x3_exp(am));
-    // pass 2: item = (pixel p, 8-channel chunk c8), lanes on consecutive items, so one store
-    // instruction covers 16 whole 64-B pixel records (1 KiB contiguous); c8 = tid & 3 for every item of a
-    // thread (the stride 192 is a multiple of 4): its 8 channels' weights stay in registers
+    // c8 = tid & 3 for every item of a thread (the stride 256 is a multiple of 4): its 8 channels' weights
+    // stay in registers
     const int c8 = tid & 3;
     float wr[8][10];
 #pragma unroll
@@ -1597,6 +1557,7 @@ __global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __r
 #pragma unroll
         for (int k = 0; k < 10; ++k) wr[j][k] = ws[(8 * c8 + j) * 10 + k];
     char* img = reinterpret_cast<char*>(act16) + (size_t)b * X3S_SAMPLE;
+    float* actb = ACT ? act + (size_t)b * A_SAMPLE : nullptr;
 #pragma unroll 2
     for (int i = tid; i < A_PIX * 4; i += C1X_T) {
         const int p = i >> 2;
@@ -1612,6 +1573,22 @@ __global__ __launch_bounds__(C1X_T, 1) void conv1_fwd_x3_kernel(const float* __r
             for (int k = 0; k < 9; ++k) sum = fmaf(xw[k], wr[j][k], sum);
             sum += wr[j][9];
             v[j] = sum > 0.f ? sum : 0.f;
+        }
+        if constexpr (ACT) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) actb[(8 * c8 + j) * A_PIX + p] = v[j];
+        }
+        if constexpr (BITS) {
+            // bit 4 cc + u of word (cg = c8, t = p >> 2) = v[cc] > 0 (v >= +0: nonzero bits iff > 0)
+            const int u = p & 3;
+            uint32_t w = 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w |= min(__float_as_uint(v[j]), 1u) << (4 * j);
+            w <<= u;
+            // OR over the row's lanes of the same chunk: lane ^ 4, lane ^ 8 (ds_swizzle bit mode, xor)
+            w |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)w, (4 << 10) | 0x1F);
+            w |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)w, (8 << 10) | 0x1F);
+            if (u == 0) relu_bits[(size_t)b * RB_SAMPLE + c8 * C1X_G + (p >> 2)] = w;
         }
         f16x8 hh, ll;
         x3_split8(v, sc, hh, ll);

@@ -156,7 +156,9 @@ def test_x3_wgrad_deterministic(gpu):
 
 
 def test_fused_amax_outputs(gpu):
-    """conv1_fwd's act_amax and fc_xent's dp_amax equal row_amax of their outputs (exact: a max)."""
+    """conv1_fwd's act_amax is the cut's x3 scale value, the bound max_c (sum_k |W1[c,k]| max|x| + b1[c]+)
+    (round 5: conv1_cut_bound, the same as slk_conv1_fwd_x3 emits), never below the cut's max; fc_xent's
+    dp_amax equals row_amax of dpooled (exact: a max)."""
     from splitcnn import ops
     from splitcnn.data import SyntheticMNIST, init_models
     B = 37
@@ -167,7 +169,15 @@ def test_fused_amax_outputs(gpu):
     am = torch.empty(B, device=gpu)
     act = ops.conv1_fwd(x, W1, b1, act_amax=am)
     assert torch.equal(act, ops.conv1_fwd(x, W1, b1))
-    assert torch.equal(am, ops.row_amax(act))
+    true_max = ops.row_amax(act)
+    assert bool((am >= true_max).all())
+    xm = x.reshape(B, -1).abs().amax(dim=1).double().cpu().numpy()
+    w = W1.reshape(32, 9).abs().double().sum(dim=1).cpu().numpy()
+    bound = (w[None, :] * xm[:, None] + np.maximum(b1.double().cpu().numpy(), 0.0)[None, :]).max(axis=1)
+    assert rel_err(am.cpu().numpy(), bound) <= 1e-6
+    am_x3 = torch.empty(B, device=gpu)
+    ops.conv1_fwd_x3(x, W1, b1, am_x3, torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu))
+    assert torch.equal(am_x3, am)   # the two client kernels emit the same value
     W2, b2 = b.conv2.weight.detach().to(gpu), b.conv2.bias.detach().to(gpu)
     W3, b3 = b.fc1.weight.detach().to(gpu), b.fc1.bias.detach().to(gpu)
     pooled, code = ops.conv2_fwd_pool(act, W2, b2)
