@@ -63,8 +63,10 @@ const char* slk_build_id(void);
  * Replaces ModelPartA.forward (src/model_def.py:11-12) as called at src/client_part.py:114. */
 int slk_conv1_fwd(const float* x, const float* W1, const float* b1, float* act, int B, void* stream);
 
-/* slk_conv1_fwd that also writes act_amax[b] = max(act[b]) (>= 0): the per-sample scale of the x3 conv2
- * kernels, fused so the 354 MB cut is not re-read at B = 4096. */
+/* slk_conv1_fwd that also writes act_amax[b], the per-sample scale value of the x3 conv2 kernels: since
+ * round 5 the bound max_c (sum_k |W1[c][k]| * max|x[b]| + max(b1[c], 0)) >= max(act[b]) (one float expression,
+ * slk_common.h conv1_cut_bound; the same value slk_conv1_fwd_x3 emits), so the 354 MB cut is never re-read
+ * and no writer needs a pass over its outputs before splitting them. */
 int slk_conv1_fwd_amax(const float* x, const float* W1, const float* b1, float* act, float* act_amax, int B,
                        void* stream);
 
@@ -186,8 +188,9 @@ int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const floa
 int64_t slk_conv2_act16_bytes(int B);
 
 /* The client's conv1 + ReLU (replaces slk_conv1_fwd_amax inside a fused step, src/client_part.py:114)
- * writing the x3 server operand directly: act_amax and the act16 images (bit-identical to those
- * slk_conv2_fwd_pool_x3s writes), plus the f32 act when act != NULL. The server forward then reads the
+ * writing the x3 server operand directly: act_amax (the bound of slk_conv1_fwd_amax) and the act16 images
+ * (bit-identical to those slk_conv2_fwd_pool_x3s writes from the f32 act with that act_amax), plus the f32
+ * act when act != NULL — one pass per (pixel, 8-channel) item. The server forward then reads the
  * images (slk_conv2_fwd_pool_x3i: same pooled / code as slk_conv2_fwd_pool_x3 on the f32 act, bitwise)
  * and so does the wgrad (slk_conv2_wgrad_x3s). relu_bits (optional, slk_relu_bits_bytes(B) bytes, 16-byte
  * aligned): the ReLU mask act > 0 of every cut element, 1 bit each (per sample [4 channel groups cg][169]
