@@ -74,7 +74,19 @@ __global__ __launch_bounds__(256) void row_amax_kernel(const float* __restrict__
     float m = 0.f;
     if ((n & 3) == 0 && ((reinterpret_cast<size_t>(x) & 15) == 0)) {
         const float4* r4 = reinterpret_cast<const float4*>(row);
-        for (int i = threadIdx.x; i < n / 4; i += 256) {
+        const int n4 = n / 4;
+        int i = threadIdx.x;
+        // 8 independent float4 loads in flight per thread (one at a time left the kernel latency-bound
+        // at ~3.9 TB/s over a 354 MB cut); max is order-independent, so the result is unchanged
+        for (; i + 7 * 256 < n4; i += 8 * 256) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = r4[i + 256 * u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+        }
+        for (; i < n4; i += 256) {
             const float4 v = r4[i];
             m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
@@ -514,6 +526,27 @@ constexpr int X3D_MPW = 4;                         // M tiles per wave and part 
 constexpr int X3D_GRID = 256;
 constexpr int X3D_ITEMS_MAX = 7 * P_HW * 8;        // (window, 4-co group) items of the largest part (672)
 static_assert(2 * X3D_IMG <= 163840, "LDS");
+#ifndef SLK_X3D_TRACE
+#define SLK_X3D_TRACE 0
+#endif
+#ifndef SLK_X3D_PROBE
+#define SLK_X3D_PROBE 0
+#endif
+#if SLK_X3D_TRACE
+// profiling probe: per (workgroup, wave, unit) shader-clock stamps of the dgrad's phases (lane 0, vector stores)
+__device__ unsigned long long g_x3d_trace[256 * 8 * 128 * 8];
+#define X3D_TS(u, slot)                                                                                     \
+    do {                                                                                                   \
+        unsigned long long _t;                                                                             \
+        asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                          \
+        if (lane == 0 && (u) < 128) g_x3d_trace[(((size_t)blockIdx.x * 8 + wave) * 128 + (u)) * 8 + (slot)] = _t; \
+    } while (0)
+extern "C" int slk_x3d_trace_read(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_x3d_trace), sizeof(g_x3d_trace)) == hipSuccess ? 0 : 1;
+}
+#else
+#define X3D_TS(u, slot)
+#endif
 
 __device__ __forceinline__ int x3d_t0(int pt) { return pt == 0 ? 0 : (pt == 1 ? 15 : 29); }
 __device__ __forceinline__ int x3d_ybase(int pt) { return pt == 0 ? -2 : (pt == 1 ? 6 : 14); }
@@ -565,6 +598,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const int nt = wave & 1, g = wave >> 1;
     const int n16 = lane & 15, kc = lane >> 4;
     const int G = gridDim.x;
+    X3D_TS(0, 7);
 
     // zero both images once: the leading pixels and columns 24-25 are never written again
     for (int o = tid * 16; o < 2 * X3D_IMG; o += X3D_THREADS * 16) *reinterpret_cast<uint4*>(smem + o) = make_uint4(0, 0, 0, 0);
@@ -599,6 +633,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             }
     }
 
+    X3D_TS(1, 7);
     // expansion items of a unit: i = tid + 512 r -> 4-co group c4 = i & 7, window wi = i >> 3 (row-major
     // over the part's image window rows); rows outside 0..11 expand to zeros
     constexpr int NR = 2, SSTR = X3D_THREADS;
@@ -622,7 +657,12 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 dcb[r][j] = CODE_NONE;  // routes nothing
             }
             if (i < nwr * P_HW * 8 && wr >= 0 && wr < P_HW) {
+#if SLK_X3D_PROBE
+                // timing probe (wrong data): lanes read consecutive windows of one co plane (coalesced)
+                const size_t o = (size_t)b * P_SAMPLE + (32 * h) * P_WIN + (i & 127);
+#else
                 const size_t o = (size_t)b * P_SAMPLE + (32 * h + 4 * c4) * P_WIN + wr * P_HW + wx;
+#endif
                 // code bytes stay one per register until store_dy: combining them here made the
                 // compiler wait for the loads on the spot (a full memory latency per unit)
 #pragma unroll
@@ -703,6 +743,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         load_dy(2 * pr + 1);
     }
     int k = 0, q = 0;
+    X3D_TS(2, 7);
     // C1W epilogue of one pair: client ReLU backward + conv1 wgrad (the cut gradient g is the value the
     // C1W = false store would write): for each tile and r, one f32 MFMA over k = the 4 lane groups' pixels
     // 16 t + 4 kc + r. All of the pair's x / bit-map reads are issued first; the ReLU mask is an integer
@@ -782,8 +823,10 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h, ++k) {
             // C1W: this pair's x / bits DMA (issued during the previous pair) retired before the barrier
+            X3D_TS(k, 6);
             if (C1W && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
+            X3D_TS(k, 0);
             // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue)
             if (C1W && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
@@ -806,6 +849,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
+            X3D_TS(k, 1);
             f16x8 fh[4], fl[4];
             f32x4 ct;  // cross products of the current tile (see the accumulation note above)
             constexpr int NS = 27;  // tiles 0..2 exist for every wave and part
@@ -827,10 +871,12 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
                 if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
+            X3D_TS(k, 2);
             if (!sfirst) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
+            X3D_TS(k, 3);
             if (T0 + g + 12 < T1) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) rd(3, q, fh[q], fl[q]);
@@ -849,11 +895,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     if (tap + 3 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
                 }
             }
+            X3D_TS(k, 4);
         }
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
         const float us1 = ldexpf(1.f, -x3_exp(amax_b)), us2 = ldexpf(1.f, -sw);
         if constexpr (C1W) {
             c1w_epi(T0, T1, us1, q);
+            X3D_TS(k - 1, 5);
         } else {
             float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
@@ -867,6 +915,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         }
         ++q;
     }
+    X3D_TS(127, 7);
     if constexpr (C1W) {
         // slab of this workgroup: D1 of the 4 tile-group waves of each ci tile, summed in wave order
         __syncthreads();

@@ -120,6 +120,7 @@ def main():
             cases[f"fc1 {tag}"] = (lambda L=L, lg=lg3: L.slk_fc_fwd(p(pooled), p(W3), p(b3), p(lg), B, st))
             cases[f"fc4 {tag}"] = (lambda L=L, dl=dl3, dpo=dpo3: L.slk_fc_dgrad(p(dl), p(W3), p(dpo), B, st))
             outs[f"fc {tag}3"] = dpo3
+            outs[f"fcl {tag}"] = lg3
         if "fcord" in args.ops.split(","):
             # launch order of the server head + fc weight gradient: A = the step's (fused head, then
             # fc_wgrad: pooled evicted by the head's own 151 MB dpooled write); B = logits, CE, fc_wgrad
