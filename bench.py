@@ -188,7 +188,7 @@ ALGO_BYTES = {"conv2_fwd_pool": 132_608, "conv2_dgrad": 46_080, "conv2_wgrad": 1
 ROCPROF_SYMBOL = {("conv2_dgrad", "x3_fused"): "conv2_dgrad_x3_kernel<true>",
                   ("conv2_dgrad", "x3"): "conv2_dgrad_x3_kernel<false>",
                   ("conv2_fwd_pool", "x3_images"): "conv2_fwd_pool_x3_kernel<true>",
-                  ("conv2_wgrad", "x3_images"): "conv2_wgrad_x3_kernel<true>"}
+                  ("conv2_wgrad", "x3_images"): "conv2_wgrad_x3q_kernel"}
 
 
 def rocprof_avg(symbol, pattern="kernel_stats_k2.csv"):
