@@ -410,7 +410,7 @@ def run_hub_loopback(args, nc=7):
     cl = ClientStage(a, device=dev)
     cl.emit_amax = True
     n = b * 32 * 26 * 26
-    acts = hub._inputs(G, dev)
+    acts = hub._inputs(G, dev, codec)
     labels = hub._buf("labels", (G,), torch.int64, dev)
     amx = hub._buf("amax", (G,), torch.float32, dev)
     hub._buf("cuts", (G, 32, 26, 26), torch.float32, dev)
@@ -422,12 +422,14 @@ def run_hub_loopback(args, nc=7):
             x, y = data.batch(b)
             if images:
                 cl.forward_images(x.to(dev), acts[sl.start * sd.IMG_BYTES:sl.stop * sd.IMG_BYTES], amx[sl])
+            elif codec is not None:   # the client's f32 cut, encoded into the server's receive buffers
+                ca = cl.forward(x.to(dev))
+                amx[sl].copy_(cl._act_amax)
+                codec.encode(ca, codec.buffers(("s", ci, k), n, dev))
             else:
                 cl.forward(x.to(dev), out=acts[sl])
                 amx[sl].copy_(cl._act_amax)
             labels[sl].copy_(y.to(dev))
-            if codec is not None:
-                codec.encode(acts[sl], codec.buffers(("s", ci, k), n, dev))
     return hub, cl, codec, data, nc
 
 
@@ -449,8 +451,10 @@ def hub_loopback_rate(args, ref_value, conv1_ms):
     dt = timed(step, K, 2, dev)
     rate = K * nc * B / dt
     fused_minus_conv1 = B / (B / ref_value - conv1_ms * 1e-3) if ref_value and conv1_ms else None
+    fused = hub._fused(codec)
     return {"workload": f"K4 hub server compute, {nc} clients x {B} samples in {m} chunks of {nc * b} "
                         f"(codec unpack/pack {'on' if codec is not None else 'off'}"
+                        f"{' (fused: unpack into the x3 images, pack in the dgrad epilogue)' if fused else ''}"
                         f"{', x3 split images in' if hub.images else ''}, HIP graph per chunk), "
                         "inputs already in the receive buffers: the 1-GPU bound of BASELINE config 4",
             "samples_per_s": round(rate, 1), "ms_per_step": round(dt / K * 1e3, 3), "global_batch": nc * B,

@@ -279,6 +279,20 @@ int slk_cut_encode(const float* x, int64_t n, uint32_t* mask, int* counts, int* 
 int slk_cut_offsets(const uint32_t* mask, int64_t n, int* counts, int* offsets, int* total, void* stream);
 int slk_cut_pack(const float* x, int64_t n, const uint32_t* mask, const int* offsets, float* vals, void* stream);
 int slk_cut_unpack(const float* vals, int64_t n, const uint32_t* mask, const int* offsets, float* x, void* stream);
+/* Fused consumers of a received micro-batch (the K3 / K4 server; each replaces an unpack or a pack pass over
+ * the dense f32 cut, src/server_part.py:39-45 and :57-58):
+ *   ranks      : ranks[w] (ceil(n/32) ints) = the vals index of mask word w's first set element
+ *                (offsets of the block + the set bits of its earlier words), from slk_cut_offsets' offsets;
+ *   unpack_x3  : the x3 input images of B samples (slk_conv2_act16_bytes(B) bytes, each sample at the scale
+ *                of act_amax[b]) straight from mask + vals + ranks: the images slk_conv1_fwd_x3 would have
+ *                written from the same cut (bit for bit), no dense f32 cut;
+ *   dgrad_pack : slk_conv2_dgrad_x3 writing the cut gradient packed (values at the mask's set positions, at
+ *                their ranks) — what slk_cut_pack would extract from its dense output. */
+int slk_cut_ranks(const uint32_t* mask, int64_t n, const int* offsets, int* ranks, void* stream);
+int slk_cut_unpack_x3(const float* vals, const uint32_t* mask, const int* ranks, const float* act_amax, int B,
+                      uint16_t* act16, void* stream);
+int slk_conv2_dgrad_x3_pack(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                            const uint32_t* mask, const int* ranks, float* vals, int B, void* stream);
 
 /* ================================================================ widened split CNN (BASELINE config 5)
  * The reference has no such model: these entry points run the north star's

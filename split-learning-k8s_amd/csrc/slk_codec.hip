@@ -94,6 +94,25 @@ __global__ __launch_bounds__(256) void cut_count_kernel(const uint32_t* __restri
     if (lane == 0) counts[b] = c;
 }
 
+// word ranks (the fused consumers, slk_cut_unpack_x3 / slk_conv2_dgrad_x3_pack): ranks[w] = the vals index of
+// the first set element of mask word w = offsets[block] + the set bits of the block's earlier words. One
+// wave per block, lane = mask word: an element's rank is then ranks[e / 32] + popc(mask[e / 32] below e % 32)
+__global__ __launch_bounds__(256) void cut_ranks_kernel(const uint32_t* __restrict__ mask, long n, int nblk,
+                                                        const int* __restrict__ offsets, int* __restrict__ ranks) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= nblk) return;  // wave-uniform
+    const long nw = (n + 31) / 32;
+    const long w = (long)b * CB_WORDS + lane;
+    const int c = w < nw ? __popc(mask[w]) : 0;
+    int inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (w < nw) ranks[w] = offsets[b] + inc - c;
+}
+
 // exclusive scan of the block counts (one workgroup) -> offsets; total -> total[0]. Up to CS_LDS counts
 // are staged in LDS by coalesced loads (each thread then scans a contiguous range from LDS).
 constexpr int CS_LDS = 12288;
@@ -210,6 +229,15 @@ extern "C" int slk_cut_offsets(const uint32_t* mask, int64_t n, int* counts, int
     hipStream_t st = slk_stream(stream);
     hipLaunchKernelGGL(cut_count_kernel, dim3((nb + 3) / 4), dim3(256), 0, st, mask, n, nb, counts);
     hipLaunchKernelGGL(cut_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nb, offsets, total);
+    return slk_launch_status();
+}
+
+extern "C" int slk_cut_ranks(const uint32_t* mask, int64_t n, const int* offsets, int* ranks, void* stream) {
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX);
+    if (n == 0) return 0;
+    SLK_CHECK_ARG(mask && offsets && ranks);
+    const int nb = cut_blocks(n);
+    hipLaunchKernelGGL(cut_ranks_kernel, dim3((nb + 3) / 4), dim3(256), 0, slk_stream(stream), mask, n, nb, offsets, ranks);
     return slk_launch_status();
 }
 

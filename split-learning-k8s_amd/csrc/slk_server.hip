@@ -587,9 +587,12 @@ __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
 #pragma unroll
         for (int c = 0; c < FCH_NS; ++c) issue(c);
         // A fragment: lane (sample s16, group kg) holds features 16 blk + 4 kg + i; B: lane (class, kg) the
-        // same features of W3 row min(class, 9) (classes 10-15: duplicates, never stored). Accumulator
+        // same features of W3 row `nrow` (classes 10-15: duplicates, never stored). Accumulator
         // (feature / 16) % 4 for every chunk size, so the sum order (and the result) does not depend on FCH_CK.
-        const int s16 = lane & 15, kg = lane >> 4, nrow = min(s16, NCLS - 1);
+        // classes 10-15 (never stored) read W3 rows 2-7: row 9 for all of them put row 9 (72 dwords x 9 = 8 mod
+        // 64) on row 1's banks in every ds_read_b128 lane group (0.59 M conflict cycles per launch); with rows
+        // 2-7 each 16-lane group's 16 reads hit 16 distinct 4-bank slots (any valid row gives the same classes 0-9)
+        const int s16 = lane & 15, kg = lane >> 4, nrow = s16 < NCLS ? s16 : s16 - 8;
         f32x4 acc[4];
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {

@@ -1228,8 +1228,13 @@ extern "C" int slk_wide_conv3_wgrad(const uint16_t* dcut, const uint8_t* code3, 
 // image [3][34][34] is staged in LDS as f32 (14 elements per thread: offsets computed once, all loads
 // issued back to back); each lane gathers its 8 im2col values of a fragment from it and converts them
 // to bf16. HBM-bound: the forward writes a1 (128 KB/sample), the weight gradient reads da1m.
-constexpr int C1P = 34;                               // padded image pitch
-constexpr int C1S = (3 * C1P * C1P + 255) / 256;      // 14 staged elements per thread
+// LDS pitches of the staged image (bank model over both kernels' im2col reads, ds_read_b32 = dword mod 32 over
+// 32-lane halves): rows of 35 and planes of 1,233 floats leave the weight gradient's B-fragment gathers 4 and
+// the forward's 16 extra cycles per fragment where the dense [3][34][34] image had 46 and 135 (8.6 M and
+// 2.9 M conflict cycles per launch)
+constexpr int C1P = 35;                               // row pitch (32 + 2 halo + 1 pad)
+constexpr int C1PS = 1233;                            // plane pitch (35 x 35 + 8)
+constexpr int C1S = (3 * C1P * C1P + 255) / 256;      // 15 staged elements per thread
 
 __device__ __forceinline__ void stage_offsets(int (&off)[C1S]) {
 #pragma unroll
@@ -1248,13 +1253,14 @@ __device__ __forceinline__ void stage_store(float* xs, const float (&v)[C1S]) {
 #pragma unroll
     for (int k = 0; k < C1S; ++k) {
         const int e = threadIdx.x + 256 * k;
-        if (e < 3 * C1P * C1P) xs[e] = v[k];
+        const int ci = e / (C1P * C1P);
+        if (e < 3 * C1P * C1P) xs[e + ci * (C1PS - C1P * C1P)] = v[k];
     }
 }
-// im2col offset of K index k (ci*1156 + ky*34 + kx) inside the padded image, -1 for k >= 27
+// im2col offset of K index k (ci*C1PS + ky*C1P + kx) inside the padded image, -1 for k >= 27
 __device__ __forceinline__ int im2col_off(int k) {
     const int ci = k / 9, t = k - (k / 9) * 9;
-    return k < 27 ? ci * C1P * C1P + (t / 3) * C1P + t % 3 : -1;
+    return k < 27 ? ci * C1PS + (t / 3) * C1P + t % 3 : -1;
 }
 
 // Forward: a1[co][px] = relu(sum_k W1b[co][k] * bf16(x)[k][px] + b1[co]); A = W1b (4 fragments in
@@ -1267,7 +1273,7 @@ __device__ __forceinline__ int im2col_off(int k) {
 __global__ __launch_bounds__(256) void wide_conv1_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ w1b,
                                                              const float* __restrict__ b1, uint16_t* __restrict__ a1, int B,
                                                              uint2* __restrict__ a1bits = nullptr) {
-    __shared__ float xs[3 * C1P * C1P];
+    __shared__ float xs[3 * C1PS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int q = lane >> 4, col = lane & 15;
     bf16x8 av[4];
@@ -1350,7 +1356,7 @@ constexpr int C1W_BUF = 8 * C1W_NPXP * 16;                     // 16,896 B
 
 __global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __restrict__ x, const uint16_t* __restrict__ da1m,
                                                                float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(1024))) char smem[2 * C1W_BUF + 3 * C1P * C1P * 4];
+    __shared__ __attribute__((aligned(1024))) char smem[2 * C1W_BUF + 3 * C1PS * 4];
     float* xs = reinterpret_cast<float*>(smem + 2 * C1W_BUF);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane >> 4, ig = lane & 15, a = ig >> 2, p = ig & 3, col = lane & 15;
@@ -1412,7 +1418,8 @@ __global__ __launch_bounds__(256) void wide_conv1_wgrad_kernel(const float* __re
         const int y = rb * 4 + wave;
 #pragma unroll
         for (int kf = 0; kf < 2; ++kf) {
-            const int base = y * C1P + 8 * q + (koff[kf] >= 0 ? koff[kf] : 0);
+            // k >= 27 (the bias column and padding; values replaced below) reads k = 18's address: a broadcast
+            const int base = y * C1P + 8 * q + (koff[kf] >= 0 ? koff[kf] : im2col_off(18));
             bf16x8 bv;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {

@@ -532,20 +532,30 @@ static_assert(2 * X3D_IMG <= 163840, "LDS");
 #ifndef SLK_X3D_PROBE
 #define SLK_X3D_PROBE 0
 #endif
+#ifndef SLK_X3D_XBLATE
+#define SLK_X3D_XBLATE 0
+#endif
 #if SLK_X3D_TRACE
 // profiling probe: per (workgroup, wave, unit) shader-clock stamps of the dgrad's phases (lane 0, vector stores)
 __device__ unsigned long long g_x3d_trace[256 * 8 * 128 * 8];
-#define X3D_TS(u, slot)                                                                                     \
+#define X3_TS(buf, u, slot)                                                                                 \
     do {                                                                                                   \
         unsigned long long _t;                                                                             \
         asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                          \
-        if (lane == 0 && (u) < 128) g_x3d_trace[(((size_t)blockIdx.x * 8 + wave) * 128 + (u)) * 8 + (slot)] = _t; \
+        if (lane == 0 && (u) < 128) buf[(((size_t)blockIdx.x * 8 + wave) * 128 + (u)) * 8 + (slot)] = _t;  \
     } while (0)
+#define X3D_TS(u, slot) X3_TS(g_x3d_trace, u, slot)
+#define X3Q_TS(u, slot) X3_TS(g_x3q_trace, u, slot)
+__device__ unsigned long long g_x3q_trace[256 * 8 * 128 * 8];
+extern "C" int slk_x3q_trace_read(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_x3q_trace), sizeof(g_x3q_trace)) == hipSuccess ? 0 : 1;
+}
 extern "C" int slk_x3d_trace_read(void* dst) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_x3d_trace), sizeof(g_x3d_trace)) == hipSuccess ? 0 : 1;
 }
 #else
 #define X3D_TS(u, slot)
+#define X3Q_TS(u, slot)
 #endif
 
 __device__ __forceinline__ int x3d_t0(int pt) { return pt == 0 ? 0 : (pt == 1 ? 15 : 29); }
@@ -566,11 +576,17 @@ __device__ __forceinline__ int x3d_nwr(int pt) { return pt == 2 ? 7 : 6; }  // i
 // 9 = bias -> 1.0), one 16 ci x 16 col accumulator per wave for the whole launch; each workgroup writes
 // one 320-float client slab (src/client_part.py:132 — the client's act.backward(cut_grad) without the
 // cut gradient ever reaching HBM). x and the bit map of the next pair are loaded a unit ahead into LDS.
+// PACK (C1W = false, pvals != nullptr): the cut gradient leaves in the codec's packed form (slk_codec.hip)
+// instead of dense: only the elements set in the received cut's mask, each at its rank (pranks[e / 32] +
+// the set bits of its word below it) — what slk_cut_pack would extract from the dense gradient, without
+// the 354 MB (B = 4096) dense write and re-read. Sample 0 of the launch is element 0 of the mask.
 template <bool C1W>
 __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ dpooled, const float* __restrict__ amax, const uint8_t* __restrict__ code,
     const float* __restrict__ W2, float* __restrict__ cut_grad, int B, const float* __restrict__ xin = nullptr,
-    const uint32_t* __restrict__ relu_bits = nullptr, float* __restrict__ c1slabs = nullptr) {
+    const uint32_t* __restrict__ relu_bits = nullptr, float* __restrict__ c1slabs = nullptr,
+    const uint32_t* __restrict__ pmask = nullptr, const int* __restrict__ pranks = nullptr,
+    float* __restrict__ pvals = nullptr) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
     // C1W: per pair, x (3,136 B), a second copy of x, then its ReLU bits (2,704 B), double-buffered
     // (XB_BYTES apart, a multiple of 128 B), moved by LDS-DMA; after both buffers the plane of ones (below).
@@ -657,7 +673,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 dcb[r][j] = CODE_NONE;  // routes nothing
             }
             if (i < nwr * P_HW * 8 && wr >= 0 && wr < P_HW) {
-#if SLK_X3D_PROBE
+#if SLK_X3D_PROBE == 1
                 // timing probe (wrong data): lanes read consecutive windows of one co plane (coalesced)
                 const size_t o = (size_t)b * P_SAMPLE + (32 * h) * P_WIN + (i & 127);
 #else
@@ -665,11 +681,22 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
 #endif
                 // code bytes stay one per register until store_dy: combining them here made the
                 // compiler wait for the loads on the spot (a full memory latency per unit)
+#if SLK_X3D_PROBE == 3
+                // timing probe (wrong data): one value + one code load per item
+                dv[r][0] = dpooled[o];
+                dcb[r][0] = code[o];
+#pragma unroll
+                for (int j = 1; j < 4; ++j) {
+                    dv[r][j] = dv[r][0];
+                    dcb[r][j] = dcb[r][0];
+                }
+#else
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     dv[r][j] = dpooled[o + j * P_WIN];
                     dcb[r][j] = code[o + j * P_WIN];
                 }
+#endif
             }
         }
     };
@@ -686,11 +713,17 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 uint32_t hv[2], lv[2];
 #pragma unroll
                 for (int j = 0; j < 4; j += 2) {
+#if SLK_X3D_PROBE == 2
+                    // timing probe (wrong data): no scale / split
+                    hv[j / 2] = __float_as_uint(dv[r][j]);
+                    lv[j / 2] = __float_as_uint(dv[r][j + 1]);
+#else
                     const float a = dv[r][j] * sc, c = dv[r][j + 1] * sc;
                     const _Float16 ha = (_Float16)a, hc = (_Float16)c;
                     const _Float16 la = (_Float16)(a - (float)ha), lc = (_Float16)(c - (float)hc);
                     hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
                     lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
+#endif
                 }
                 const uint32_t dcw = dcb[r][0] | (dcb[r][1] << 8) | (dcb[r][2] << 16) | (dcb[r][3] << 24);
                 const uint32_t cA = __builtin_amdgcn_perm(0u, dcw, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw, 0x03030202u);
@@ -700,8 +733,16 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     const uint32_t T = 0xFFu << (8 * pos);
                     const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
                     char* o = rec + ((pos >> 1) * A_HW + (pos & 1)) * X3D_REC;
+#if SLK_X3D_PROBE == 4
+                    // timing probe (wrong data): no routing masks
+                    (void)mA;
+                    (void)mB;
+                    *reinterpret_cast<uint2*>(o) = make_uint2(hv[0], hv[1]);
+                    *reinterpret_cast<uint2*>(o + 64) = make_uint2(lv[0], lv[1]);
+#else
                     *reinterpret_cast<uint2*>(o) = make_uint2(hv[0] & mA, hv[1] & mB);
                     *reinterpret_cast<uint2*>(o + 64) = make_uint2(lv[0] & mA, lv[1] & mB);
+#endif
                 }
             }
         }
@@ -827,8 +868,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             if (C1W && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
             X3D_TS(k, 0);
-            // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue)
-            if (C1W && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
+            // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue). The
+            // staging-first waves issue it after their staging: hipcc cannot see the asm DMA, and its vmcnt(0)
+            // for the dY registers would wait for the DMA just issued (a full memory latency per pair)
+            const bool sfirst = wave >= 4;
+            if (C1W && h == 0 && !(SLK_X3D_XBLATE && sfirst)) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
             const int unx = min(h ? 2 * (pr + 1) : 2 * pr + 1, 2 * p1 - 1);   // the unit after this one
@@ -844,10 +888,10 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused).
             // Half the waves stage before their MFMAs, half after, so the two waves of a SIMD overlap
             // one's staging with the other's MFMAs (both staging at once left the SIMD's MFMA idle).
-            const bool sfirst = wave >= 4;
             if (sfirst) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
+                if (C1W && SLK_X3D_XBLATE && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             }
             X3D_TS(k, 1);
             f16x8 fh[4], fl[4];
@@ -902,6 +946,22 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         if constexpr (C1W) {
             c1w_epi(T0, T1, us1, q);
             X3D_TS(k - 1, 5);
+        } else if (pvals != nullptr) {
+            // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4)
+            const size_t e0 = ((size_t)b * C1 + 16 * nt + n16) * A_PIX;
+#pragma unroll
+            for (int i = 0; i < X3D_MPW; ++i) {
+                const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
+                if (t < T1 && p < A_PIX) {
+                    const size_t e = e0 + p, w = e >> 5;
+                    const int bit = (int)(e & 31);
+                    const uint32_t m = pmask[w];
+                    int r = pranks[w] + __popc(m & ((1u << bit) - 1u));
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if ((m >> (bit + rr)) & 1u) pvals[r++] = x3_unscale(acc[i][rr], us1, us2);
+                }
+            }
         } else {
             float* gb = cut_grad + (size_t)b * A_SAMPLE + (16 * nt + n16) * A_PIX;
 #pragma unroll
@@ -1313,7 +1373,11 @@ constexpr int X3Q_BUF = (X3Q_DYOFF + 2 * X3Q_DYC + 1023) / 1024 * 1024;  // 45,0
 constexpr int X3Q_NKS = 256;                             // K shares (slabs): one workgroup per CU
 constexpr int X3Q_DYITEMS = 24 * 16;                     // (window, 4-co group, co half) items per unit
 constexpr int X3Q_XPIECES = X3Q_XP / 1024 + 1;           // 10 DMA pieces per input plane (the last 768 B)
-static_assert(2 * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
+#ifndef SLK_X3Q_NBUF
+#define SLK_X3Q_NBUF 2
+#endif
+constexpr int X3Q_NBUF = SLK_X3Q_NBUF;                   // buffers: the image DMA runs NBUF - 1 units ahead
+static_assert(X3Q_NBUF * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
 
 // LDS-DMA of unit uu's input image (rows 4t .. 4t + 5 of both planes of the sample's act16 image)
 __device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
@@ -1330,16 +1394,30 @@ __device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int
     }
 }
 
+// NBUF = 3: waves 6 and 7 (which route no dY) move the whole image, one plane each (10 pieces), so the
+// dY register loads of waves 0-5 and the DMA never share a wave's vmcnt: the DMA can run two units ahead
+// without the compiler's waits for the dY registers also waiting for it
+__device__ __forceinline__ void x3q_issue_img_loader(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
+    const int b = uu / 6, t = uu - (uu / 6) * 6;
+    const int pl = wave - 6;
+    const char* src = reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t * (X3Q_ROWS * A_HW * 64) + pl * X3S_PLANE;
+#pragma unroll
+    for (int pp = 0; pp < X3Q_XPIECES; ++pp)
+        if (pp < X3Q_XPIECES - 1 || lane < (X3Q_XP % 1024) / 16)
+            glds16_so(src, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3Q_XP + pp * 1024);
+}
+
 __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
     const uint16_t* __restrict__ act16, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
     const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(1024))) char smem[2 * X3Q_BUF];
+    __shared__ __attribute__((aligned(1024))) char smem[X3Q_NBUF * X3Q_BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = wave & 1, c = (wave >> 1) & 1, tg = wave >> 2;
     const int ks = blockIdx.x, nks = gridDim.x;
     const int U = 6 * B;
     float* red = reinterpret_cast<float*>(smem);  // prologue scratch (buffer 0, before any staging)
+    X3Q_TS(0, 7);
 
     // launch scales: max over the batch of the per-sample maxima (as conv2_wgrad_x3_kernel)
     float ma = 0.f, md = 0.f;
@@ -1492,7 +1570,11 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
     const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
     int u = u0;
     if (u < u1) {
-        x3q_issue_img(act16, u, wave, lane, lds_u32(smem));
+        if (X3Q_NBUF == 2) x3q_issue_img(act16, u, wave, lane, lds_u32(smem));
+        else if (wave >= 6) {
+            x3q_issue_img_loader(act16, u, wave, lane, lds_u32(smem));
+            x3q_issue_img_loader(act16, min(u + 1, u1 - 1), wave, lane, lds_u32(smem + X3Q_BUF));
+        }
         if (dstage) {
             load_dy(u);
             store_dy(smem, true);
@@ -1500,30 +1582,53 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
         }
     }
     int k = 0;
+    // buffer of this unit, of the next, and (NBUF = 3) of the one after: rotating indices
+    int bc = 0, bn = 1, bn2 = X3Q_NBUF == 3 ? 2 : 0;
+    // NBUF = 3: the loader waves (6, 7) keep the unit after next's 10 pieces in flight at the barrier
 #pragma unroll 1
     for (; u < u1; ++u, ++k) {
         // this unit's image DMA landed; the 8 dY loads (every staging wave's last memory instructions,
         // issued after its DMA) may stay in flight
-        if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        __syncthreads();  // buffer k&1 complete; buffer (k+1)&1 free
+        X3Q_TS(k, 6);
+        if (X3Q_NBUF == 2) {
+            if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (wave >= 6) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3Q_XPIECES) : "memory");
+        }
+        __syncthreads();  // buffer bc complete; the buffer of unit u - 1 free
+        X3Q_TS(k, 0);
         const int nx = u + 1, nx2 = u + 2;
-        const char* img = smem + (k & 1) * X3Q_BUF;
-        char* nimg = smem + ((k & 1) ^ 1) * X3Q_BUF;
+        const char* img = smem + bc * X3Q_BUF;
+        char* nimg = smem + bn * X3Q_BUF;
         // tap-group-1 waves (the lighter MFMA share) route dY before their MFMAs, tap-group-0 after:
         // the two waves of a SIMD overlap routing with MFMAs; store_dy before the DMA issue (hipcc does
         // not count the asm DMAs: its wait for the dY registers would also wait for them)
         const bool dfirst = tg == 1;
         if (dfirst && dstage) store_dy(nimg, nx < u1);
-        x3q_issue_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
+        if (X3Q_NBUF == 2) x3q_issue_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
+        else if (wave >= 6) x3q_issue_img_loader(act16, min(nx2, u1 - 1), wave, lane, lds_u32(smem + bn2 * X3Q_BUF));
         if (dfirst && dstage) load_dy(min(nx2, u1 - 1));
+        X3Q_TS(k, 1);
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
         else unit_mfma(img, std::integral_constant<int, 1>{});
+        X3Q_TS(k, 2);
         if (!dfirst && dstage) {
             store_dy(nimg, nx < u1);
             load_dy(min(nx2, u1 - 1));
         }
+        X3Q_TS(k, 3);
+        if (X3Q_NBUF == 3) {
+            const int t = bc;
+            bc = bn;
+            bn = bn2;
+            bn2 = t;
+        } else {
+            bc ^= 1;
+            bn ^= 1;
+        }
     }
+    X3Q_TS(127, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped) image DMA lands before LDS reuse
     __syncthreads();
     // db partials of the staging items -> LDS; co = 32 dc + 4 dg + j summed over the 24 windows in order
@@ -1647,6 +1752,59 @@ __global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __rest
     }
 }
 
+// ============================================================================ codec -> x3 input images
+// The server side of the compressed cut exchange (slk_codec.hip) writing conv2's x3 operand directly: a
+// micro-batch's received mask + values + word ranks (slk_cut_ranks) and the shipped per-sample scale value
+// become the act16 images the client's conv1_fwd_x3 would have written (the same f32 values split at the
+// same 2^x3_exp(amax): bit for bit), with no dense f32 cut in HBM. One workgroup per sample: its 676 mask
+// words and ranks staged in LDS; item (pixel p, chunk c8) gathers its 8 channels' values (element
+// c * 676 + p of the sample; unset elements are +0) and stores 16 B per plane, as conv1_fwd_x3.
+__global__ __launch_bounds__(C1X_T) void cut_unpack_x3_kernel(const float* __restrict__ vals,
+                                                              const uint32_t* __restrict__ mask,
+                                                              const int* __restrict__ ranks,
+                                                              const float* __restrict__ amax,
+                                                              uint16_t* __restrict__ act16) {
+    constexpr int NW = A_SAMPLE / 32;  // 676 mask words per sample
+    __shared__ uint32_t sm[NW];
+    __shared__ int sr[NW];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < NW; i += C1X_T) {
+        sm[i] = mask[(size_t)b * NW + i];
+        sr[i] = ranks[(size_t)b * NW + i];
+    }
+    __syncthreads();
+    const float sc = ldexpf(1.f, x3_exp(amax[b]));
+    const int c8 = tid & 3;
+    char* img = reinterpret_cast<char*>(act16) + (size_t)b * X3S_SAMPLE;
+#pragma unroll 2
+    for (int i = tid; i < A_PIX * 4; i += C1X_T) {
+        const int p = i >> 2, xx = p - (p / A_HW) * A_HW;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int e = (8 * c8 + j) * A_PIX + p, w = e >> 5, bit = e & 31;
+            const uint32_t m = sm[w];
+            v[j] = 0.f;
+            if ((m >> bit) & 1u) v[j] = vals[(size_t)sr[w] + __popc(m & ((1u << bit) - 1u))];
+        }
+        f16x8 hh, ll;
+        x3_split8(v, sc, hh, ll);
+        char* o = img + p * 64 + (c8 ^ (xx & 2)) * 16;
+        *reinterpret_cast<f16x8*>(o) = hh;
+        *reinterpret_cast<f16x8*>(o + X3S_PLANE) = ll;
+    }
+}
+
+extern "C" int slk_cut_unpack_x3(const float* vals, const uint32_t* mask, const int* ranks, const float* act_amax,
+                                 int B, uint16_t* act16, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && (int64_t)B * A_SAMPLE <= 2147483647LL);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(vals && mask && ranks && act_amax && act16);
+    hipLaunchKernelGGL(cut_unpack_x3_kernel, dim3(B), dim3(C1X_T), 0, slk_stream(stream), vals, mask, ranks, act_amax,
+                       act16);
+    return slk_launch_status();
+}
+
 // ============================================================================ C-ABI
 extern "C" int slk_row_amax(const float* x, int rows, int n, float* amax, void* stream) {
     SLK_CHECK_ARG(rows >= 0 && n > 0 && (rows == 0 || (x && amax)));
@@ -1710,6 +1868,20 @@ extern "C" int slk_conv2_dgrad_x3(const float* dpooled, const float* dp_amax, co
     const int P = 3 * B;
     hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
                        slk_stream(stream), dpooled, dp_amax, code, W2, cut_grad, B, nullptr, nullptr, nullptr);
+    return slk_launch_status();
+}
+
+// the cut gradient in the codec's packed form (conv2_dgrad_x3_kernel's PACK note): values of the elements set
+// in `mask` (the received cut's, B samples from element 0) at their ranks (slk_cut_ranks)
+extern "C" int slk_conv2_dgrad_x3_pack(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                                       const uint32_t* mask, const int* ranks, float* vals, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && (int64_t)B * A_SAMPLE <= 2147483647LL);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(dpooled && dp_amax && code && W2 && mask && ranks && vals);
+    const int P = 3 * B;
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
+                       slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, nullptr, nullptr, nullptr, mask, ranks,
+                       vals);
     return slk_launch_status();
 }
 

@@ -29,6 +29,9 @@ _SIGS = {
     "slk_cut_offsets": [_P, _L, _P, _P, _P, _P],
     "slk_cut_pack": [_P, _L, _P, _P, _P, _P],
     "slk_cut_unpack": [_P, _L, _P, _P, _P, _P],
+    "slk_cut_ranks": [_P, _L, _P, _P, _P],
+    "slk_cut_unpack_x3": [_P, _P, _P, _P, _I, _P, _P],
+    "slk_conv2_dgrad_x3_pack": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
     "slk_error_string": [_I],
     "slk_build_id": [],
     "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],

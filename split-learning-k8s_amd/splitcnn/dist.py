@@ -290,15 +290,21 @@ class Hub:
     sending it, on a side stream, while k+1 computes; the server posts micro-batch k's receives once
     its count has landed), so no step-wide host sync holds the first send back. Results are
     bit-identical to the dense exchange. False = the dense fp32 exchange; a codec object (the
-    CutCodec interface) is used as given. `compress` and `ship_amax` are constructor arguments that
+    CutCodec interface) is used as given.
+    fuse_codec (default True; server, compress on, ship_amax on, an x3 engine stage): the received
+    micro-batch is unpacked straight into the x3 input images (ops.cut_unpack_x3: no dense f32 cut) and
+    the dgrad writes the cut gradient already packed at the mask's positions (ops.conv2_dgrad_x3_pack:
+    no dense gradient, no pack pass); the server then computes exactly what the dense images exchange
+    (images=True) computes, bit for bit. `compress` and `ship_amax` are constructor arguments that
     both sides must agree on — neither side infers them from its own device.
     `exchange_bytes` counts what moved on this rank's link(s), `dense_bytes` what the dense exchange
     would have moved."""
 
     def __init__(self, stage, rank: int, world: int, client_group=None, micro: int = 1, compress=True,
                  server_rank: Optional[int] = None, client_ranks=None, graph: bool = True, groups=None,
-                 ship_amax: bool = True, images: bool = False):
+                 ship_amax: bool = True, images: bool = False, fuse_codec: bool = True):
         self.stage, self.rank, self.world = stage, rank, world
+        self.fuse_codec = bool(fuse_codec)
         # images (dense exchange only): the client ships its x3 split images (act16, the same 86,528 B a
         # sample as the f32 cut) + per-sample max instead of the f32 act, and the server runs the image
         # forward (conv2_fwd_pool_x3i) instead of staging + splitting f32 rows in-kernel
@@ -324,6 +330,9 @@ class Hub:
         self.exchange_bytes = 0
         self.dense_bytes = 0
         self._codec = None
+        # server: False after a step whose cut gradient left packed (fuse_codec): the dense `cuts` buffer
+        # was not written; cuts_by_client scatters what went on the wire instead
+        self.cut_dense = True
         # the server passes the shipped max on only to stages whose compute takes it (engine stages)
         self._amax_kw = "act_amax" in inspect.signature(stage.compute).parameters if hasattr(stage, "compute") else False
         if self.images and self.is_server:
@@ -340,6 +349,15 @@ class Hub:
     @property
     def is_server(self):
         return self.rank == self.server_rank
+
+    def _fused(self, codec) -> bool:
+        """Server: the codec exchange runs through the fused kernels (see fuse_codec)."""
+        if codec is None or not (self.fuse_codec and self.ship_amax and self._amax_kw) or self.images:
+            return False
+        st = self.stage
+        takes = inspect.signature(st.compute).parameters if hasattr(st, "compute") else {}
+        impls = tuple(getattr(st, a, None) for a in ("impl_fwd", "impl_dgrad", "impl_wgrad"))
+        return impls == ("x3", "x3", "x3") and "act16" in takes and "cut_pack" in takes
 
     def _use_codec(self, device):
         if self.compress is False or self.compress is None:
@@ -500,34 +518,48 @@ class Hub:
         b, G = B // m, nc * B
         CH = nc * b
         n = b * 32 * 26 * 26
-        acts = self._inputs(G, device)
+        acts = self._inputs(G, device, codec)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         parts = self._buf("loss_parts", (m,), torch.float32, device)
         ch = slice(k * CH, (k + 1) * CH)
+        fused = self._fused(codec)
+        amx = self._buf("amax", (G,), torch.float32, device) if self.ship_amax else None
+        packs = []
         if codec is not None:
             for ci in range(nc):
                 bk = codec.buffers(("s", ci, k), n, device)
                 codec.offsets(n, bk)
-                codec.unpack(acts[k * CH + ci * b:k * CH + (ci + 1) * b], bk)
+                s0 = k * CH + ci * b
+                if fused:
+                    from . import ops
+                    rk = codec.ranks(("s", ci, k), n, bk)
+                    ops.cut_unpack_x3(bk[4], bk[0], rk, amx[s0:s0 + b], acts[s0 * IMG_BYTES:(s0 + b) * IMG_BYTES])
+                    packs.append((ci * b, (ci + 1) * b, bk[0], rk,
+                                  self._buf(("gvals", ci, k), (n,), torch.float32, device)))
+                else:
+                    codec.unpack(acts[s0:s0 + b], bk)
         kw = {}
         if self.ship_amax and self._amax_kw:
-            kw["act_amax"] = self._buf("amax", (G,), torch.float32, device)[ch]
-        if self.images:
+            kw["act_amax"] = amx[ch]
+        if self.images or fused:
             kw["act16"] = acts[k * CH * IMG_BYTES:(k + 1) * CH * IMG_BYTES]
+            if fused:
+                kw["cut_pack"] = packs
             _, loss_i = s.compute(None, labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         else:
             _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         _loss_sum(loss_i, 1.0 / G, parts[k:k + 1])
-        if codec is not None:
+        if codec is not None and not fused:
             for ci in range(nc):
                 bk = codec.buffers(("s", ci, k), n, device)
                 codec.pack(cuts[k * CH + ci * b:k * CH + (ci + 1) * b], bk,
                            vals=self._buf(("gvals", ci, k), (n,), torch.float32, device))
 
-    def _inputs(self, G, device):
-        """The server's receive buffer of the cut: f32 act [G, 32, 26, 26], or the images' bytes."""
-        if self.images:
+    def _inputs(self, G, device, codec=None):
+        """The server's input buffer of the cut: f32 act [G, 32, 26, 26], or the images' bytes (the dense
+        images exchange receives them; the fused codec path unpacks into them)."""
+        if self.images or self._fused(codec):
             return self._buf("imgs", (G * IMG_BYTES,), torch.uint8, device)
         return self._buf("acts", (G, 32, 26, 26), torch.float32, device)
 
@@ -540,7 +572,7 @@ class Hub:
         if not self._graphed(device) or all((k, B, codec is not None) in self._graphs for k in range(self.micro)):
             return
         G = self.nclients * B
-        self._inputs(G, device).zero_()
+        self._inputs(G, device, codec).zero_()
         self._buf("labels", (G,), torch.int64, device).zero_()
         if self.ship_amax:
             self._buf("amax", (G,), torch.float32, device).zero_()
@@ -583,12 +615,13 @@ class Hub:
         n = b * 32 * 26 * 26
         fw, bw = self.groups
         ship = self.ship_amax
-        acts = self._inputs(G, device)
+        codec = self._use_codec(device)
+        self.cut_dense = not self._fused(codec)
+        acts = self._inputs(G, device, codec)
         labels = self._buf("labels", (G,), torch.int64, device)
         cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         amx = self._buf("amax", (G,), torch.float32, device) if ship else None
         parts = self._buf("loss_parts", (m,), torch.float32, device)
-        codec = self._use_codec(device)
         self._prepare(B, device, codec)
         part = lambda k, ci: slice(k * CH + ci * b, k * CH + (ci + 1) * b)  # noqa: E731
         side = self._side_stream(device)
@@ -642,9 +675,19 @@ class Hub:
         self.global_step += 1
 
     def cuts_by_client(self, B: int) -> torch.Tensor:
-        """The last step's cut gradient in client order [client][B] (the server keeps [k][client][b])."""
+        """The last step's cut gradient in client order [client][B] (the server keeps [k][client][b]).
+        After a fused-codec step (cut_dense False) that is what went on the wire, scattered: the gradient at
+        the cut's nonzero positions, zeros elsewhere (positions the client's ReLU discards)."""
         m, nc = self.micro, self.nclients
         cuts = self._bufs["cuts"]
+        if not self.cut_dense:
+            b = B // m
+            n = b * 32 * 26 * 26
+            for k in range(m):
+                for ci in range(nc):
+                    s0 = (k * nc + ci) * b
+                    self._codec.unpack(cuts[s0:s0 + b], self._codec.buffers(("s", ci, k), n, cuts.device),
+                                       vals=self._buf(("gvals", ci, k), (n,), torch.float32, cuts.device))
         return cuts.view(m, nc, B // m, *cuts.shape[1:]).transpose(0, 1).reshape(nc * B, *cuts.shape[1:])
 
 
@@ -654,13 +697,13 @@ class Pipeline(Hub):
     the micro-batches and step once per batch (= the reference step at batch B)."""
 
     def __init__(self, stage, role: str, peer: int, micro: int = 4, compress=True, graph: bool = True,
-                 groups=None, ship_amax: bool = True, images: bool = False):
+                 groups=None, ship_amax: bool = True, images: bool = False, fuse_codec: bool = True):
         assert role in ("client", "server")
         me = dist.get_rank()
         super().__init__(stage, me, dist.get_world_size(), None, micro, compress,
                          server_rank=peer if role == "client" else me,
                          client_ranks=[me] if role == "client" else [peer], graph=graph, groups=groups,
-                         ship_amax=ship_amax, images=images)
+                         ship_amax=ship_amax, images=images, fuse_codec=fuse_codec)
         self.role, self.peer = role, peer
 
 

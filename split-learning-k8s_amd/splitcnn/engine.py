@@ -295,14 +295,17 @@ class ServerStage:
 
     def forward_backward(self, act: Optional[torch.Tensor], labels: torch.Tensor, grad_scale: float,
                          cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
-                         act16: Optional[torch.Tensor] = None, client_fuse=None):
+                         act16: Optional[torch.Tensor] = None, client_fuse=None, cut_pack=None):
         """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
         conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
         of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise.
         act16 (with act_amax, x3 forward + wgrad only): the client's split input images
         (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, relu_bits,
         slabs) (x3 dgrad only, single-GPU step): the dgrad also runs the client's ReLU backward +
-        conv1 wgrad into `slabs` and the cut gradient is not materialised (returned as None)."""
+        conv1 wgrad into `slabs` and the cut gradient is not materialised (returned as None).
+        cut_pack = [(start, stop, mask, ranks, vals), ...] (x3 dgrad only; the codec exchange, dist.Hub):
+        the cut gradient of samples start:stop leaves packed at the positions of that part's received mask
+        (ops.conv2_dgrad_x3_pack) instead of dense; returned as None."""
         B = labels.shape[0]
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
@@ -354,7 +357,14 @@ class ServerStage:
                                              impl=wi, act_amax=act_amax, dp_amax=dp_amax, act16=act16)
         if self.wgrad_first:
             s2 = wgrad()
-        if client_fuse is not None:
+        if cut_pack is not None:
+            if di != "x3":
+                raise ValueError("cut_pack needs the x3 dgrad (conv preset 'x3' or 'x3w')")
+            with TIMER("conv2_dgrad"):
+                for s0, s1, pmask, pranks, pvals in cut_pack:
+                    ops.conv2_dgrad_x3_pack(dpooled[s0:s1], code[s0:s1], W2, dp_amax[s0:s1], pmask, pranks, pvals)
+            cut_grad = None
+        elif client_fuse is not None:
             if di != "x3":
                 raise ValueError("client_fuse needs the x3 dgrad (conv preset 'x3' or 'x3w')")
             cx, cbits, cslabs = client_fuse
@@ -384,10 +394,11 @@ class ServerStage:
         ops.reduce_slabs(s2, out=self.grads[:ops.CONV2_SLAB], accumulate=accumulate)
         ops.reduce_slabs(s3, out=self.grads[ops.CONV2_SLAB:], accumulate=accumulate)
 
-    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act_amax=None, act16=None):
+    def compute(self, act, labels, grad_scale, accumulate=False, cut_grad=None, act_amax=None, act16=None,
+                cut_pack=None):
         """forward_backward + reduce into self.grads; returns (cut_grad, loss_i)."""
         cut_grad, loss_i, s2, s3 = self.forward_backward(act, labels, grad_scale, cut_grad=cut_grad,
-                                                         act_amax=act_amax, act16=act16)
+                                                         act_amax=act_amax, act16=act16, cut_pack=cut_pack)
         self.reduce_grads(s2, s3, accumulate=accumulate)
         return cut_grad, loss_i
 

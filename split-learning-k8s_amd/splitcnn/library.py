@@ -294,11 +294,13 @@ def _linear_setup(ctx, inputs, output):
 
 def _linear_backward(ctx, dlogits):
     flat, W3 = ctx.saved_tensors
-    dflat = torch.ops.splitcnn.linear_dgrad(dlogits, W3) if ctx.needs_input_grad[0] else None
     dW3 = db3 = None
+    # the weight gradient first: it re-reads flat (151 MB at B = 4096) while the forward's copy is still in
+    # the Infinity Cache; the input gradient's 151 MB write would evict it (the fused step's order too)
     if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
         g = torch.ops.splitcnn.linear_wgrad(dlogits, flat)
         dW3, db3 = g[:92160].view(10, 9216), g[92160:].view(10)
+    dflat = torch.ops.splitcnn.linear_dgrad(dlogits, W3) if ctx.needs_input_grad[0] else None
     return dflat, dW3, db3
 
 

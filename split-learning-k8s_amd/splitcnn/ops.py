@@ -301,6 +301,30 @@ def conv2_dgrad(dpooled, code, W2, out=None, direct=False, impl=None, dp_amax=No
     return cut_grad
 
 
+def conv2_dgrad_x3_pack(dpooled, code, W2, dp_amax, mask, ranks, vals):
+    """The x3 cut gradient in the codec's packed form (slk_conv2_dgrad_x3_pack): the values of the elements
+    set in `mask` (the received cut's: int32 words, ceil(B*21632/32)) at their word ranks (cut_ranks), into
+    `vals` — what CutCodec.pack extracts from conv2_dgrad(..., impl="x3") without the dense gradient."""
+    B = _dpooled_batch(dpooled)
+    nw = (B * 21632 + 31) // 32
+    _lib.call("slk_conv2_dgrad_x3_pack", _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
+              _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+              _dev(mask, "mask", (nw,), torch.int32), _dev(ranks, "ranks", (nw,), torch.int32),
+              _dev(vals, "vals"), B, _stream(dpooled))
+    return vals
+
+
+def cut_unpack_x3(vals, mask, ranks, act_amax, act16):
+    """A received codec micro-batch (mask + values + word ranks, B samples) -> the x3 input images act16
+    (conv2_act16_bytes(B) uint8) at the scales act_amax: conv1_fwd_x3's images of the same cut, bit for bit."""
+    B = batch_of(act_amax, (), "act_amax")
+    nw = (B * 21632 + 31) // 32
+    _lib.call("slk_cut_unpack_x3", _dev(vals, "vals"), _dev(mask, "mask", (nw,), torch.int32),
+              _dev(ranks, "ranks", (nw,), torch.int32), _dev(act_amax, "act_amax", (B,)), B, _act16(act16, B),
+              _stream(act_amax))
+    return act16
+
+
 def conv2_wgrad_nslab(B: int, direct: bool = False, impl=None) -> int:
     impl = _impl(direct, impl)
     return _lib.query({"wino": "slk_conv2_wgrad_nslab", "direct": "slk_conv2_wgrad_direct_nslab",

@@ -1,0 +1,136 @@
+"""The fused consumers of the compressed cut exchange (round 5, VERDICT r4 "missing" item 3): the server
+unpacks a received micro-batch straight into the x3 input images and the dgrad writes the cut gradient
+already packed. Both must reproduce the unfused path (dense unpack -> x3 forward from f32 rows; dense
+dgrad -> pack) bit for bit. Reference exchange: src/client_part.py:117-131 <-> src/server_part.py:38-58."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cut(gpu, B, seed=4):
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage
+    a, s = init_models(seed=seed)
+    x, y = SyntheticMNIST(seed).batch(B)
+    cl = ClientStage(a, device=gpu)
+    cl.emit_amax = True
+    act = cl.forward(x.to(gpu)).clone()
+    return a, s, x.to(gpu), y.to(gpu), act, cl._act_amax.clone()
+
+
+@pytest.mark.parametrize("B", [1, 3, 64])
+def test_cut_ranks_match_the_mask_prefix(gpu, B):
+    from splitcnn.codec import CutCodec
+    *_, act, _ = _cut(gpu, B)
+    n = act.numel()
+    c = CutCodec()
+    bk = c.buffers("t", n, gpu)
+    c.encode(act, bk)
+    rk = c.ranks("t", n, bk)
+    torch.cuda.synchronize()
+    bits = (act.reshape(-1).view(torch.int32) != 0).to(torch.int64)
+    want = torch.cumsum(bits, 0) - bits                     # rank of every element = set elements before it
+    assert torch.equal(rk.to(torch.int64), want[::32])
+    assert int(bk[3].item()) == int(bits.sum())
+
+
+@pytest.mark.parametrize("B", [1, 5, 96])
+def test_unpack_into_images_matches_the_client_images(gpu, B):
+    """cut_unpack_x3 of the encoded cut == the images conv1_fwd_x3 writes for the same cut and scale."""
+    from splitcnn import ops
+    from splitcnn.codec import CutCodec
+    a, _, x, _, act, amx = _cut(gpu, B)
+    ref = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu)
+    am2 = torch.empty(B, device=gpu)
+    ops.conv1_fwd_x3(x, a.conv1.weight.detach().to(gpu).contiguous(), a.conv1.bias.detach().to(gpu).contiguous(), am2, ref)
+    assert torch.equal(am2, amx)
+    n = act.numel()
+    c = CutCodec()
+    bk = c.buffers("t", n, gpu)
+    c.encode(act, bk)
+    # the receiving side: offsets from the mask alone, then ranks
+    bk2 = c.buffers("r", n, gpu)
+    bk2[0].copy_(bk[0])
+    bk2[4].copy_(bk[4])
+    c.offsets(n, bk2)
+    rk = c.ranks("r", n, bk2)
+    img = torch.full_like(ref, 0xA5)
+    ops.cut_unpack_x3(bk2[4], bk2[0], rk, amx, img)
+    torch.cuda.synchronize()
+    assert torch.equal(img, ref)
+
+
+@pytest.mark.parametrize("B", [2, 48])
+def test_packed_dgrad_matches_pack_of_dense_dgrad(gpu, B):
+    """conv2_dgrad_x3_pack == CutCodec.pack(conv2_dgrad(..., impl='x3')) at the cut's set positions."""
+    from splitcnn import ops
+    from splitcnn.codec import CutCodec
+    _, s, _, y, act, amx = _cut(gpu, B)
+    W2, b2 = s.conv2.weight.detach().to(gpu).contiguous(), s.conv2.bias.detach().to(gpu).contiguous()
+    W3, b3 = s.fc1.weight.detach().to(gpu).contiguous(), s.fc1.bias.detach().to(gpu).contiguous()
+    pooled, code = ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amx)
+    dpa = torch.empty(B, device=gpu)
+    _, _, _, dp = ops.fc_xent(pooled, W3, b3, y, 1.0 / B, dp_amax=dpa)
+    dense = ops.conv2_dgrad(dp, code, W2, impl="x3", dp_amax=dpa)
+    n = act.numel()
+    c = CutCodec()
+    bk = c.buffers("t", n, gpu)
+    c.encode(act, bk)
+    want = torch.zeros(n, device=gpu)
+    c.pack(dense, bk, vals=want)
+    rk = c.ranks("t", n, bk)
+    got = torch.full((n,), float("nan"), device=gpu)
+    ops.conv2_dgrad_x3_pack(dp, code, W2, dpa, bk[0], rk, got)
+    torch.cuda.synchronize()
+    t = int(bk[3].item())
+    assert 0 < t < n
+    assert torch.equal(got[:t].view(torch.int32), want[:t].view(torch.int32))
+    assert torch.isnan(got[t:]).all()       # nothing written past the packed values
+
+
+def test_hub_fused_codec_server_matches_unfused_bitwise(gpu):
+    """dist.Hub server chunks with the fused codec kernels (default) vs fuse_codec=False (dense unpack ->
+    x3 forward from f32 rows, dense dgrad -> pack): losses, every packed cut gradient and the parameters
+    after the SGD step are bit-identical. K4 shape: 3 clients x 2 chunks, graphs on."""
+    from splitcnn import dist as sd
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    nc, m, B = 3, 2, 32
+    b, G = B // m, nc * B
+    n = b * 32 * 26 * 26
+    data = SyntheticMNIST(9)
+    parts = [data.batch(b) for _ in range(m * nc)]
+    res = []
+    for fuse in (False, True):
+        a, s = init_models(seed=2)
+        hub = sd.Hub(ServerStage(s, device=gpu), rank=nc, world=nc + 1, micro=m, compress=True, fuse_codec=fuse)
+        cl = ClientStage(a, device=gpu)
+        cl.emit_amax = True
+        codec = hub._use_codec(gpu)
+        assert hub._fused(codec) == fuse
+        hub._prepare(B, gpu, codec)
+        labels = hub._buf("labels", (G,), torch.int64, gpu)
+        amx = hub._buf("amax", (G,), torch.float32, gpu)
+        hub._buf("cuts", (G, 32, 26, 26), torch.float32, gpu)
+        hub._buf("loss_parts", (m,), torch.float32, gpu)
+        for k in range(m):
+            for ci in range(nc):
+                sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
+                x, y = parts[k * nc + ci]
+                act = cl.forward(x.to(gpu))
+                amx[sl].copy_(cl._act_amax)
+                labels[sl].copy_(y.to(gpu))
+                codec.encode(act, codec.buffers(("s", ci, k), n, gpu))
+        for k in range(m):
+            hub._run_chunk(k, B, gpu, codec)
+        hub.stage.step()
+        torch.cuda.synchronize()
+        tot = [int(codec.buffers(("s", ci, k), n, gpu)[3].item()) for k in range(m) for ci in range(nc)]
+        gv = [hub._buf(("gvals", ci, k), (n,), torch.float32, gpu)[:tot[k * nc + ci]].clone()
+              for k in range(m) for ci in range(nc)]
+        res.append((hub._bufs["loss_parts"].clone(), gv, hub.stage.params.clone()))
+    (l0, g0, p0), (l1, g1, p1) = res
+    assert torch.equal(l0, l1)
+    assert all(torch.equal(u.view(torch.int32), v.view(torch.int32)) for u, v in zip(g0, g1))
+    assert torch.equal(p0, p1)

@@ -3,6 +3,7 @@ tools/build_variant.sh, or older trees) side by side in ONE process, interleaved
 usage: python tools/ablate.py lib0.so lib1.so ... [--batch 4096 --rounds 5]"""
 import argparse
 import ctypes
+import os
 import json
 
 import torch
@@ -12,13 +13,14 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--cases", default="", help="comma-separated subset of the cases (default: all)")
 args = ap.parse_args()
 B = args.batch
 dev = torch.device("cuda:0")
 P = ctypes.c_void_p
 libs = []
 for path in args.libs:
-    L = ctypes.CDLL(path)
+    L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_DEEPBIND)  # own symbols first
     for n in ("slk_conv2_fwd_pool", "slk_conv2_dgrad", "slk_conv2_wgrad", "slk_conv1_fwd", "slk_conv1_wgrad",
               "slk_fc_xent", "slk_fc_wgrad", "slk_conv1_wgrad_remask"):
         getattr(L, n).restype = ctypes.c_int
@@ -78,8 +80,13 @@ def calls(L):
         "conv1_wgrad": lambda: L.slk_conv1_wgrad(p(x), p(act), p(gcut), p(slabs), B, P(s)),
         "conv1_wgrad_remask": lambda: L.slk_conv1_wgrad_remask(p(x), p(W1), p(b1), p(gcut), p(slabs), B, P(s)),
         "fc_wgrad": lambda: L.slk_fc_wgrad(p(dl), p(pooled), p(slabs), B, P(s)),
+        "row_amax": lambda: L.slk_row_amax(p(act), B, 32 * 26 * 26, p(amx), P(s)),
     }
 
+amx = torch.empty(B, device=dev)
+_all_calls = calls
+if args.cases:
+    calls = lambda L: {k: v for k, v in _all_calls(L).items() if k in args.cases.split(",")}  # noqa: E731
 res = {i: {} for i in range(len(libs))}
 for r in range(args.rounds):
     for i, L in enumerate(libs):

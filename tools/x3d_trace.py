@@ -2,7 +2,9 @@
 build with -DSLK_X3D_TRACE=1 (tools/build_variant.sh x3dtrace "-DSLK_X3D_TRACE=1"): per (workgroup, wave,
 unit) shader-clock stamps at the unit barrier, around the staging and the MFMA loops and after the
 conv1-gradient epilogue. Prints the mean cycles per phase per wave slot.
-usage: python tools/x3d_trace.py build_abl/x3dtrace.so [--B 4096]"""
+--kernel wgrad: the same for conv2_wgrad_x3q_kernel (stamps at the unit barrier, after the first-half
+waves' dY routing + image DMA issue, after the MFMAs, after the second-half waves' routing).
+usage: python tools/x3d_trace.py build_abl/x3dtrace.so [--B 4096] [--kernel dgrad|wgrad]"""
 import argparse
 import ctypes
 import os
@@ -21,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--B", type=int, default=4096)
+    ap.add_argument("--kernel", default="dgrad", choices=["dgrad", "wgrad"])
     args = ap.parse_args()
     from splitcnn import ops
     from splitcnn.data import SyntheticMNIST, init_models
@@ -54,6 +57,12 @@ def main():
     L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 7 + [ctypes.c_int, P]
     sl = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
     run = lambda: L.slk_conv2_dgrad_x3_c1w(p(dp), p(dpa), p(code), p(W2), p(xg), p(bits), p(sl), B, st)  # noqa: E731
+    if args.kernel == "wgrad":
+        L.slk_conv2_wgrad_x3_nslab.restype = ctypes.c_int
+        L.slk_conv2_wgrad_x3s.restype = ctypes.c_int
+        L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
+        slw = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), 18496, device=dev)
+        run = lambda: L.slk_conv2_wgrad_x3s(p(a16), p(am1), p(dp), p(dpa), p(code), p(slw), B, st)  # noqa: E731
     ms = []
     for i in range(12):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,13 +73,17 @@ def main():
         ms.append(e0.elapsed_time(e1))
     ms = sorted(ms[2:])
     buf = np.zeros(256 * 8 * NU * NS, dtype=np.uint64)
-    assert L.slk_x3d_trace_read(ctypes.c_void_p(buf.ctypes.data)) == 0
+    rd = L.slk_x3q_trace_read if args.kernel == "wgrad" else L.slk_x3d_trace_read
+    assert rd(ctypes.c_void_p(buf.ctypes.data)) == 0
     T = buf.reshape(256, 8, NU, NS).astype(np.int64)
     t_start = T[:, :, 0, 7]
     t_end = T[:, :, 127, 7]
     span = (t_end.max() - t_start.min())
     print(f"kernel median {ms[len(ms) // 2]:.4f} ms; stamp span {span} ticks -> {span / (ms[len(ms) // 2] * 1e3):.1f} ticks/us")
     G = 256
+    if args.kernel == "wgrad":
+        wgrad_report(T, (6 * B + G - 1) // G)
+        return
     per = (3 * B + G - 1) // G
     nu = 2 * per
     print(f"units per workgroup {nu}")
@@ -111,6 +124,24 @@ def main():
             print(f"part {pt} h {h}: unit {unit[wgs, :, uus].mean():7.0f}  barrier wait by wave "
                   + " ".join(f"{bar[wgs, w, uus].mean():5.0f}" for w in range(8))
                   + "  mfma by wave " + " ".join(f"{(main_ + t3)[wgs, w, uus].mean():5.0f}" for w in range(8)))
+
+
+def wgrad_report(T, nu):
+    u = np.arange(nu)
+    print(f"units per workgroup {nu}; prologue {(T[:, :, 0, 0] - T[:, :, 0, 7]).mean():.0f}")
+    bar = T[:, :, u, 0] - T[:, :, u, 6]
+    pre = T[:, :, u, 1] - T[:, :, u, 0]
+    mf = T[:, :, u, 2] - T[:, :, u, 1]
+    post = T[:, :, u, 3] - T[:, :, u, 2]
+    gap = np.zeros_like(bar)
+    gap[:, :, :-1] = T[:, :, u[1:], 6] - T[:, :, u[:-1], 3]
+    unit = np.zeros_like(bar)
+    unit[:, :, :-1] = T[:, :, u[1:], 0] - T[:, :, u[:-1], 0]
+    print("wave = 4 tg + 2 c + h; tg 1 (waves 4-7) route before their MFMAs; waves 6-7 route nothing")
+    print(f"{'wave':>4} {'barrier':>8} {'route<':>8} {'mfma':>8} {'route>':>8} {'gap':>6} {'unit':>8}")
+    for w in range(8):
+        print(f"{w:>4} {bar[:, w].mean():8.0f} {pre[:, w].mean():8.0f} {mf[:, w].mean():8.0f} {post[:, w].mean():8.0f} "
+              f"{gap[:, w, :-1].mean():6.0f} {unit[:, w, :-1].mean():8.0f}")
 
 
 if __name__ == "__main__":
