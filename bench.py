@@ -501,7 +501,7 @@ XGMI_LINK_GBPS = 153.6   # vendor per-link xGMI figure (task brief: 7 links x ~1
 # Server-side rates of the hub step on one GPU (bench k4_server_loopback; samples/s at B = 4096 per
 # client): with the dense exchange the server runs the plain stage kernels, with the codec it also unpacks
 # and packs. Used only for the exchange PREDICTION reported next to the measured trial that decides.
-HUB_SERVER_RATE = {"dense": 5.2e6, "codec": 3.5e6}   # round 4: dense = the image exchange (Hub images=True)
+HUB_SERVER_RATE = {"dense": 5.1e6, "codec": 4.1e6}   # round 5: dense = the image exchange; codec = the fused server kernels
 CODEC_WIRE_FRACTION = 0.456   # wire bytes / dense bytes of the codec on the synthetic data
 
 

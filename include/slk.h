@@ -293,6 +293,16 @@ int slk_cut_unpack_x3(const float* vals, const uint32_t* mask, const int* ranks,
                       uint16_t* act16, void* stream);
 int slk_conv2_dgrad_x3_pack(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
                             const uint32_t* mask, const int* ranks, float* vals, int B, void* stream);
+/* The same over the np parts of one server chunk (one part per client, each n elements / part_b samples) in
+ * one launch per pass: `parts` is a device table of pointers (uint64 each) —
+ *   offsets_ranks_parts: [np][5] = (mask, counts, offsets, total, ranks): count + scan + ranks of every part;
+ *   unpack_x3_parts    : [B / part_b][3] = (vals, mask, ranks); sample b reads part b / part_b;
+ *   dgrad_x3_pack_parts: [B / part_b][3] = (mask, ranks, vals). */
+int slk_cut_offsets_ranks_parts(const uint64_t* parts, int np, int64_t n, void* stream);
+int slk_cut_unpack_x3_parts(const uint64_t* parts, int part_b, const float* act_amax, int B, uint16_t* act16,
+                            void* stream);
+int slk_conv2_dgrad_x3_pack_parts(const float* dpooled, const float* dp_amax, const uint8_t* code, const float* W2,
+                                  const uint64_t* parts, int part_b, int B, void* stream);
 
 /* ================================================================ widened split CNN (BASELINE config 5)
  * The reference has no such model: these entry points run the north star's

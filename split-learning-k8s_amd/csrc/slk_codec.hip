@@ -17,6 +17,7 @@
 namespace {
 constexpr int CB = 2048;            // elements per block
 constexpr int CB_WORDS = CB / 32;   // uint32 mask words per block
+constexpr int CS_LDS = 12288;       // block counts the scan stages in LDS
 }  // namespace
 
 // Thread t of a block owns elements 8t .. 8t+7 of the block (bits 8 (t & 3) .. +7 of mask word t / 4):
@@ -82,8 +83,7 @@ __global__ __launch_bounds__(CT) void cut_mask_kernel(const uint32_t* __restrict
 }
 
 // per-block counts from a mask (the receiving side): one wave per block, lane = mask word
-__global__ __launch_bounds__(256) void cut_count_kernel(const uint32_t* __restrict__ mask, long n, int nblk,
-                                                        int* __restrict__ counts) {
+__device__ __forceinline__ void cut_count_body(const uint32_t* __restrict__ mask, long n, int nblk, int* __restrict__ counts) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= nblk) return;  // wave-uniform
     const long nw = (n + 31) / 32;
@@ -93,12 +93,16 @@ __global__ __launch_bounds__(256) void cut_count_kernel(const uint32_t* __restri
     for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
     if (lane == 0) counts[b] = c;
 }
+__global__ __launch_bounds__(256) void cut_count_kernel(const uint32_t* __restrict__ mask, long n, int nblk,
+                                                        int* __restrict__ counts) {
+    cut_count_body(mask, n, nblk, counts);
+}
 
 // word ranks (the fused consumers, slk_cut_unpack_x3 / slk_conv2_dgrad_x3_pack): ranks[w] = the vals index of
 // the first set element of mask word w = offsets[block] + the set bits of the block's earlier words. One
 // wave per block, lane = mask word: an element's rank is then ranks[e / 32] + popc(mask[e / 32] below e % 32)
-__global__ __launch_bounds__(256) void cut_ranks_kernel(const uint32_t* __restrict__ mask, long n, int nblk,
-                                                        const int* __restrict__ offsets, int* __restrict__ ranks) {
+__device__ __forceinline__ void cut_ranks_body(const uint32_t* __restrict__ mask, long n, int nblk,
+                                               const int* __restrict__ offsets, int* __restrict__ ranks) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= nblk) return;  // wave-uniform
     const long nw = (n + 31) / 32;
@@ -112,14 +116,38 @@ __global__ __launch_bounds__(256) void cut_ranks_kernel(const uint32_t* __restri
     }
     if (w < nw) ranks[w] = offsets[b] + inc - c;
 }
+__global__ __launch_bounds__(256) void cut_ranks_kernel(const uint32_t* __restrict__ mask, long n, int nblk,
+                                                        const int* __restrict__ offsets, int* __restrict__ ranks) {
+    cut_ranks_body(mask, n, nblk, offsets, ranks);
+}
+
+__device__ void cut_scan_body(const int* __restrict__ counts, int nblk, int* __restrict__ offsets,
+                              int* __restrict__ total, int* part, int* cs);
+
+// The same three passes over the np parts of a chunk in one launch each (dist.Hub: one part per client):
+// parts = device table [np][5] of (mask, counts, offsets, total, ranks) pointers, every part n elements;
+// blockIdx.y (count, ranks) / blockIdx.x (scan) = the part
+__global__ __launch_bounds__(256) void cut_count_parts_kernel(const uint64_t* __restrict__ parts, long n, int nblk) {
+    const uint64_t* e = parts + 5 * blockIdx.y;
+    cut_count_body(reinterpret_cast<const uint32_t*>(e[0]), n, nblk, reinterpret_cast<int*>(e[1]));
+}
+__global__ __launch_bounds__(1024) void cut_scan_parts_kernel(const uint64_t* __restrict__ parts, int nblk) {
+    __shared__ int part[1024];
+    __shared__ int cs[CS_LDS];
+    const uint64_t* e = parts + 5 * blockIdx.x;
+    cut_scan_body(reinterpret_cast<const int*>(e[1]), nblk, reinterpret_cast<int*>(e[2]), reinterpret_cast<int*>(e[3]),
+                  part, cs);
+}
+__global__ __launch_bounds__(256) void cut_ranks_parts_kernel(const uint64_t* __restrict__ parts, long n, int nblk) {
+    const uint64_t* e = parts + 5 * blockIdx.y;
+    cut_ranks_body(reinterpret_cast<const uint32_t*>(e[0]), n, nblk, reinterpret_cast<const int*>(e[2]),
+                   reinterpret_cast<int*>(e[4]));
+}
 
 // exclusive scan of the block counts (one workgroup) -> offsets; total -> total[0]. Up to CS_LDS counts
 // are staged in LDS by coalesced loads (each thread then scans a contiguous range from LDS).
-constexpr int CS_LDS = 12288;
-__global__ __launch_bounds__(1024) void cut_scan_kernel(const int* __restrict__ counts, int nblk,
-                                                        int* __restrict__ offsets, int* __restrict__ total) {
-    __shared__ int part[1024];
-    __shared__ int cs[CS_LDS];
+__device__ void cut_scan_body(const int* __restrict__ counts, int nblk, int* __restrict__ offsets,
+                              int* __restrict__ total, int* part, int* cs) {
     const int t = threadIdx.x;
     const bool staged = nblk <= CS_LDS;
     if (staged) {
@@ -155,6 +183,12 @@ __global__ __launch_bounds__(1024) void cut_scan_kernel(const int* __restrict__ 
         }
     }
     if (t == 1023) total[0] = part[1023];
+}
+__global__ __launch_bounds__(1024) void cut_scan_kernel(const int* __restrict__ counts, int nblk,
+                                                        int* __restrict__ offsets, int* __restrict__ total) {
+    __shared__ int part[1024];
+    __shared__ int cs[CS_LDS];
+    cut_scan_body(counts, nblk, offsets, total, part, cs);
 }
 
 // PACK: vals[offset + rank] = x[i] for the set elements; UNPACK: x[i] = set ? vals[...] : 0. The block's
@@ -238,6 +272,18 @@ extern "C" int slk_cut_ranks(const uint32_t* mask, int64_t n, const int* offsets
     SLK_CHECK_ARG(mask && offsets && ranks);
     const int nb = cut_blocks(n);
     hipLaunchKernelGGL(cut_ranks_kernel, dim3((nb + 3) / 4), dim3(256), 0, slk_stream(stream), mask, n, nb, offsets, ranks);
+    return slk_launch_status();
+}
+
+extern "C" int slk_cut_offsets_ranks_parts(const uint64_t* parts, int np, int64_t n, void* stream) {
+    SLK_CHECK_ARG(n >= 0 && n <= CUT_NMAX && np >= 0 && np <= 65535);
+    if (n == 0 || np == 0) return 0;
+    SLK_CHECK_ARG(parts);
+    const int nb = cut_blocks(n);
+    hipStream_t st = slk_stream(stream);
+    hipLaunchKernelGGL(cut_count_parts_kernel, dim3((nb + 3) / 4, np), dim3(256), 0, st, parts, n, nb);
+    hipLaunchKernelGGL(cut_scan_parts_kernel, dim3(np), dim3(1024), 0, st, parts, nb);
+    hipLaunchKernelGGL(cut_ranks_parts_kernel, dim3((nb + 3) / 4, np), dim3(256), 0, st, parts, n, nb);
     return slk_launch_status();
 }
 

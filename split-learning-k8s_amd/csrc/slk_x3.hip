@@ -586,7 +586,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     const float* __restrict__ W2, float* __restrict__ cut_grad, int B, const float* __restrict__ xin = nullptr,
     const uint32_t* __restrict__ relu_bits = nullptr, float* __restrict__ c1slabs = nullptr,
     const uint32_t* __restrict__ pmask = nullptr, const int* __restrict__ pranks = nullptr,
-    float* __restrict__ pvals = nullptr) {
+    float* __restrict__ pvals = nullptr, const uint64_t* __restrict__ pparts = nullptr, int ppart_b = 0) {
     __shared__ __attribute__((aligned(1024))) char smem[2 * X3D_IMG];
     // C1W: per pair, x (3,136 B), a second copy of x, then its ReLU bits (2,704 B), double-buffered
     // (XB_BYTES apart, a multiple of 128 B), moved by LDS-DMA; after both buffers the plane of ones (below).
@@ -946,20 +946,32 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         if constexpr (C1W) {
             c1w_epi(T0, T1, us1, q);
             X3D_TS(k - 1, 5);
-        } else if (pvals != nullptr) {
-            // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4)
-            const size_t e0 = ((size_t)b * C1 + 16 * nt + n16) * A_PIX;
+        } else if (pvals != nullptr || pparts != nullptr) {
+            // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4);
+            // pparts: the sample's part (dist.Hub chunk = one part per client) picks (mask, ranks, vals)
+            const uint32_t* pmask_ = pmask;
+            const int* pranks_ = pranks;
+            float* pvals_ = pvals;
+            int lb = b;
+            if (pparts != nullptr) {
+                const int part = b / ppart_b;
+                lb = b - part * ppart_b;
+                pmask_ = reinterpret_cast<const uint32_t*>(pparts[3 * part]);
+                pranks_ = reinterpret_cast<const int*>(pparts[3 * part + 1]);
+                pvals_ = reinterpret_cast<float*>(pparts[3 * part + 2]);
+            }
+            const size_t e0 = ((size_t)lb * C1 + 16 * nt + n16) * A_PIX;
 #pragma unroll
             for (int i = 0; i < X3D_MPW; ++i) {
                 const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
                 if (t < T1 && p < A_PIX) {
                     const size_t e = e0 + p, w = e >> 5;
                     const int bit = (int)(e & 31);
-                    const uint32_t m = pmask[w];
-                    int r = pranks[w] + __popc(m & ((1u << bit) - 1u));
+                    const uint32_t m = pmask_[w];
+                    int r = pranks_[w] + __popc(m & ((1u << bit) - 1u));
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr)
-                        if ((m >> (bit + rr)) & 1u) pvals[r++] = x3_unscale(acc[i][rr], us1, us2);
+                        if ((m >> (bit + rr)) & 1u) pvals_[r++] = x3_unscale(acc[i][rr], us1, us2);
                 }
             }
         } else {
@@ -1759,18 +1771,30 @@ __global__ __launch_bounds__(C1X_T) void conv1_fwd_x3_kernel(const float* __rest
 // same 2^x3_exp(amax): bit for bit), with no dense f32 cut in HBM. One workgroup per sample: its 676 mask
 // words and ranks staged in LDS; item (pixel p, chunk c8) gathers its 8 channels' values (element
 // c * 676 + p of the sample; unset elements are +0) and stores 16 B per plane, as conv1_fwd_x3.
+// parts (optional): a device table [np][3] of (vals, mask, ranks) pointers, part_b samples each (one launch for
+// a dist.Hub chunk: one part per client)
 __global__ __launch_bounds__(C1X_T) void cut_unpack_x3_kernel(const float* __restrict__ vals,
                                                               const uint32_t* __restrict__ mask,
                                                               const int* __restrict__ ranks,
                                                               const float* __restrict__ amax,
-                                                              uint16_t* __restrict__ act16) {
+                                                              uint16_t* __restrict__ act16,
+                                                              const uint64_t* __restrict__ parts = nullptr,
+                                                              int part_b = 0) {
     constexpr int NW = A_SAMPLE / 32;  // 676 mask words per sample
     __shared__ uint32_t sm[NW];
     __shared__ int sr[NW];
     const int b = blockIdx.x, tid = threadIdx.x;
+    int lb = b;
+    if (parts != nullptr) {
+        const int part = b / part_b;
+        lb = b - part * part_b;
+        vals = reinterpret_cast<const float*>(parts[3 * part]);
+        mask = reinterpret_cast<const uint32_t*>(parts[3 * part + 1]);
+        ranks = reinterpret_cast<const int*>(parts[3 * part + 2]);
+    }
     for (int i = tid; i < NW; i += C1X_T) {
-        sm[i] = mask[(size_t)b * NW + i];
-        sr[i] = ranks[(size_t)b * NW + i];
+        sm[i] = mask[(size_t)lb * NW + i];
+        sr[i] = ranks[(size_t)lb * NW + i];
     }
     __syncthreads();
     const float sc = ldexpf(1.f, x3_exp(amax[b]));
@@ -1801,7 +1825,18 @@ extern "C" int slk_cut_unpack_x3(const float* vals, const uint32_t* mask, const 
     if (B == 0) return 0;
     SLK_CHECK_ARG(vals && mask && ranks && act_amax && act16);
     hipLaunchKernelGGL(cut_unpack_x3_kernel, dim3(B), dim3(C1X_T), 0, slk_stream(stream), vals, mask, ranks, act_amax,
-                       act16);
+                       act16, nullptr, 0);
+    return slk_launch_status();
+}
+
+// all parts of a chunk in one launch: parts = device table [B / part_b][3] of (vals, mask, ranks) pointers
+extern "C" int slk_cut_unpack_x3_parts(const uint64_t* parts, int part_b, const float* act_amax, int B, uint16_t* act16,
+                                       void* stream) {
+    SLK_CHECK_ARG(B >= 0 && part_b > 0 && B % part_b == 0 && (int64_t)part_b * A_SAMPLE <= 2147483647LL);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(parts && act_amax && act16);
+    hipLaunchKernelGGL(cut_unpack_x3_kernel, dim3(B), dim3(C1X_T), 0, slk_stream(stream), nullptr, nullptr, nullptr,
+                       act_amax, act16, parts, part_b);
     return slk_launch_status();
 }
 
@@ -1882,6 +1917,19 @@ extern "C" int slk_conv2_dgrad_x3_pack(const float* dpooled, const float* dp_ama
     hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
                        slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, nullptr, nullptr, nullptr, mask, ranks,
                        vals);
+    return slk_launch_status();
+}
+
+// all parts of a chunk in one launch: parts = device table [B / part_b][3] of (mask, ranks, vals) pointers
+extern "C" int slk_conv2_dgrad_x3_pack_parts(const float* dpooled, const float* dp_amax, const uint8_t* code,
+                                             const float* W2, const uint64_t* parts, int part_b, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && part_b > 0 && B % part_b == 0 && (int64_t)part_b * A_SAMPLE <= 2147483647LL);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(dpooled && dp_amax && code && W2 && parts);
+    const int P = 3 * B;
+    hipLaunchKernelGGL(conv2_dgrad_x3_kernel<false>, dim3(P < X3D_GRID ? P : X3D_GRID), dim3(X3D_THREADS), 0,
+                       slk_stream(stream), dpooled, dp_amax, code, W2, nullptr, B, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, parts, part_b);
     return slk_launch_status();
 }
 

@@ -32,6 +32,9 @@ _SIGS = {
     "slk_cut_ranks": [_P, _L, _P, _P, _P],
     "slk_cut_unpack_x3": [_P, _P, _P, _P, _I, _P, _P],
     "slk_conv2_dgrad_x3_pack": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_cut_offsets_ranks_parts": [_P, _I, _L, _P],
+    "slk_cut_unpack_x3_parts": [_P, _I, _P, _I, _P, _P],
+    "slk_conv2_dgrad_x3_pack_parts": [_P, _P, _P, _P, _P, _I, _I, _P],
     "slk_error_string": [_I],
     "slk_build_id": [],
     "slk_conv1_fwd": [_P, _P, _P, _P, _I, _P],

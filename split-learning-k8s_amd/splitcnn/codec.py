@@ -40,12 +40,16 @@ class CutCodec:
                 self._buf((key, "total"), (1,), torch.int32, device),
                 self._buf((key, "vals"), (n,), torch.float32, device))
 
+    def ranks_buffer(self, key, n: int, device):
+        """The word-ranks buffer of key's micro-batch (int32, ceil(n/32)), not computed."""
+        return self._buf((key, "ranks"), ((n + 31) // 32,), torch.int32, device)
+
     def ranks(self, key, n: int, bufs):
         """Word ranks of a micro-batch whose offsets are computed (offsets() / encode()): ranks[w] = the vals
         index of mask word w's first set element, for the fused consumers (ops.cut_unpack_x3,
         ops.conv2_dgrad_x3_pack). Buffer keyed like buffers()."""
         mask, _, offsets, _, _ = bufs
-        r = self._buf((key, "ranks"), (mask.numel(),), torch.int32, mask.device)
+        r = self.ranks_buffer(key, n, mask.device)
         _lib.call("slk_cut_ranks", mask.data_ptr(), n, offsets.data_ptr(), r.data_ptr(), _stream(mask))
         return r
 

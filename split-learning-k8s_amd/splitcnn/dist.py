@@ -525,27 +525,26 @@ class Hub:
         ch = slice(k * CH, (k + 1) * CH)
         fused = self._fused(codec)
         amx = self._buf("amax", (G,), torch.float32, device) if self.ship_amax else None
-        packs = []
-        if codec is not None:
+        if fused:
+            # every client part of the chunk in ONE launch per pass (per-launch prologues x parts were most of
+            # the codec's cost): count + scan + word ranks, unpack into the images, and (the dgrad) pack
+            from . import ops
+            t_off, t_unp, t_pack = self._part_tables(k, b, n, device, codec)
+            ops.cut_offsets_ranks_parts(t_off, n)
+            ops.cut_unpack_x3_parts(t_unp, b, amx[ch], acts[k * CH * IMG_BYTES:(k + 1) * CH * IMG_BYTES])
+        elif codec is not None:
             for ci in range(nc):
                 bk = codec.buffers(("s", ci, k), n, device)
                 codec.offsets(n, bk)
                 s0 = k * CH + ci * b
-                if fused:
-                    from . import ops
-                    rk = codec.ranks(("s", ci, k), n, bk)
-                    ops.cut_unpack_x3(bk[4], bk[0], rk, amx[s0:s0 + b], acts[s0 * IMG_BYTES:(s0 + b) * IMG_BYTES])
-                    packs.append((ci * b, (ci + 1) * b, bk[0], rk,
-                                  self._buf(("gvals", ci, k), (n,), torch.float32, device)))
-                else:
-                    codec.unpack(acts[s0:s0 + b], bk)
+                codec.unpack(acts[s0:s0 + b], bk)
         kw = {}
         if self.ship_amax and self._amax_kw:
             kw["act_amax"] = amx[ch]
         if self.images or fused:
             kw["act16"] = acts[k * CH * IMG_BYTES:(k + 1) * CH * IMG_BYTES]
             if fused:
-                kw["cut_pack"] = packs
+                kw["cut_pack"] = (t_pack, b)
             _, loss_i = s.compute(None, labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         else:
             _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
@@ -555,6 +554,28 @@ class Hub:
                 bk = codec.buffers(("s", ci, k), n, device)
                 codec.pack(cuts[k * CH + ci * b:k * CH + (ci + 1) * b], bk,
                            vals=self._buf(("gvals", ci, k), (n,), torch.float32, device))
+
+    def _part_tables(self, k, b, n, device, codec):
+        """Device pointer tables of chunk k's client parts for the fused codec kernels (int64 [nc, 5] / [nc, 3]
+        / [nc, 3], see ops.cut_offsets_ranks_parts / cut_unpack_x3_parts / conv2_dgrad_x3_pack_parts). The
+        buffers they point to are never replaced (keyed by size), so each table is written once per (k, b) —
+        by the eager warm-up before a graph capture, never inside it."""
+        nc = self.nclients
+        key = ("tables", k, b)
+        tabs = self._pool.get(key)
+        if tabs is None:
+            rows_off, rows_unp, rows_pack = [], [], []
+            for ci in range(nc):
+                mask, counts, offsets, total, vals = codec.buffers(("s", ci, k), n, device)
+                rk = codec.ranks_buffer(("s", ci, k), n, device)
+                gv = self._buf(("gvals", ci, k), (n,), torch.float32, device)
+                rows_off.append([t.data_ptr() for t in (mask, counts, offsets, total, rk)])
+                rows_unp.append([vals.data_ptr(), mask.data_ptr(), rk.data_ptr()])
+                rows_pack.append([mask.data_ptr(), rk.data_ptr(), gv.data_ptr()])
+            tabs = tuple(torch.tensor(r, dtype=torch.int64).to(device) for r in (rows_off, rows_unp, rows_pack))
+            torch.cuda.current_stream(device).synchronize()
+            self._pool[key] = tabs
+        return tabs
 
     def _inputs(self, G, device, codec=None):
         """The server's input buffer of the cut: f32 act [G, 32, 26, 26], or the images' bytes (the dense

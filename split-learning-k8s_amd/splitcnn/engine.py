@@ -303,9 +303,10 @@ class ServerStage:
         (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, relu_bits,
         slabs) (x3 dgrad only, single-GPU step): the dgrad also runs the client's ReLU backward +
         conv1 wgrad into `slabs` and the cut gradient is not materialised (returned as None).
-        cut_pack = [(start, stop, mask, ranks, vals), ...] (x3 dgrad only; the codec exchange, dist.Hub):
-        the cut gradient of samples start:stop leaves packed at the positions of that part's received mask
-        (ops.conv2_dgrad_x3_pack) instead of dense; returned as None."""
+        cut_pack = (parts, part_b) (x3 dgrad only; the codec exchange, dist.Hub): the cut gradient leaves
+        packed at the positions of each part's received mask — parts = int64 device table [B / part_b, 3] of
+        (mask, ranks, vals) pointers, one part per part_b samples (ops.conv2_dgrad_x3_pack_parts) — instead
+        of dense; returned as None."""
         B = labels.shape[0]
         m = self.model
         W2, b2 = m.conv2.weight.detach(), m.conv2.bias.detach()
@@ -361,8 +362,7 @@ class ServerStage:
             if di != "x3":
                 raise ValueError("cut_pack needs the x3 dgrad (conv preset 'x3' or 'x3w')")
             with TIMER("conv2_dgrad"):
-                for s0, s1, pmask, pranks, pvals in cut_pack:
-                    ops.conv2_dgrad_x3_pack(dpooled[s0:s1], code[s0:s1], W2, dp_amax[s0:s1], pmask, pranks, pvals)
+                ops.conv2_dgrad_x3_pack_parts(dpooled, code, W2, dp_amax, *cut_pack)
             cut_grad = None
         elif client_fuse is not None:
             if di != "x3":

@@ -314,6 +314,35 @@ def conv2_dgrad_x3_pack(dpooled, code, W2, dp_amax, mask, ranks, vals):
     return vals
 
 
+def conv2_dgrad_x3_pack_parts(dpooled, code, W2, dp_amax, parts, part_b):
+    """conv2_dgrad_x3_pack over the B / part_b parts of a server chunk in one launch: parts = int64 device
+    table [B / part_b, 3] of (mask, ranks, vals) pointers (slk_conv2_dgrad_x3_pack_parts)."""
+    B = _dpooled_batch(dpooled)
+    if part_b <= 0 or B % part_b:
+        raise ValueError(f"part_b {part_b} must divide the chunk's {B} samples")
+    _lib.call("slk_conv2_dgrad_x3_pack_parts", _dev(dpooled, "dpooled"), _dev(dp_amax, "dp_amax", (B,)),
+              _dev(code, "code", (B, 64, 12, 12), torch.uint8), _dev(W2, "conv2.weight", (64, 32, 3, 3)),
+              _dev(parts, "parts", (B // part_b, 3), torch.int64), part_b, B, _stream(dpooled))
+
+
+def cut_unpack_x3_parts(parts, part_b, act_amax, act16):
+    """cut_unpack_x3 over the B / part_b parts of a server chunk in one launch: parts = int64 device table
+    [B / part_b, 3] of (vals, mask, ranks) pointers (slk_cut_unpack_x3_parts)."""
+    B = batch_of(act_amax, (), "act_amax")
+    if part_b <= 0 or B % part_b:
+        raise ValueError(f"part_b {part_b} must divide the chunk's {B} samples")
+    _lib.call("slk_cut_unpack_x3_parts", _dev(parts, "parts", (B // part_b, 3), torch.int64), part_b,
+              _dev(act_amax, "act_amax", (B,)), B, _act16(act16, B), _stream(act_amax))
+    return act16
+
+
+def cut_offsets_ranks_parts(parts, n):
+    """Counts, offsets, totals and word ranks of every part of a chunk from its received mask, three launches
+    for all parts: parts = int64 device table [np, 5] of (mask, counts, offsets, total, ranks) pointers."""
+    _lib.call("slk_cut_offsets_ranks_parts", _dev(parts, "parts", (parts.shape[0], 5), torch.int64), parts.shape[0], n,
+              _stream(parts))
+
+
 def cut_unpack_x3(vals, mask, ranks, act_amax, act16):
     """A received codec micro-batch (mask + values + word ranks, B samples) -> the x3 input images act16
     (conv2_act16_bytes(B) uint8) at the scales act_amax: conv1_fwd_x3's images of the same cut, bit for bit."""
