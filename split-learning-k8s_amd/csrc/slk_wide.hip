@@ -336,50 +336,9 @@ __device__ __forceinline__ void exp_store(char* slot, int i, uint4 v, uint2 cw) 
     }
 }
 
-// SLK_WIDE_EXPPAIR (HW = 32, where the per-lane column rotation of exp_store measured slower): two lanes per
-// pooled chunk, lane pair (i, dx) storing the column-dx positions of both window rows: the 8 lanes of a
-// ds_write_b128 group (4 consecutive px x 2 dx) then fill all 8 16-B slots of 128 B
-#ifndef SLK_WIDE_EXPPAIR
-#define SLK_WIDE_EXPPAIR 0
-#endif
-template <class C>
-__device__ __forceinline__ void exp_store_half(char* slot, int i, int dx, uint4 v, uint2 cw) {
-    constexpr int PH = C::HW / 2;
-    const int c = i / (C::XPR * PH), rem = i - c * (C::XPR * PH), pr = rem / PH, px = rem - pr * PH;
-    const uint32_t cA = __builtin_amdgcn_perm(0u, cw.x, 0x01010000u), cB = __builtin_amdgcn_perm(0u, cw.x, 0x03030202u);
-    const uint32_t cC = __builtin_amdgcn_perm(0u, cw.y, 0x01010000u), cD = __builtin_amdgcn_perm(0u, cw.y, 0x03030202u);
-    char* base = slot + (c * C::NPP + 2 * px + 1 + dx) * 16;
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy) {
-        const int ry = 2 * pr + dy - 1;
-        if (ry < 0 || ry > C::TR + 1) continue;
-        lds_store16(base + ry * C::PW * 16, route_chunk(v, cA, cB, cC, cD, 2 * dy + dx));
-    }
-}
-
 // the staged items of this thread (landed and barrier-published) -> the tile in `slot`
 template <class C>
 __device__ __forceinline__ void exp_expand(char* slot, const char* raw, int tid) {
-    if constexpr (SLK_WIDE_EXPPAIR && C::HW == 32) {
-        constexpr int XR2 = (2 * C::XITEMS + C::THREADS - 1) / C::THREADS;
-#pragma unroll
-        for (int r = 0; r < XR2; ++r) {
-            const int i2 = tid + r * C::THREADS;
-            if (i2 >= 2 * C::XITEMS) break;
-            const int i = i2 >> 1;
-            const uint32_t a = (uint32_t)(size_t)(lds_ptr_t)(raw + i * 16);
-            const uint32_t b = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 16 + i * 4);
-            const uint32_t c = (uint32_t)(size_t)(lds_ptr_t)(raw + C::XN * 20 + i * 4);
-            u32x4 v4;
-            uint32_t c0, c1;
-            asm volatile("ds_read_b128 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-                         : "=&v"(v4), "=&v"(c0), "=&v"(c1)
-                         : "v"(a), "v"(b), "v"(c)
-                         : "memory");
-            exp_store_half<C>(slot, i, i2 & 1, make_uint4(v4[0], v4[1], v4[2], v4[3]), make_uint2(c0, c1));
-        }
-        return;
-    }
 #pragma unroll
     for (int r = 0; r < C::XR; ++r) {
         const int i = tid + r * C::THREADS;

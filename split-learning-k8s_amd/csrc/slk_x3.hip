@@ -601,7 +601,10 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
     static_assert(XB_X > 3072 && XB_X <= 4096 && XB_X % 16 == 0 && RB_SAMPLE * 4 > 2048 && RB_SAMPLE * 4 <= 3072 &&
                   RB_SAMPLE % 4 == 0 && XB_COPY % 16 == 0 && XB_BITS % 16 == 0, "DMA pieces of issue_xb");
     static_assert((XB_COPY / 4) % 32 == 12 && XB_BYTES % 128 == 0, "x copy 12 banks over");
-    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 * XB_BYTES + 32 + XB_X : 16];
+    // PACK (C1W = false): per pair, the mask words and word ranks its epilogue needs — [ci 32][PKW words] of
+    // each, from the pair's first pixel — double-buffered like C1W's x / bits (2 x 2,560 B)
+    constexpr int PKW = 10, PK_BYTES = 2 * C1 * PKW * 4;
+    __shared__ __attribute__((aligned(1024))) char xbm[C1W ? 2 * XB_BYTES + 32 + XB_X : 2 * PK_BYTES];
     // C1W: each wave's conv1-gradient accumulator D1[ci 16 nt + 4 (lane >> 4) + r][col lane & 15] (col =
     // tap 0-8, 9 = bias), kept here between epilogues (not in the MFMA loop's registers)
     __shared__ __attribute__((aligned(16))) f32x4 d1s[C1W ? X3D_THREADS : 1];
@@ -772,6 +775,47 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             glds16_so(reinterpret_cast<const char*>(relu_bits + b * RB_SAMPLE) + wave * 1024, (uint32_t)lane * 16,
                       dst + XB_BITS + wave * 1024);
     };
+    // PACK: sample bb's (mask, ranks, vals) and its index within them (pparts: its part's, else the launch's)
+    const bool pack = !C1W && (pvals != nullptr || pparts != nullptr);
+    auto pack_ptrs = [&](int bb, const uint32_t*& mk, const int*& rk, float*& vl, int& lb, int& nsb) {
+        mk = pmask;
+        rk = pranks;
+        vl = pvals;
+        lb = bb;
+        nsb = B;
+        if (pparts != nullptr) {
+            const int part = bb / ppart_b;
+            lb = bb - part * ppart_b;
+            nsb = ppart_b;
+            mk = reinterpret_cast<const uint32_t*>(pparts[3 * part]);
+            rk = reinterpret_cast<const int*>(pparts[3 * part + 1]);
+            vl = reinterpret_cast<float*>(pparts[3 * part + 2]);
+        }
+    };
+    // PACK: pair pp's words -> buffer buf: 640 words (mask then ranks, [ci][PKW] each) in 10 glds4 pieces of 64
+    // lanes (waves 0-7 one each, waves 0-1 a second); words past the part's last read its last word (unused)
+    auto issue_pk = [&](int pp, int buf) {
+        const int bb = pp / 3, pt = pp - (pp / 3) * 3;
+        const uint32_t* mk;
+        const int* rk;
+        float* vl;
+        int lb, nsb;
+        pack_ptrs(bb, mk, rk, vl, lb, nsb);
+        const int q0 = 16 * x3d_t0(pt);
+        const uint32_t dst = lds_u32(xbm) + buf * PK_BYTES;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int piece = wave + 8 * r;
+            if (piece < 2 * C1 * PKW / 64) {
+                const int idx = piece * 64 + lane, arr = idx >= C1 * PKW ? 1 : 0, j = idx - arr * C1 * PKW;
+                const int ci = j / PKW, jj = j - (j / PKW) * PKW;
+                const int w = min(((((lb * C1 + ci) * A_PIX) + q0) >> 5) + jj, nsb * (A_SAMPLE / 32) - 1);
+                glds4(arr ? reinterpret_cast<const void*>(rk + w) : reinterpret_cast<const void*>(mk + w),
+                      dst + piece * 256);
+            }
+        }
+    };
+    if (pack && pr < p1) issue_pk(pr, 0);
     if constexpr (C1W) {
         d1s[tid] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int e = tid; e < IN_HW * IN_HW; e += X3D_THREADS) ones[e] = 1.f;
@@ -865,7 +909,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         for (int h = 0; h < 2; ++h, ++k) {
             // C1W: this pair's x / bits DMA (issued during the previous pair) retired before the barrier
             X3D_TS(k, 6);
-            if (C1W && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((C1W || pack) && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
             X3D_TS(k, 0);
             // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue). The
@@ -873,6 +917,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // for the dY registers would wait for the DMA just issued (a full memory latency per pair)
             const bool sfirst = wave >= 4;
             if (C1W && h == 0 && !(SLK_X3D_XBLATE && sfirst)) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
+            if (pack && h == 0) issue_pk(min(pr + 1, p1 - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
             const int unx = min(h ? 2 * (pr + 1) : 2 * pr + 1, 2 * p1 - 1);   // the unit after this one
@@ -946,29 +991,26 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         if constexpr (C1W) {
             c1w_epi(T0, T1, us1, q);
             X3D_TS(k - 1, 5);
-        } else if (pvals != nullptr || pparts != nullptr) {
+        } else if (pack) {
             // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4);
-            // pparts: the sample's part (dist.Hub chunk = one part per client) picks (mask, ranks, vals)
-            const uint32_t* pmask_ = pmask;
-            const int* pranks_ = pranks;
-            float* pvals_ = pvals;
-            int lb = b;
-            if (pparts != nullptr) {
-                const int part = b / ppart_b;
-                lb = b - part * ppart_b;
-                pmask_ = reinterpret_cast<const uint32_t*>(pparts[3 * part]);
-                pranks_ = reinterpret_cast<const int*>(pparts[3 * part + 1]);
-                pvals_ = reinterpret_cast<float*>(pparts[3 * part + 2]);
-            }
-            const size_t e0 = ((size_t)lb * C1 + 16 * nt + n16) * A_PIX;
+            // the word and its rank come from this pair's LDS copy (issue_pk, one pair ahead)
+            const uint32_t* mk;
+            const int* rk;
+            float* pvals_;
+            int lb, nsb;
+            pack_ptrs(b, mk, rk, pvals_, lb, nsb);
+            const int ci = 16 * nt + n16;
+            const uint32_t* smk = reinterpret_cast<const uint32_t*>(xbm + (q & 1) * PK_BYTES) + ci * PKW;
+            const int* srk = reinterpret_cast<const int*>(xbm + (q & 1) * PK_BYTES) + C1 * PKW + ci * PKW;
+            const int e0 = (lb * C1 + ci) * A_PIX, wst = (e0 + 16 * T0) >> 5;
 #pragma unroll
             for (int i = 0; i < X3D_MPW; ++i) {
                 const int t = T0 + g + 4 * i, p = 16 * t + 4 * kc;
                 if (t < T1 && p < A_PIX) {
-                    const size_t e = e0 + p, w = e >> 5;
-                    const int bit = (int)(e & 31);
-                    const uint32_t m = pmask_[w];
-                    int r = pranks_[w] + __popc(m & ((1u << bit) - 1u));
+                    const int e = e0 + p, jj = (e >> 5) - wst;
+                    const int bit = e & 31;
+                    const uint32_t m = smk[jj];
+                    int r = srk[jj] + __popc(m & ((1u << bit) - 1u));
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr)
                         if ((m >> (bit + rr)) & 1u) pvals_[r++] = x3_unscale(acc[i][rr], us1, us2);
