@@ -1427,19 +1427,24 @@ constexpr int X3Q_BUF = (X3Q_DYOFF + 2 * X3Q_DYC + 1023) / 1024 * 1024;  // 45,0
 constexpr int X3Q_NKS = 256;                             // K shares (slabs): one workgroup per CU
 constexpr int X3Q_DYITEMS = 24 * 16;                     // (window, 4-co group, co half) items per unit
 constexpr int X3Q_XPIECES = X3Q_XP / 1024 + 1;           // 10 DMA pieces per input plane (the last 768 B)
-#ifndef SLK_X3Q_NBUF
-#define SLK_X3Q_NBUF 2
+static_assert(2 * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
+
+// SLK_X3Q_W12: 12 waves (3 per SIMD) = (tap group tg 0-2: taps 3 tg .. 3 tg + 2, co half c, ci half h), at most
+// 168 VGPRs each, instead of 8 waves (2 per SIMD) with tap groups of 5 and 4 taps
+#ifndef SLK_X3Q_W12
+#define SLK_X3Q_W12 0
 #endif
-constexpr int X3Q_NBUF = SLK_X3Q_NBUF;                   // buffers: the image DMA runs NBUF - 1 units ahead
-static_assert(X3Q_NBUF * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
+constexpr int X3Q_THREADS = SLK_X3Q_W12 ? 768 : 512;
+constexpr int X3Q_WAVES = X3Q_THREADS / 64;
+constexpr int X3Q_NTMAX = SLK_X3Q_W12 ? 3 : 5;          // taps per wave (max)
 
 // LDS-DMA of unit uu's input image (rows 4t .. 4t + 5 of both planes of the sample's act16 image)
 __device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
     const int b = uu / 6, t = uu - (uu / 6) * 6;
     const char* src = reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t * (X3Q_ROWS * A_HW * 64);
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int k = wave + 8 * r;  // piece k of the 20: plane k / 10, piece k % 10
+    for (int r = 0; r < (2 * X3Q_XPIECES + X3Q_WAVES - 1) / X3Q_WAVES; ++r) {
+        const int k = wave + X3Q_WAVES * r;  // piece k of the 20: plane k / 10, piece k % 10
         if (k < 2 * X3Q_XPIECES) {
             const int pl = k >= X3Q_XPIECES ? 1 : 0, pp = k - X3Q_XPIECES * pl;
             if (pp < X3Q_XPIECES - 1 || lane < (X3Q_XP % 1024) / 16)
@@ -1448,23 +1453,10 @@ __device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int
     }
 }
 
-// NBUF = 3: waves 6 and 7 (which route no dY) move the whole image, one plane each (10 pieces), so the
-// dY register loads of waves 0-5 and the DMA never share a wave's vmcnt: the DMA can run two units ahead
-// without the compiler's waits for the dY registers also waiting for it
-__device__ __forceinline__ void x3q_issue_img_loader(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
-    const int b = uu / 6, t = uu - (uu / 6) * 6;
-    const int pl = wave - 6;
-    const char* src = reinterpret_cast<const char*>(act16) + (size_t)b * X3S_SAMPLE + t * (X3Q_ROWS * A_HW * 64) + pl * X3S_PLANE;
-#pragma unroll
-    for (int pp = 0; pp < X3Q_XPIECES; ++pp)
-        if (pp < X3Q_XPIECES - 1 || lane < (X3Q_XP % 1024) / 16)
-            glds16_so(src, (uint32_t)(pp * 1024 + lane * 16), lds + pl * X3Q_XP + pp * 1024);
-}
-
-__global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
+__global__ __launch_bounds__(X3Q_THREADS, 1) void conv2_wgrad_x3q_kernel(
     const uint16_t* __restrict__ act16, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
     const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3Q_NBUF * X3Q_BUF];
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3Q_BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = wave & 1, c = (wave >> 1) & 1, tg = wave >> 2;
@@ -1475,7 +1467,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
 
     // launch scales: max over the batch of the per-sample maxima (as conv2_wgrad_x3_kernel)
     float ma = 0.f, md = 0.f;
-    for (int i = tid; i < B; i += X3W_THREADS) {
+    for (int i = tid; i < B; i += X3Q_THREADS) {
         ma = fmaxf(ma, act_amax[i]);
         md = fmaxf(md, dp_amax[i]);
     }
@@ -1483,15 +1475,15 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
     md = wave_max(md);
     if (lane == 0) {
         red[wave] = ma;
-        red[8 + wave] = md;
+        red[16 + wave] = md;
     }
     __syncthreads();
     ma = red[0];
-    md = red[8];
+    md = red[16];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) {
+    for (int i = 1; i < X3Q_WAVES; ++i) {
         ma = fmaxf(ma, red[i]);
-        md = fmaxf(md, red[8 + i]);
+        md = fmaxf(md, red[16 + i]);
     }
     __syncthreads();
     const int sx = x3_exp(ma), sd = x3_exp(md);
@@ -1570,14 +1562,15 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     };
 
-    f32x4 acc[2][5];
+    f32x4 acc[2][X3Q_NTMAX];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int t = 0; t < 5; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < X3Q_NTMAX; ++t) acc[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     auto unit_mfma = [&](const char* img, auto TG) {
-        constexpr int T0 = decltype(TG)::value ? 5 : 0, NT = decltype(TG)::value ? 4 : 5;
+        constexpr int TGV = decltype(TG)::value;
+        constexpr int T0 = SLK_X3Q_W12 ? 3 * TGV : (TGV ? 5 : 0), NT = SLK_X3Q_W12 ? 3 : (TGV ? 4 : 5);
         constexpr int N = 3 * NT;
         f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
         auto rdA = [&](int j, int slot) {
@@ -1624,11 +1617,7 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
     const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
     int u = u0;
     if (u < u1) {
-        if (X3Q_NBUF == 2) x3q_issue_img(act16, u, wave, lane, lds_u32(smem));
-        else if (wave >= 6) {
-            x3q_issue_img_loader(act16, u, wave, lane, lds_u32(smem));
-            x3q_issue_img_loader(act16, min(u + 1, u1 - 1), wave, lane, lds_u32(smem + X3Q_BUF));
-        }
+        x3q_issue_img(act16, u, wave, lane, lds_u32(smem));
         if (dstage) {
             load_dy(u);
             store_dy(smem, true);
@@ -1636,51 +1625,35 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
         }
     }
     int k = 0;
-    // buffer of this unit, of the next, and (NBUF = 3) of the one after: rotating indices
-    int bc = 0, bn = 1, bn2 = X3Q_NBUF == 3 ? 2 : 0;
-    // NBUF = 3: the loader waves (6, 7) keep the unit after next's 10 pieces in flight at the barrier
 #pragma unroll 1
     for (; u < u1; ++u, ++k) {
         // this unit's image DMA landed; the 8 dY loads (every staging wave's last memory instructions,
         // issued after its DMA) may stay in flight
         X3Q_TS(k, 6);
-        if (X3Q_NBUF == 2) {
-            if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else if (wave >= 6) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3Q_XPIECES) : "memory");
-        }
-        __syncthreads();  // buffer bc complete; the buffer of unit u - 1 free
+        if (!dstage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __syncthreads();  // buffer k&1 complete; buffer (k+1)&1 free
         X3Q_TS(k, 0);
         const int nx = u + 1, nx2 = u + 2;
-        const char* img = smem + bc * X3Q_BUF;
-        char* nimg = smem + bn * X3Q_BUF;
+        const char* img = smem + (k & 1) * X3Q_BUF;
+        char* nimg = smem + ((k & 1) ^ 1) * X3Q_BUF;
         // tap-group-1 waves (the lighter MFMA share) route dY before their MFMAs, tap-group-0 after:
         // the two waves of a SIMD overlap routing with MFMAs; store_dy before the DMA issue (hipcc does
         // not count the asm DMAs: its wait for the dY registers would also wait for them)
         const bool dfirst = tg == 1;
         if (dfirst && dstage) store_dy(nimg, nx < u1);
-        if (X3Q_NBUF == 2) x3q_issue_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
-        else if (wave >= 6) x3q_issue_img_loader(act16, min(nx2, u1 - 1), wave, lane, lds_u32(smem + bn2 * X3Q_BUF));
+        x3q_issue_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
         if (dfirst && dstage) load_dy(min(nx2, u1 - 1));
         X3Q_TS(k, 1);
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
-        else unit_mfma(img, std::integral_constant<int, 1>{});
+        else if (!SLK_X3Q_W12 || tg == 1) unit_mfma(img, std::integral_constant<int, 1>{});
+        else if constexpr (SLK_X3Q_W12 != 0) unit_mfma(img, std::integral_constant<int, 2>{});
         X3Q_TS(k, 2);
         if (!dfirst && dstage) {
             store_dy(nimg, nx < u1);
             load_dy(min(nx2, u1 - 1));
         }
         X3Q_TS(k, 3);
-        if (X3Q_NBUF == 3) {
-            const int t = bc;
-            bc = bn;
-            bn = bn2;
-            bn2 = t;
-        } else {
-            bc ^= 1;
-            bn ^= 1;
-        }
     }
     X3Q_TS(127, 7);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped) image DMA lands before LDS reuse
@@ -1700,16 +1673,16 @@ __global__ __launch_bounds__(X3W_THREADS, 1) void conv2_wgrad_x3q_kernel(
     }
     const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
     const int ci = 16 * h + (lane & 15);
-    const int nt = tg ? 4 : 5;
+    const int nt = SLK_X3Q_W12 ? 3 : (tg ? 4 : 5), tap0 = SLK_X3Q_W12 ? 3 * tg : 5 * tg;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
 #pragma unroll
-        for (int t = 0; t < 5; ++t)
+        for (int t = 0; t < X3Q_NTMAX; ++t)
             if (t < nt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int co = 32 * c + 16 * mi + 4 * (lane >> 4) + r;
-                    slab[(co * C1 + ci) * 9 + 5 * tg + t] = x3_unscale(acc[mi][t][r], us1, us2);
+                    slab[(co * C1 + ci) * 9 + tap0 + t] = x3_unscale(acc[mi][t][r], us1, us2);
                 }
     }
 }
@@ -2011,7 +1984,7 @@ extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax,
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<true>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), nullptr,
                        act_amax, dpooled, dp_amax, code, slabs, B, act16);
 #else
-    hipLaunchKernelGGL(conv2_wgrad_x3q_kernel, dim3(nks), dim3(X3W_THREADS), 0, slk_stream(stream), act16, act_amax,
+    hipLaunchKernelGGL(conv2_wgrad_x3q_kernel, dim3(nks), dim3(X3Q_THREADS), 0, slk_stream(stream), act16, act_amax,
                        dpooled, dp_amax, code, slabs, B);
 #endif
     return slk_launch_status();
