@@ -1429,14 +1429,10 @@ constexpr int X3Q_DYITEMS = 24 * 16;                     // (window, 4-co group,
 constexpr int X3Q_XPIECES = X3Q_XP / 1024 + 1;           // 10 DMA pieces per input plane (the last 768 B)
 static_assert(2 * X3Q_BUF <= 163840 && X3Q_XP % 1024 == 768 && (X3Q_DYC / 4) % 32 == 16, "x3q layout");
 
-// SLK_X3Q_W12: 12 waves (3 per SIMD) = (tap group tg 0-2: taps 3 tg .. 3 tg + 2, co half c, ci half h), at most
-// 168 VGPRs each, instead of 8 waves (2 per SIMD) with tap groups of 5 and 4 taps
-#ifndef SLK_X3Q_W12
-#define SLK_X3Q_W12 0
-#endif
-constexpr int X3Q_THREADS = SLK_X3Q_W12 ? 768 : 512;
+// (round 5: 12 waves = 3 per SIMD at <= 168 VGPRs, tap groups of 3, measured the same: 0.2369 vs 0.2376 ms)
+constexpr int X3Q_THREADS = 512;
 constexpr int X3Q_WAVES = X3Q_THREADS / 64;
-constexpr int X3Q_NTMAX = SLK_X3Q_W12 ? 3 : 5;          // taps per wave (max)
+constexpr int X3Q_NTMAX = 5;                             // taps per wave (max)
 
 // LDS-DMA of unit uu's input image (rows 4t .. 4t + 5 of both planes of the sample's act16 image)
 __device__ __forceinline__ void x3q_issue_img(const uint16_t* act16, int uu, int wave, int lane, uint32_t lds) {
@@ -1570,7 +1566,7 @@ __global__ __launch_bounds__(X3Q_THREADS, 1) void conv2_wgrad_x3q_kernel(
 
     auto unit_mfma = [&](const char* img, auto TG) {
         constexpr int TGV = decltype(TG)::value;
-        constexpr int T0 = SLK_X3Q_W12 ? 3 * TGV : (TGV ? 5 : 0), NT = SLK_X3Q_W12 ? 3 : (TGV ? 4 : 5);
+        constexpr int T0 = TGV ? 5 : 0, NT = TGV ? 4 : 5;
         constexpr int N = 3 * NT;
         f16x8 Ah[2][2], Al[2][2], Bh[3], Bl[3];
         auto rdA = [&](int j, int slot) {
@@ -1646,8 +1642,7 @@ __global__ __launch_bounds__(X3Q_THREADS, 1) void conv2_wgrad_x3q_kernel(
         if (dfirst && dstage) load_dy(min(nx2, u1 - 1));
         X3Q_TS(k, 1);
         if (tg == 0) unit_mfma(img, std::integral_constant<int, 0>{});
-        else if (!SLK_X3Q_W12 || tg == 1) unit_mfma(img, std::integral_constant<int, 1>{});
-        else if constexpr (SLK_X3Q_W12 != 0) unit_mfma(img, std::integral_constant<int, 2>{});
+        else unit_mfma(img, std::integral_constant<int, 1>{});
         X3Q_TS(k, 2);
         if (!dfirst && dstage) {
             store_dy(nimg, nx < u1);
@@ -1673,7 +1668,7 @@ __global__ __launch_bounds__(X3Q_THREADS, 1) void conv2_wgrad_x3q_kernel(
     }
     const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
     const int ci = 16 * h + (lane & 15);
-    const int nt = SLK_X3Q_W12 ? 3 : (tg ? 4 : 5), tap0 = SLK_X3Q_W12 ? 3 * tg : 5 * tg;
+    const int nt = tg ? 4 : 5, tap0 = 5 * tg;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
 #pragma unroll
