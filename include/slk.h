@@ -183,6 +183,11 @@ int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float*
                            uint8_t* code, uint16_t* act16, int B, void* stream);
 int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled, const float* dp_amax,
                         const uint8_t* code, float* slabs, int B, void* stream);
+/* slk_conv2_fwd_pool_x3s with the per-sample max |act| computed inside the forward (written to act_amax,
+ * the values slk_row_amax gives) instead of read: the drop-in module path has no separate pass over the cut.
+ * act 16-byte aligned. Replaces the row_amax + forward pair behind ModelPartB.forward (src/model_def.py:25-26). */
+int slk_conv2_fwd_pool_x3sa(const float* act, float* act_amax, const float* W2, const float* b2, float* pooled,
+                            uint8_t* code, uint16_t* act16, int B, void* stream);
 /* act16 layout: per sample an h plane then an l plane, each [26 x 26 pixels][32 ci] f16 with 64-B pixels
  * (8-channel chunk c8 at slot c8 ^ (x & 2)): B x 86,528 bytes. */
 int64_t slk_conv2_act16_bytes(int B);

@@ -64,6 +64,16 @@ __device__ __forceinline__ f32x4 mfma_x3(const f16x8& ah, const f16x8& al, const
     return mfma_f16(al, bh, c);
 }
 
+// max over the wave: within 16-lane rows by DPP, then across rows (2 LDS-path shuffles instead of 6)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));   // quad_perm 1,0,3,2
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));   // quad_perm 2,3,0,1
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+
 }  // namespace
 
 // ============================================================================ per-row max |x|
@@ -131,6 +141,17 @@ constexpr int X3F_IPT = (X3F_ITEMS + X3F_THREADS - 1) / X3F_THREADS;  // 3
 constexpr int X3F_GRID = 256;
 constexpr int X3F_STORES = 2 * X3F_NT;            // epilogue global stores per wave and unit (x3f_store_row)
 static_assert(X3F_RAW % 1024 == 512, "the last DMA wave-instruction is a half piece");
+// AMX (f32 rows in, the drop-in module path): the kernel computes each sample's max |act| itself instead of a
+// separate row_amax pass over the cut. A sample's 5,408 16-B pieces are read in 3 contiguous chunks by
+// LDS-DMA into one chunk buffer — chunk j of sample b in unit 3b - 5 + j, at the wave's split point;
+// folded into a per-lane running max in the next unit (its top wait has retired the DMA) by the lanes that
+// DMA'd it; reduced across the waves through red_amx in unit 3b - 1, just before its split of unit 3b,
+// the sample's first use of its scale. The chunk reads add the cut's bytes once more to the kernel's
+// traffic: 0.257 -> 0.306 ms at B = 4096, against a 0.06-0.09 ms row_amax pass it replaces.
+constexpr int X3F_SP16 = A_SAMPLE * 4 / 16;                        // 5,408 pieces per sample
+constexpr int X3F_CP = (X3F_SP16 + 2) / 3;                         // 1,803 pieces per chunk
+constexpr int X3F_CI = (X3F_CP + 63) / 64;                         // 29 wave-instructions per chunk
+constexpr int X3F_CIW = (X3F_CI + X3F_WAVES - 1) / X3F_WAVES;      // per wave (max)
 // act16 images in HBM: per SAMPLE, the whole 26 x 26 cut as an h plane then an l plane ([pixel][32 ci]
 // f16, 64-B pixels, chunk slot c8 ^ (x & 2)), 86,528 B a sample: a unit (sample, third t3) is rows
 // 8 t3 .. 8 t3 + 9 of each plane — two contiguous 16,640-B runs — so no row is stored twice
@@ -221,14 +242,20 @@ __device__ __forceinline__ void x3f_store_row(float m0, float m1, float m2, uint
 // to the per-sample act16 image (X3S_*) for conv2_wgrad_x3's input operand.
 // IN16 = true: the input IS such an image array (slk_conv1_fwd_x3 wrote it): each unit's image is moved
 // by LDS-DMA two units ahead into a 3-deep ring of f16 buffers — no f32 rows, no split.
-template <bool IN16>
+// AMX = true (IN16 false, act16 required): amax is not read; the per-sample max |act| is computed here
+// (layout above X3F_SP16) and written to amax_out.
+template <bool IN16, bool AMX = false>
 __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     const float* __restrict__ act, const float* __restrict__ amax, const float* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ pooled, uint8_t* __restrict__ code, int B,
-    uint16_t* __restrict__ act16 = nullptr) {
+    uint16_t* __restrict__ act16 = nullptr, float* __restrict__ amax_out = nullptr) {
     static_assert(3 * X3F_BUF <= 2 * X3F_BUF + 2 * X3F_RAW, "IN16 ring fits");
-    __shared__ __attribute__((aligned(1024))) char smem[2 * X3F_BUF + 2 * X3F_RAW];
+    static_assert(!(IN16 && AMX), "AMX reads f32 rows");
+    constexpr int SMEM = 2 * X3F_BUF + 2 * X3F_RAW + (AMX ? X3F_CI * 1024 : 0);
+    static_assert(SMEM + 64 <= 163840, "LDS");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
     __shared__ float red[X3F_WAVES];
+    __shared__ float red_amx[X3F_WAVES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ch = wave & 1, wr = wave >> 1;
@@ -238,10 +265,45 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     const int U = 3 * B;
     const int G = gridDim.x;
     // a contiguous range of units per workgroup: the three thirds of a sample run back to back on one
-    // CU, so the 2 halo rows each shares with the next come from that XCD's L2, not HBM
-    const int per = (U + G - 1) / G;
+    // CU, so the 2 halo rows each shares with the next come from that XCD's L2, not HBM (AMX: whole
+    // samples per workgroup)
+    const int per = AMX ? 3 * ((B + G - 1) / G) : (U + G - 1) / G;
     const int u0 = min((int)blockIdx.x * per, U), u1 = min(u0 + per, U);
     int u = u0;
+    // AMX state: the running max of the sample being read (per lane), the current unit's sample max and
+    // the next sample's (wave-uniform)
+    float run = 0.f, am_cur = 0.f, am_nxt = 0.f;
+    char* const cbuf = smem + 2 * X3F_BUF + 2 * X3F_RAW;
+    auto amx_chunk = [&](int v, int& sb, int& lim) {  // unit v reads chunk (v + 2) % 3 of sample (v + 5) / 3
+        sb = __builtin_amdgcn_readfirstlane((v + 5) / 3);
+        const int j = __builtin_amdgcn_readfirstlane((v + 2) - 3 * ((v + 2) / 3));
+        lim = j == 2 ? X3F_SP16 - 2 * X3F_CP : X3F_CP;
+        return reinterpret_cast<const char*>(act + (size_t)sb * A_SAMPLE) + j * X3F_CP * 16;
+    };
+    auto amx_issue = [&](int v) {
+        int sb, lim;
+        const char* src = amx_chunk(v, sb, lim);
+        if (3 * sb >= u1) return;
+        const uint32_t dst = lds_u32(cbuf);
+#pragma unroll
+        for (int r = 0; r < X3F_CIW; ++r) {
+            const int i = wave + X3F_WAVES * r, q = 64 * i + lane;
+            if (i < X3F_CI && q < lim) glds16_so(src, (uint32_t)(q * 16), dst + i * 1024);
+        }
+    };
+    auto amx_fold = [&](int v) {  // at the top of unit v + 1, after its barrier: unit v's chunk has landed
+        int sb, lim;
+        amx_chunk(v, sb, lim);
+        if (3 * sb >= u1) return;
+#pragma unroll
+        for (int r = 0; r < X3F_CIW; ++r) {
+            const int i = wave + X3F_WAVES * r, q = 64 * i + lane;
+            if (i < X3F_CI && q < lim) {
+                const float4 v4 = *reinterpret_cast<const float4*>(cbuf + i * 1024 + lane * 16);
+                run = fmaxf(run, fmaxf(fmaxf(fabsf(v4.x), fabsf(v4.y)), fmaxf(fabsf(v4.z), fabsf(v4.w))));
+            }
+        }
+    };
     // DMA source offsets (bytes within a unit): piece g = 64k' + lane -> channel g / 65, 16-B run g % 65
     uint32_t voff[X3F_WPIECES];
 #pragma unroll
@@ -259,6 +321,31 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         if (u < u1) x3f_issue_raw(act, u, wave, lane, voff, lds_u32(raw0));
         if (u + 1 < u1) x3f_issue_raw(act, u + 1, wave, lane, voff, lds_u32(raw0 + X3F_RAW));
     }
+    if constexpr (AMX) {  // sample u0 / 3 whole and chunks 0-1 of the next one, by plain loads
+        float m0 = 0.f;
+        if (u0 < u1) {
+            // all loads in flight at once (11 + 8 per lane), then the maxima
+            const float4* s4 = reinterpret_cast<const float4*>(act + (size_t)(u0 / 3) * A_SAMPLE);
+            constexpr int NS = (X3F_SP16 + X3F_THREADS - 1) / X3F_THREADS;
+            constexpr int NC = (2 * X3F_CP + X3F_THREADS - 1) / X3F_THREADS;
+            const bool nxt = u0 + 3 < u1;
+            float4 v4[NS + NC];
+#pragma unroll
+            for (int r = 0; r < NS + NC; ++r) {
+                const int i = tid + X3F_THREADS * (r < NS ? r : r - NS);
+                const bool ok = r < NS ? i < X3F_SP16 : (nxt && i < 2 * X3F_CP);
+                v4[r] = ok ? s4[(r < NS ? 0 : X3F_SP16) + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int r = 0; r < NS + NC; ++r) {
+                const float m = fmaxf(fmaxf(fabsf(v4[r].x), fabsf(v4[r].y)), fmaxf(fabsf(v4[r].z), fabsf(v4[r].w)));
+                if (r < NS) m0 = fmaxf(m0, m);
+                else run = fmaxf(run, m);
+            }
+        }
+        m0 = wave_max(m0);
+        if (lane == 0) red_amx[wave] = m0;
+    }
 
     // weight scale: max |W2| over the whole tensor
     float wm = 0.f;
@@ -271,8 +358,38 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
     for (int i = 1; i < X3F_WAVES; ++i) wm = fmaxf(wm, red[i]);
     const int sw = x3_exp(wm);
     const float wsc = ldexpf(1.f, sw);
-    // data scale: per sample
-    auto sexp = [&](int b) { return x3_exp(amax[b]); };
+    auto red_amx_max = [&]() {
+        float m = red_amx[0];
+#pragma unroll
+        for (int i = 1; i < X3F_WAVES; ++i) m = fmaxf(m, red_amx[i]);
+        return m;
+    };
+    if constexpr (AMX) {
+        am_cur = red_amx_max();
+        if (tid == 0 && u0 < u1) amax_out[u0 / 3] = am_cur;
+    }
+    // AMX, once per unit at the wave's split point (before the split; at the unit's top instead — after the
+    // barrier, before the MFMA stream — the LDS latencies were on the critical path: 0.328 vs 0.306 ms):
+    // the next sample's max from the partials, the fold of the chunk unit u - 1 read (its DMA retired by
+    // this unit's top wait), this wave's partial after a sample's last chunk, the DMA of this unit's chunk
+    auto amx_step = [&](int r3) {
+        if (r3 == 2) {  // the next sample's partials (written by unit u - 1, a barrier ago)
+            am_nxt = red_amx_max();
+            if (tid == 0 && u + 1 < u1) amax_out[u / 3 + 1] = am_nxt;
+        }
+        if (u > u0) amx_fold(u - 1);
+        if (r3 == 1) {  // unit u - 1 read the next sample's last chunk: this wave's partial
+            const float m = wave_max_dpp(run);
+            if (lane == 0) red_amx[wave] = m;
+            run = 0.f;
+        }
+        amx_issue(u);
+    };
+    // data scale: per sample (AMX: sample b is the current unit's or the next one)
+    auto sexp = [&](int b) {
+        if constexpr (AMX) return x3_exp(b == u / 3 ? am_cur : am_nxt);
+        else return x3_exp(amax[b]);
+    };
 
     // B fragments: lane (n16, kc) holds W2[co][8kc .. 8kc+7][tap], co = 16nt + n16
     f16x8 wh[X3F_NT][9], wl[X3F_NT][9];
@@ -365,6 +482,10 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X3F_STORES) : "memory");
         __syncthreads();
         const int kr = k % 3;  // IN16 ring slot of unit u
+        if constexpr (AMX) {
+            if (u - 3 * (u / 3) == 0 && u > u0) am_cur = am_nxt;
+
+        }
         // IN16: unit u+2's image (past the range: a clamped unit into the free slot, never read) — the
         // quarters now, the 4 full pieces of each wave spread over the first MFMA steps (one burst here
         // measured 0.2456 vs 0.2336 ms, interleaved A/B)
@@ -452,6 +573,9 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
             // staging after M tile 0 on waves 4-7 and after M tile 1 on waves 0-3 (waves w and w + 4
             // share a SIMD; measured: 0/1 beats 0/0 and 0/2). Past the last unit this splits a clamped
             // unit's stale raw rows into a buffer nobody reads
+            if constexpr (AMX) {
+                if (mt == sph) amx_step(u - 3 * (u / 3));
+            }
             if (!IN16 && mt == sph) split_unit(min(u + 1, u1 - 1), raw0 + (cb ^ 1) * X3F_RAW, smem + (cb ^ 1) * X3F_BUF);
             if (!IN16 && mt == sph && act16) {
                 // this unit's f16 image -> HBM for the wgrad (2,080 16-B pieces)
@@ -1865,6 +1989,17 @@ extern "C" int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, c
     const int U = 3 * B;
     hipLaunchKernelGGL(conv2_fwd_pool_x3_kernel<false>, dim3(U < X3F_GRID ? U : X3F_GRID), dim3(X3F_THREADS), 0,
                        slk_stream(stream), act, act_amax, W2, b2, pooled, code, B, act16);
+    return slk_launch_status();
+}
+// the same with the per-sample max |act| computed in the kernel (written to act_amax) instead of read
+extern "C" int slk_conv2_fwd_pool_x3sa(const float* act, float* act_amax, const float* W2, const float* b2,
+                                       float* pooled, uint8_t* code, uint16_t* act16, int B, void* stream) {
+    SLK_CHECK_ARG(B >= 0 && act && act_amax && W2 && b2 && pooled && code && act16);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG((reinterpret_cast<size_t>(act) & 15) == 0);
+    const int G = B < X3F_GRID ? B : X3F_GRID;
+    hipLaunchKernelGGL((conv2_fwd_pool_x3_kernel<false, true>), dim3(G), dim3(X3F_THREADS), 0, slk_stream(stream),
+                       act, nullptr, W2, b2, pooled, code, B, act16, act_amax);
     return slk_launch_status();
 }
 extern "C" int64_t slk_conv2_act16_bytes(int B) { return B > 0 ? (int64_t)B * X3S_SAMPLE : 0; }

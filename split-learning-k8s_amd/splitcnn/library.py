@@ -149,8 +149,14 @@ def conv2_relu_pool(act: Tensor, W2: Tensor, b2: Tensor) -> Tuple[Tensor, Tensor
     if fi != "x3":
         pooled, code = ops.conv2_fwd_pool(act, W2.contiguous(), b2.contiguous(), impl=fi)
         return pooled, code, act.new_empty((0,)), act.new_empty((0,), dtype=torch.uint8)
-    amax = ops.row_amax(act)
     a16 = act.new_empty((ops.conv2_act16_bytes(B) if wi == "x3" else 0,), dtype=torch.uint8)
+    if wi == "x3" and act.data_ptr() % 16 == 0:
+        # the forward computes the per-sample max itself (no separate 354 MB pass at B = 4096)
+        amax = act.new_empty((B,))
+        pooled, code = ops.conv2_fwd_pool(act, W2.contiguous(), b2.contiguous(), impl="x3", act16=a16,
+                                          act_amax_out=amax)
+        return pooled, code, amax, a16
+    amax = ops.row_amax(act)
     pooled, code = ops.conv2_fwd_pool(act, W2.contiguous(), b2.contiguous(), impl="x3", act_amax=amax,
                                       act16=a16 if wi == "x3" else None)
     return pooled, code, amax, a16

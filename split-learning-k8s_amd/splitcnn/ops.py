@@ -174,16 +174,27 @@ def _act16(t, B):
     return t.data_ptr()
 
 
-def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None, act16=None):
+def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None, act16=None,
+                   act_amax_out=None):
     """impl: 'wino' (Winograd F(2x2,3x3) on the f32 MFMA, default), 'direct' (direct f32 MFMA kernel,
     cross-check; also direct=True) or 'x3' (direct on the f16 MFMA with split operands; act_amax =
     per-sample max |act|, computed here when not given). act16 (x3 only, a uint8 tensor of
-    conv2_act16_bytes(B)): also write the split input images for conv2_wgrad_slabs(act16=...)."""
+    conv2_act16_bytes(B)): also write the split input images for conv2_wgrad_slabs(act16=...).
+    act_amax_out (x3 with act16, act_amax not given; a float tensor [B]): the forward kernel computes the
+    per-sample max itself and writes it there (slk_conv2_fwd_pool_x3sa: no separate pass over act; the
+    same values as row_amax, so the same outputs bitwise)."""
     impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
     pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
     code = _out(code, (B, 64, 12, 12), act, torch.uint8, "code")
     if impl == "x3":
+        if act_amax_out is not None:
+            if act_amax is not None or act16 is None:
+                raise ValueError("act_amax_out needs act16 and no act_amax")
+            _lib.call("slk_conv2_fwd_pool_x3sa", _dev(act, "act"), _dev(act_amax_out, "act_amax_out", (B,)),
+                      _dev(W2, "conv2.weight", (64, 32, 3, 3)), _dev(b2, "conv2.bias", (64,)), _dev(pooled, "pooled"),
+                      _dev(code, "code", dtype=torch.uint8), _act16(act16, B), B, _stream(act))
+            return pooled, code
         if act_amax is None:
             act_amax = row_amax(act)
         if act16 is not None:

@@ -234,6 +234,33 @@ def test_x3_wgrad_from_forward_images_bitwise(gpu, B):
     assert rel_err(ps.cpu().numpy(), r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))) <= 1e-5
 
 
+@pytest.mark.parametrize("B", [1, 2, 4, 300, 513, 4096])
+def test_x3_fwd_with_in_kernel_amax_bitwise(gpu, B):
+    """slk_conv2_fwd_pool_x3sa (the drop-in module forward: the per-sample max |act| computed inside the
+    forward, whole samples per workgroup, chunks of the next sample read ahead) == row_amax + the x3
+    forward writing act16: amax, pooled, code and every act16 byte. B = 1, 2, 4: one sample per
+    workgroup (no read-ahead); 300, 513: ragged ranges (2-3 samples on some workgroups, none on others);
+    4096: 16 samples per workgroup. One sample carries a NaN (ignored by both maxima) and one is zero."""
+    from splitcnn import ops
+    act, p, _ = _inputs(gpu, B, seed=B + 77)
+    act[B // 2] *= 2.0 ** -20
+    if B > 2:
+        act[1] = 0.0
+        act[2, 5, 3, 4] = float("nan")
+    am = ops.row_amax(act)
+    nb = ops.conv2_act16_bytes(B)
+    i0 = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    p0, c0 = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=am, act16=i0)
+    am1 = torch.full((B,), -1.0, device=gpu)
+    i1 = torch.full((nb,), 0x5A, dtype=torch.uint8, device=gpu)
+    p1, c1 = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act16=i1, act_amax_out=am1)
+    torch.cuda.synchronize()
+    assert torch.equal(am1, am)
+    assert torch.equal(c1, c0)
+    assert torch.equal(p1.view(torch.int32), p0.view(torch.int32))
+    assert torch.equal(i1, i0)
+
+
 @pytest.mark.parametrize("B", [1, 6, 257])
 def test_conv1_x3_images_and_forward_from_images_bitwise(gpu, B):
     """slk_conv1_fwd_x3 writes the same f32 act and act_amax as conv1_fwd(act_amax=...), and the same

@@ -76,6 +76,13 @@ def main():
             L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
             cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
                 p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+        if "fwdsa" in args.ops and hasattr(L, "slk_conv2_fwd_pool_x3sa"):
+            po3, co3, a16s, ams = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16), torch.empty_like(amax)
+            L.slk_conv2_fwd_pool_x3sa.restype = ctypes.c_int
+            L.slk_conv2_fwd_pool_x3sa.argtypes = [P] * 7 + [ctypes.c_int, P]
+            cases[f"fwdsa {tag}"] = (lambda L=L, po=po3, co=co3, a16o=a16s, ams=ams: L.slk_conv2_fwd_pool_x3sa(
+                p(act), p(ams), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+            outs[f"fwdsa {tag}"] = po3
         if "fwdi" in args.ops:
             po2, co2 = torch.empty_like(pooled), torch.empty_like(code)
             L.slk_conv2_fwd_pool_x3i.restype = ctypes.c_int
