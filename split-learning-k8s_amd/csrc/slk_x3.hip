@@ -653,12 +653,6 @@ static_assert(2 * X3D_IMG <= 163840, "LDS");
 #ifndef SLK_X3D_TRACE
 #define SLK_X3D_TRACE 0
 #endif
-#ifndef SLK_X3D_PROBE
-#define SLK_X3D_PROBE 0
-#endif
-#ifndef SLK_X3D_XBLATE
-#define SLK_X3D_XBLATE 0
-#endif
 #if SLK_X3D_TRACE
 // profiling probe: per (workgroup, wave, unit) shader-clock stamps of the dgrad's phases (lane 0, vector stores)
 __device__ unsigned long long g_x3d_trace[256 * 8 * 128 * 8];
@@ -800,30 +794,14 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 dcb[r][j] = CODE_NONE;  // routes nothing
             }
             if (i < nwr * P_HW * 8 && wr >= 0 && wr < P_HW) {
-#if SLK_X3D_PROBE == 1
-                // timing probe (wrong data): lanes read consecutive windows of one co plane (coalesced)
-                const size_t o = (size_t)b * P_SAMPLE + (32 * h) * P_WIN + (i & 127);
-#else
                 const size_t o = (size_t)b * P_SAMPLE + (32 * h + 4 * c4) * P_WIN + wr * P_HW + wx;
-#endif
                 // code bytes stay one per register until store_dy: combining them here made the
                 // compiler wait for the loads on the spot (a full memory latency per unit)
-#if SLK_X3D_PROBE == 3
-                // timing probe (wrong data): one value + one code load per item
-                dv[r][0] = dpooled[o];
-                dcb[r][0] = code[o];
-#pragma unroll
-                for (int j = 1; j < 4; ++j) {
-                    dv[r][j] = dv[r][0];
-                    dcb[r][j] = dcb[r][0];
-                }
-#else
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     dv[r][j] = dpooled[o + j * P_WIN];
                     dcb[r][j] = code[o + j * P_WIN];
                 }
-#endif
             }
         }
     };
@@ -840,17 +818,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 uint32_t hv[2], lv[2];
 #pragma unroll
                 for (int j = 0; j < 4; j += 2) {
-#if SLK_X3D_PROBE == 2
-                    // timing probe (wrong data): no scale / split
-                    hv[j / 2] = __float_as_uint(dv[r][j]);
-                    lv[j / 2] = __float_as_uint(dv[r][j + 1]);
-#else
                     const float a = dv[r][j] * sc, c = dv[r][j + 1] * sc;
                     const _Float16 ha = (_Float16)a, hc = (_Float16)c;
                     const _Float16 la = (_Float16)(a - (float)ha), lc = (_Float16)(c - (float)hc);
                     hv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{ha, hc});
                     lv[j / 2] = __builtin_bit_cast(uint32_t, f16x2{la, lc});
-#endif
                 }
                 const uint32_t dcw = dcb[r][0] | (dcb[r][1] << 8) | (dcb[r][2] << 16) | (dcb[r][3] << 24);
                 const uint32_t cA = __builtin_amdgcn_perm(0u, dcw, 0x01010000u), cB = __builtin_amdgcn_perm(0u, dcw, 0x03030202u);
@@ -860,16 +832,8 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     const uint32_t T = 0xFFu << (8 * pos);
                     const uint32_t mA = __builtin_amdgcn_perm(0u, T, cA), mB = __builtin_amdgcn_perm(0u, T, cB);
                     char* o = rec + ((pos >> 1) * A_HW + (pos & 1)) * X3D_REC;
-#if SLK_X3D_PROBE == 4
-                    // timing probe (wrong data): no routing masks
-                    (void)mA;
-                    (void)mB;
-                    *reinterpret_cast<uint2*>(o) = make_uint2(hv[0], hv[1]);
-                    *reinterpret_cast<uint2*>(o + 64) = make_uint2(lv[0], lv[1]);
-#else
                     *reinterpret_cast<uint2*>(o) = make_uint2(hv[0] & mA, hv[1] & mB);
                     *reinterpret_cast<uint2*>(o + 64) = make_uint2(lv[0] & mA, lv[1] & mB);
-#endif
                 }
             }
         }
@@ -1040,7 +1004,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // staging-first waves issue it after their staging: hipcc cannot see the asm DMA, and its vmcnt(0)
             // for the dY registers would wait for the DMA just issued (a full memory latency per pair)
             const bool sfirst = wave >= 4;
-            if (C1W && h == 0 && !(SLK_X3D_XBLATE && sfirst)) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
+            if (C1W && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             if (pack && h == 0) issue_pk(min(pr + 1, p1 - 1), (q + 1) & 1);
             const char* img = smem + (k & 1) * X3D_IMG;
             char* nimg = smem + ((k & 1) ^ 1) * X3D_IMG;
@@ -1060,7 +1024,6 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             if (sfirst) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
-                if (C1W && SLK_X3D_XBLATE && h == 0) issue_xb(min(pr + 1, p1 - 1), (q + 1) & 1);
             }
             X3D_TS(k, 1);
             f16x8 fh[4], fl[4];
