@@ -61,6 +61,42 @@ def test_unpack_into_images_matches_the_client_images(gpu, B):
     assert torch.equal(img, ref)
 
 
+@pytest.mark.parametrize("aligned", [True, False])
+def test_unpack_dense_samples_and_unaligned_values(gpu, aligned):
+    """Samples denser than the unpack's LDS stage (every element set: 21,632 values against 12,288 staged;
+    the rest gathered from HBM), a sparse one, an all-zero one; and a value array that is not 16-B aligned
+    (staging off: every value gathered from HBM). Images == the dense path's, bitwise."""
+    from splitcnn import ops
+    from splitcnn.codec import CutCodec
+    B = 5
+    *_, act, _ = _cut(gpu, B, seed=11)
+    act[0] = act[0].abs() + 0.5          # every element set
+    act[2] = act[2].abs() + 1e-3
+    act[3] = 0.0                          # nothing set
+    act[4] = torch.where(act[4] > 2 * act[4].mean(), act[4], torch.zeros_like(act[4]))
+    amx = ops.row_amax(act)
+    ref = torch.empty(ops.conv2_act16_bytes(B), dtype=torch.uint8, device=gpu)
+    # the dense x3 forward writes the images from the f32 cut at the same scales
+    W2 = torch.randn(64, 32, 3, 3, device=gpu) * 0.05
+    b2 = torch.zeros(64, device=gpu)
+    ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amx, act16=ref)
+    n = act.numel()
+    c = CutCodec()
+    bk = c.buffers("t", n, gpu)
+    c.encode(act, bk)
+    rk = c.ranks("t", n, bk)
+    vals = bk[4]
+    if not aligned:
+        buf = torch.empty(n + 1, device=gpu)
+        buf[1:].copy_(vals)
+        vals = buf[1:]
+        assert vals.data_ptr() % 16 != 0
+    img = torch.full_like(ref, 0x3C)
+    ops.cut_unpack_x3(vals, bk[0], rk, amx, img)
+    torch.cuda.synchronize()
+    assert torch.equal(img, ref)
+
+
 @pytest.mark.parametrize("B", [2, 48])
 def test_packed_dgrad_matches_pack_of_dense_dgrad(gpu, B):
     """conv2_dgrad_x3_pack == CutCodec.pack(conv2_dgrad(..., impl='x3')) at the cut's set positions."""

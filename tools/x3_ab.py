@@ -44,6 +44,14 @@ def main():
     ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amax, act16=a16)
     P = ctypes.c_void_p
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    if "unp" in args.ops.split(","):  # the codec's packed form of act (mask, values, word ranks)
+        from splitcnn.codec import CutCodec
+        cc = CutCodec()
+        nel = act.numel()
+        cbk = cc.buffers("ab", nel, dev)
+        cc.encode(act, cbk)
+        crk = cc.ranks("ab", nel, cbk)
+        print("unp: set fraction", round(int(cbk[3].item()) / nel, 4), flush=True)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     cases = {}
     outs = {}  # case -> output tensor (compared across libraries after the timing)
@@ -76,6 +84,12 @@ def main():
             L.slk_conv2_fwd_pool_x3s.argtypes = [P] * 7 + [ctypes.c_int, P]
             cases[f"fwd {tag}"] = (lambda L=L, po=po, co=co, a16o=a16o: L.slk_conv2_fwd_pool_x3s(
                 p(act), p(amax), p(W2), p(b2), p(po), p(co), p(a16o), B, st))
+        if "unp" in args.ops.split(","):
+            L.slk_cut_unpack_x3.restype = ctypes.c_int
+            L.slk_cut_unpack_x3.argtypes = [P] * 4 + [ctypes.c_int, P, P]
+            iu = torch.empty_like(a16)
+            cases[f"unp {tag}"] = (lambda L=L, iu=iu: L.slk_cut_unpack_x3(p(cbk[4]), p(cbk[0]), p(crk), p(amax), B, p(iu), st))
+            outs[f"unp {tag}"] = iu
         if "fwdsa" in args.ops and hasattr(L, "slk_conv2_fwd_pool_x3sa"):
             po3, co3, a16s, ams = torch.empty_like(pooled), torch.empty_like(code), torch.empty_like(a16), torch.empty_like(amax)
             L.slk_conv2_fwd_pool_x3sa.restype = ctypes.c_int
