@@ -995,9 +995,12 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         for (int i = 0; i < X3D_MPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int h = 0; h < 2; ++h, ++k) {
-            // C1W: this pair's x / bits DMA (issued during the previous pair) retired before the barrier
+            // C1W: this pair's x / bits DMA (issued during the previous pair) retired before the barrier.
+            // PACK: the next pair's words (issued at this pair's top) retired at its second unit's top, so
+            // the previous epilogue's scattered stores drain during the first unit instead of being waited
+            // for here (0.322 -> 0.305 ms at B = 4096, x3_ab dgp; the dense dgrad 0.255)
             X3D_TS(k, 6);
-            if ((C1W || pack) && h == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((C1W && h == 0) || (pack && h == 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // image k&1 complete; image (k+1)&1 free
             X3D_TS(k, 0);
             // C1W: the next pair's x / bits into the other buffer (last read by the previous epilogue). The
@@ -1080,7 +1083,9 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             X3D_TS(k - 1, 5);
         } else if (pack) {
             // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4);
-            // the word and its rank come from this pair's LDS copy (issue_pk, one pair ahead)
+            // the word and its rank come from this pair's LDS copy (issue_pk, one pair ahead). (Tried: the
+            // pair's runs assembled in LDS and written by coalesced stores at the next pair's top, 0.335 vs
+            // 0.312 ms: the LDS round trip cost more than the scattered 4-B stores it replaced.)
             const uint32_t* mk;
             const int* rk;
             float* pvals_;

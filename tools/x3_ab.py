@@ -44,7 +44,7 @@ def main():
     ops.conv2_fwd_pool(act, W2, b2, impl="x3", act_amax=amax, act16=a16)
     P = ctypes.c_void_p
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    if "unp" in args.ops.split(","):  # the codec's packed form of act (mask, values, word ranks)
+    if "unp" in args.ops.split(",") or "dgp" in args.ops.split(","):  # the codec's packed form of act (mask, values, word ranks)
         from splitcnn.codec import CutCodec
         cc = CutCodec()
         nel = act.numel()
@@ -109,6 +109,13 @@ def main():
             L.slk_conv2_dgrad_x3.argtypes = [P] * 5 + [ctypes.c_int, P]
             cases[f"dgrad {tag}"] = (lambda L=L, g=g: L.slk_conv2_dgrad_x3(p(dp), p(dpa), p(code), p(W2), p(g), B, st))
             outs[f"dgrad {tag}"] = g
+        if "dgp" in args.ops.split(",") and hasattr(L, "slk_conv2_dgrad_x3_pack"):
+            gv = torch.empty(act.numel(), device=dev)
+            L.slk_conv2_dgrad_x3_pack.restype = ctypes.c_int
+            L.slk_conv2_dgrad_x3_pack.argtypes = [P] * 7 + [ctypes.c_int, P]
+            cases[f"dgp {tag}"] = (lambda L=L, gv=gv: L.slk_conv2_dgrad_x3_pack(
+                p(dp), p(dpa), p(code), p(W2), p(cbk[0]), p(crk), p(gv), B, st))
+            outs[f"dgp {tag}"] = gv
         if "dgc1" in args.ops:
             sl1 = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
             L.slk_conv2_dgrad_x3_c1w.restype = ctypes.c_int
