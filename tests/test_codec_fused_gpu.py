@@ -63,9 +63,8 @@ def test_unpack_into_images_matches_the_client_images(gpu, B):
 
 @pytest.mark.parametrize("aligned", [True, False])
 def test_unpack_dense_samples_and_unaligned_values(gpu, aligned):
-    """Samples denser than the unpack's LDS stage (every element set: 21,632 values against 12,288 staged;
-    the rest gathered from HBM), a sparse one, an all-zero one; and a value array that is not 16-B aligned
-    (staging off: every value gathered from HBM). Images == the dense path's, bitwise."""
+    """A fully dense sample (21,632 values), a sparse one, an all-zero one; and a value array that is not
+    16-B aligned. Images == the dense path's, bitwise."""
     from splitcnn import ops
     from splitcnn.codec import CutCodec
     B = 5
