@@ -185,6 +185,8 @@ def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None,
     same values as row_amax, so the same outputs bitwise)."""
     impl = _impl(direct, impl)
     B = batch_of(act, (32, 26, 26), "act")
+    if act_amax_out is not None and impl != "x3":
+        raise ValueError("act_amax_out is an output of the x3 forward only")
     pooled = _out(pooled, (B, 64, 12, 12), act, name="pooled")
     code = _out(code, (B, 64, 12, 12), act, torch.uint8, "code")
     if impl == "x3":
