@@ -482,3 +482,33 @@ def test_dropin_fused_byproducts_bitwise_vs_recomputed(gpu, monkeypatch, B):
     want = run(False)
     for a, b in zip(got, want):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [3, 300])
+def test_dropin_server_unaligned_cut_bitwise(gpu, B):
+    """ModelPartB on a cut whose storage is not 16-byte aligned takes the row_amax + x3 forward path
+    instead of the forward that computes its scales in-kernel (slk_conv2_fwd_pool_x3sa needs 16-B rows):
+    the same logits, loss and every gradient bit for bit."""
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.model_def import CrossEntropyLoss
+    x, y = SyntheticMNIST(33).batch(B)
+    x, y = x.to(gpu), y.to(gpu)
+    client, _ = (m.to(gpu) for m in init_models(seed=3))
+    act = client(x).detach()
+    buf = torch.empty(act.numel() + 1, device=gpu)
+
+    def run(cut):
+        _, server = (m.to(gpu) for m in init_models(seed=3))
+        ca = cut.requires_grad_(True)
+        logits = server(ca)
+        loss = CrossEntropyLoss()(logits, y)
+        loss.backward()
+        return [logits.detach(), loss.detach(), ca.grad] + [p.grad for p in server.parameters()]
+
+    want = run(act.clone())
+    un = buf[1:].view(act.shape)
+    un.copy_(act)
+    assert un.data_ptr() % 16 != 0
+    got = run(un)
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
