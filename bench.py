@@ -318,6 +318,18 @@ def run_single(args, out):
                         "conv2_wgrad": ("x3_images" if tr2.client.emit_act16 else wi)}
             out["roofline"] = roofline_from(kern, B, {"conv2_fwd_pool": fi, "conv2_dgrad": di, "conv2_wgrad": wi},
                                             variants)
+            try:  # this box's sustained f16 MFMA rate: the pool's boxes differ by several per cent under load
+                from splitcnn import ops
+                box = ops.mfma_probe_tflops(dev)
+                r = out["roofline"]
+                r["box_probe"] = {"mfma_f16_dense_tflops": round(box, 1), "nominal_tflops": BF16_PEAK_TFLOPS,
+                                  "ratio": round(box / BF16_PEAK_TFLOPS, 4),
+                                  "probe": "slk_mfma_probe: 6 independent v_mfma_f32_16x16x32_f16 chains per wave, "
+                                           "2 waves per SIMD, varied operands; median of 3 launches"}
+                if r.get("unit") == "TFLOP/s" and r.get("achieved"):
+                    r["frac_of_box_probe"] = round(r["achieved"] / box, 4)
+            except Exception as e:  # reported, never fatal
+                out["roofline"]["box_probe"] = {"error": repr(e)[:200]}
             if tr2.fuse_client_backward and out["roofline"].get("kernel") == "conv2_dgrad":
                 out["roofline"]["note"] = ("conv2_dgrad here also runs the client's ReLU backward + conv1 wgrad in "
                                            "its epilogue (slk_conv2_dgrad_x3_c1w); those FLOPs are not counted, its "

@@ -186,6 +186,11 @@ int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const floa
 /* slk_conv2_fwd_pool_x3s with the per-sample max |act| computed inside the forward (written to act_amax,
  * the values slk_row_amax gives) instead of read: the drop-in module path has no separate pass over the cut.
  * act 16-byte aligned. Replaces the row_amax + forward pair behind ModelPartB.forward (src/model_def.py:25-26). */
+/* Measurement only: the device's sustained dense f16 MFMA rate (v_mfma_f32_16x16x32_f16, 6 independent chains
+ * per wave, 2 waves per SIMD, varied operands). out: slk_mfma_probe_blocks() * 256 floats; FLOPs per launch =
+ * slk_mfma_probe_blocks() * 4 * iters * 6 * 16384. bench.py prices the kernels against it beside the nominal peak. */
+int slk_mfma_probe_blocks(void);
+int slk_mfma_probe(float* out, int iters, void* stream);
 int slk_conv2_fwd_pool_x3sa(const float* act, float* act_amax, const float* W2, const float* b2, float* pooled,
                             uint8_t* code, uint16_t* act16, int B, void* stream);
 /* act16 layout: per sample an h plane then an l plane, each [26 x 26 pixels][32 ci] f16 with 64-B pixels

@@ -1945,6 +1945,47 @@ extern "C" int slk_cut_unpack_x3_parts(const uint64_t* parts, int part_b, const 
 }
 
 // ============================================================================ C-ABI
+// ============================================================================ box probe (measurement only)
+// The sustained dense f16 MFMA rate of THIS device (boxes of the pool differ by several per cent in clocks
+// under load): every wave issues 6 independent v_mfma_f32_16x16x32_f16 chains on varied nonzero operands
+// (the MFMA's power, and so the clock it sustains, depends on the data), 2 waves per SIMD on every CU.
+// bench.py reports the kernels' fractions of this next to the nominal 2.5 PF/s. FLOPs per launch:
+// blocks x 4 waves x iters x 6 x 16,384.
+__global__ __launch_bounds__(256) void mfma_probe_kernel(float* __restrict__ out, int iters) {
+    const int tid = threadIdx.x;
+    f16x8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = (_Float16)((float)((tid * 13 + j * 7 + blockIdx.x) % 97) / 97.f - 0.5f);
+        b[j] = (_Float16)((float)((tid * 29 + j * 11) % 89) / 89.f - 0.5f);
+    }
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0;
+    // the MFMAs as asm on VGPR accumulators: through the builtin, hipcc rotated the chains through
+    // AGPR <-> VGPR copies inside the loop (a probe of the copies, not of the MFMA pipe); each chain's next
+    // MFMA is 6 instructions later, far past any dependency wait
+    for (int i = 0; i < iters; ++i)
+        asm volatile(
+            "v_mfma_f32_16x16x32_f16 %0, %6, %7, %0\n\t"
+            "v_mfma_f32_16x16x32_f16 %1, %6, %7, %1\n\t"
+            "v_mfma_f32_16x16x32_f16 %2, %6, %7, %2\n\t"
+            "v_mfma_f32_16x16x32_f16 %3, %6, %7, %3\n\t"
+            "v_mfma_f32_16x16x32_f16 %4, %6, %7, %4\n\t"
+            "v_mfma_f32_16x16x32_f16 %5, %6, %7, %5"
+            : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5)
+            : "v"(a), "v"(b));
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // the last MFMAs' results settle before VALU reads them
+    const f32x4 t4 = ((c0 + c1) + (c2 + c3)) + (c4 + c5);
+    out[blockIdx.x * 256 + tid] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+}
+
+extern "C" int slk_mfma_probe_blocks() { return 2 * X3F_GRID; }  // 2 workgroups of 4 waves per CU
+
+extern "C" int slk_mfma_probe(float* out, int iters, void* stream) {
+    SLK_CHECK_ARG(out && iters > 0);
+    hipLaunchKernelGGL(mfma_probe_kernel, dim3(2 * X3F_GRID), dim3(256), 0, slk_stream(stream), out, iters);
+    return slk_launch_status();
+}
+
 extern "C" int slk_row_amax(const float* x, int rows, int n, float* amax, void* stream) {
     SLK_CHECK_ARG(rows >= 0 && n > 0 && (rows == 0 || (x && amax)));
     if (rows == 0) return 0;

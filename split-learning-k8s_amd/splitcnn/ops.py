@@ -356,6 +356,27 @@ def cut_offsets_ranks_parts(parts, n):
               _stream(parts))
 
 
+def mfma_probe_tflops(device=None, iters: int = 40000, reps: int = 3) -> float:
+    """Measurement only: this device's sustained dense f16 MFMA rate in TFLOP/s (slk_mfma_probe: 6 independent
+    v_mfma_f32_16x16x32_f16 chains per wave on varied operands, 2 waves per SIMD on every CU), median of
+    `reps` launches timed with HIP events on the current stream."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    nb = _lib.query("slk_mfma_probe_blocks")
+    out = torch.empty(nb * 256, device=dev)
+    st = torch.cuda.current_stream(dev)
+    _lib.call("slk_mfma_probe", out.data_ptr(), iters, st.cuda_stream)   # warm-up (clocks ramp)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _lib.call("slk_mfma_probe", out.data_ptr(), iters, st.cuda_stream)
+        e1.record(st)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts)[len(ts) // 2]
+    return nb * 4 * iters * 6 * 16384 / (ms * 1e-3) / 1e12
+
+
 def cut_unpack_x3(vals, mask, ranks, act_amax, act16):
     """A received codec micro-batch (mask + values + word ranks, B samples) -> the x3 input images act16
     (conv2_act16_bytes(B) uint8) at the scales act_amax: conv1_fwd_x3's images of the same cut, bit for bit."""
