@@ -43,6 +43,7 @@ SERVER_N = 110666
 # bytes per sample of the x3 split images (act16: 32 channels x 676 pixels x (hi, lo) f16) = the f32 cut's
 # 32 x 26 x 26 x 4: the image exchange moves the same bytes (ops.conv2_act16_bytes(1), checked in the GPU tests)
 IMG_BYTES = 2 * 2 * 32 * 26 * 26
+CUT_ELEMS = 32 * 26 * 26
 
 
 class _Staged:
@@ -351,8 +352,13 @@ class Hub:
         return self.rank == self.server_rank
 
     def _fused(self, codec) -> bool:
-        """Server: the codec exchange runs through the fused kernels (see fuse_codec)."""
+        """Server: the codec exchange runs through the fused kernels (see fuse_codec). Only for the
+        CutCodec itself: the fused kernels read its mask / word-rank / values layout, so a codec object
+        passed as `compress` (any other encode) always takes the unfused unpack / pack."""
         if codec is None or not (self.fuse_codec and self.ship_amax and self._amax_kw) or self.images:
+            return False
+        from .codec import CutCodec
+        if type(codec) is not CutCodec:
             return False
         st = self.stage
         takes = inspect.signature(st.compute).parameters if hasattr(st, "compute") else {}
@@ -520,10 +526,13 @@ class Hub:
         n = b * 32 * 26 * 26
         acts = self._inputs(G, device, codec)
         labels = self._buf("labels", (G,), torch.int64, device)
-        cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
+        fused = self._fused(codec)
+        self.cut_dense = not fused
+        # the fused codec path never writes a dense cut gradient (the dgrad packs it): no [G, 32, 26, 26]
+        # buffer (1 GB at K4's 28,672 samples); cuts_by_client allocates it on demand
+        cuts = None if fused else self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         parts = self._buf("loss_parts", (m,), torch.float32, device)
         ch = slice(k * CH, (k + 1) * CH)
-        fused = self._fused(codec)
         amx = self._buf("amax", (G,), torch.float32, device) if self.ship_amax else None
         if fused:
             # every client part of the chunk in ONE launch per pass (per-launch prologues x parts were most of
@@ -545,7 +554,8 @@ class Hub:
             kw["act16"] = acts[k * CH * IMG_BYTES:(k + 1) * CH * IMG_BYTES]
             if fused:
                 kw["cut_pack"] = (t_pack, b)
-            _, loss_i = s.compute(None, labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
+            _, loss_i = s.compute(None, labels[ch], 1.0 / G, accumulate=k > 0,
+                                  cut_grad=None if fused else cuts[ch], **kw)
         else:
             _, loss_i = s.compute(acts[ch], labels[ch], 1.0 / G, accumulate=k > 0, cut_grad=cuts[ch], **kw)
         _loss_sum(loss_i, 1.0 / G, parts[k:k + 1])
@@ -640,7 +650,7 @@ class Hub:
         self.cut_dense = not self._fused(codec)
         acts = self._inputs(G, device, codec)
         labels = self._buf("labels", (G,), torch.int64, device)
-        cuts = self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
+        cuts = None if not self.cut_dense else self._buf("cuts", (G, 32, 26, 26), torch.float32, device)
         amx = self._buf("amax", (G,), torch.float32, device) if ship else None
         parts = self._buf("loss_parts", (m,), torch.float32, device)
         self._prepare(B, device, codec)
@@ -689,7 +699,7 @@ class Hub:
         for w in sends:
             w.wait()
         extra = labels.numel() * 8 + (G * 4 if ship else 0)
-        self.dense_bytes = 2 * cuts.numel() * 4 + extra
+        self.dense_bytes = 2 * G * CUT_ELEMS * 4 + extra
         self.exchange_bytes = (self.dense_bytes if codec is None else
                                nc * m * 4 + sum(codec.buffers(("s", ci, k), n, device)[0].numel() * 4 + 2 * t * 4
                                                 for (ci, k), t in totals.items()) + extra)
@@ -700,8 +710,10 @@ class Hub:
         After a fused-codec step (cut_dense False) that is what went on the wire, scattered: the gradient at
         the cut's nonzero positions, zeros elsewhere (positions the client's ReLU discards)."""
         m, nc = self.micro, self.nclients
-        cuts = self._bufs["cuts"]
         if not self.cut_dense:
+            # the fused step wrote no dense buffer: scatter the packed gradient into one made here
+            dev = self._bufs["labels"].device
+            cuts = self._buf("cuts", (nc * B, 32, 26, 26), torch.float32, dev)
             b = B // m
             n = b * 32 * 26 * 26
             for k in range(m):
@@ -709,6 +721,8 @@ class Hub:
                     s0 = (k * nc + ci) * b
                     self._codec.unpack(cuts[s0:s0 + b], self._codec.buffers(("s", ci, k), n, cuts.device),
                                        vals=self._buf(("gvals", ci, k), (n,), torch.float32, cuts.device))
+        else:
+            cuts = self._bufs["cuts"]
         return cuts.view(m, nc, B // m, *cuts.shape[1:]).transpose(0, 1).reshape(nc * B, *cuts.shape[1:])
 
 

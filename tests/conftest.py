@@ -12,7 +12,7 @@ for p in (PKG, ROOT):
         sys.path.insert(0, p)
 
 FIXTURES = ["split_step_b4.npz", "split_step_b1.npz", "split_step_b12.npz", "split_step_b13.npz",
-            "split_step_ties_b2.npz"]
+            "split_step_ties_b2.npz", "split_step_b14.npz"]
 PARAMS = ["W1", "b1", "W2", "b2", "W3", "b3"]
 
 

@@ -144,11 +144,16 @@ def check_split_equals_full(md, B=64, nsteps=20):
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     md = ref_model_def()
+    if sys.argv[1:] == ["b14"]:     # add the K4-shape fixture alone (the others are unchanged)
+        fixture_steps(md, "split_step_b14.npz", B=14, nsteps=1, seed=7, data_seed=17)
+        return
     check_split_equals_full(md)
     fixture_steps(md, "split_step_b4.npz", B=4, nsteps=3, weights_at=(1,))
     fixture_steps(md, "split_step_b1.npz", B=1, nsteps=1, seed=3, data_seed=7)
     fixture_steps(md, "split_step_b12.npz", B=12, nsteps=1, seed=5, data_seed=11)  # SplitFed 3x4 concat
     fixture_steps(md, "split_step_b13.npz", B=13, nsteps=1, seed=6, data_seed=13)  # ragged batch
+    # BASELINE config 4's shape: SplitFed 7 clients x 2 samples, concatenated (round 6)
+    fixture_steps(md, "split_step_b14.npz", B=14, nsteps=1, seed=7, data_seed=17)
 
     def ties(x, s):  # all-constant images: every pooling window is a 4-way tie
         x = torch.zeros_like(x)

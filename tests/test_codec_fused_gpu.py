@@ -169,3 +169,147 @@ def test_hub_fused_codec_server_matches_unfused_bitwise(gpu):
     assert torch.equal(l0, l1)
     assert all(torch.equal(u.view(torch.int32), v.view(torch.int32)) for u, v in zip(g0, g1))
     assert torch.equal(p0, p1)
+
+
+class _LegacyCodec:
+    """A codec object with only the CutCodec interface of round 3 (buffers / encode / offsets / pack / unpack,
+    no ranks_buffer), delegating to a CutCodec: what a caller passing its own codec as `compress` has."""
+
+    def __init__(self):
+        from splitcnn.codec import CutCodec
+        self._c = CutCodec()
+
+    def buffers(self, key, n, device):
+        return self._c.buffers(key, n, device)
+
+    def encode(self, x, bufs):
+        self._c.encode(x, bufs)
+
+    def offsets(self, n, bufs):
+        self._c.offsets(n, bufs)
+
+    def pack(self, x, bufs, vals=None):
+        self._c.pack(x, bufs, vals=vals)
+
+    def unpack(self, out, bufs, vals=None):
+        self._c.unpack(out, bufs, vals=vals)
+
+
+def _hub_chunks(gpu, hub, cl, parts, B):
+    """Feed a server Hub's receive buffers as the clients' sends would (cut encode, labels, per-sample max)
+    and run its chunks; returns (loss parts, packed cut gradients per (k, ci), parameters after the step)."""
+    nc, m = hub.nclients, hub.micro
+    b, G = B // m, nc * B
+    n = b * 32 * 26 * 26
+    codec = hub._use_codec(gpu)
+    hub._prepare(B, gpu, codec)
+    labels = hub._buf("labels", (G,), torch.int64, gpu)
+    amx = hub._buf("amax", (G,), torch.float32, gpu)
+    hub._buf("loss_parts", (m,), torch.float32, gpu)
+    for k in range(m):
+        for ci in range(nc):
+            sl = slice(k * nc * b + ci * b, k * nc * b + (ci + 1) * b)
+            x, y = parts[k * nc + ci]
+            act = cl.forward(x.to(gpu))
+            amx[sl].copy_(cl._act_amax)
+            labels[sl].copy_(y.to(gpu))
+            codec.encode(act, codec.buffers(("s", ci, k), n, gpu))
+    for k in range(m):
+        hub._run_chunk(k, B, gpu, codec)
+    hub.stage.step()
+    torch.cuda.synchronize()
+    tot = [int(codec.buffers(("s", ci, k), n, gpu)[3].item()) for k in range(m) for ci in range(nc)]
+    gv = [hub._buf(("gvals", ci, k), (n,), torch.float32, gpu)[:tot[k * nc + ci]].clone()
+          for k in range(m) for ci in range(nc)]
+    return hub._bufs["loss_parts"].clone(), gv, hub.stage.params.clone()
+
+
+def test_hub_custom_codec_object_takes_the_unfused_path(gpu):
+    """a codec object passed as `compress` is used as given. On an x3 server it must not reach the
+    fused kernels (they read CutCodec's word-rank layout; a codec without ranks_buffer would raise there):
+    the hub takes the dense unpack -> forward, dense dgrad -> codec.pack path, and its results equal
+    fuse_codec=False with the CutCodec bit for bit. 3 clients x 2 chunks, graphs on."""
+    from splitcnn import dist as sd
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    nc, m, B = 3, 2, 16
+    data = SyntheticMNIST(4)
+    parts = [data.batch(B // m) for _ in range(m * nc)]
+    res = []
+    for compress, fuse in ((_LegacyCodec(), True), (True, False)):
+        a, s = init_models(seed=1)
+        hub = sd.Hub(ServerStage(s, device=gpu), rank=nc, world=nc + 1, micro=m, compress=compress, fuse_codec=fuse)
+        assert not hub._fused(hub._use_codec(gpu))
+        cl = ClientStage(a, device=gpu)
+        cl.emit_amax = True
+        res.append(_hub_chunks(gpu, hub, cl, parts, B))
+    (l0, g0, p0), (l1, g1, p1) = res
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
+    assert all(torch.equal(u.view(torch.int32), v.view(torch.int32)) for u, v in zip(g0, g1))
+
+
+def test_hub_k4_shape_full_size_fused_codec(gpu):
+    """BASELINE config 4 at its own size: 7 clients x 4096 samples, the hub server's 4
+    chunks of 7,168 samples through the fused codec kernels (unpack into the x3 images, the dgrad packing
+    the cut gradient at each part's mask) under HIP graphs — the step the 8-GPU node runs
+    (src/server_part.py:47-52 at the concatenated batch of 28,672).
+      * the server's gradient equals the unfused path's (dense f32 cut -> x3 forward, dense dgrad) fed the
+        same chunks, bit for bit (the fused/unfused identity at full size), and the sum of the four chunks
+        computed independently to 1e-5 (linearity over chunks);
+      * sampled rows of several client parts: the packed cut gradient scattered back equals the same samples
+        run as a small batch at the same grad scale 1/G, bit for bit, at the positions the wire carries
+        (per-sample independence, as test_b4096_per_sample_independence checks for K2);
+      * the 4 loss parts equal the unfused path's bit for bit."""
+    from conftest import rel_err
+    from splitcnn import dist as sd
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.engine import ClientStage, ServerStage
+    nc, m, B = 7, 4, 4096
+    b, G, CH = B // m, nc * B, nc * (B // m)
+    data = SyntheticMNIST(21)
+    parts = [data.batch(b) for _ in range(m * nc)]
+    a, s = init_models(seed=8)
+    hub = sd.Hub(ServerStage(s, device=gpu), rank=nc, world=nc + 1, micro=m, compress=True)
+    cl = ClientStage(a, device=gpu)
+    cl.emit_amax = True
+    assert hub._fused(hub._use_codec(gpu))
+    loss_parts, gv, _ = _hub_chunks(gpu, hub, cl, parts, B)
+    assert "cuts" not in hub._bufs            # ADVICE r5: no dense gradient buffer on the fused server
+    g_hub = hub.stage.grads.clone()
+    cut_hub = hub.cuts_by_client(B)           # the packed gradients scattered: [client][B]
+
+    # the unfused path on the same chunks (f32 cut, dense dgrad), and each chunk on its own
+    _, s_ref = init_models(seed=8)
+    ref = ServerStage(s_ref, device=gpu)
+    _, s_one = init_models(seed=8)
+    one = ServerStage(s_one, device=gpu)
+    acc64 = torch.zeros_like(g_hub, dtype=torch.float64)
+    ref_parts = torch.empty(m, device=gpu)
+    for k in range(m):
+        xs = torch.cat([parts[k * nc + ci][0] for ci in range(nc)]).to(gpu)
+        ys = torch.cat([parts[k * nc + ci][1] for ci in range(nc)]).to(gpu)
+        act = cl.forward(xs).clone()
+        amax = cl._act_amax.clone()
+        _, loss_i = ref.compute(act, ys, 1.0 / G, accumulate=k > 0, act_amax=amax)
+        sd._loss_sum(loss_i, 1.0 / G, ref_parts[k:k + 1])
+        one.compute(act, ys, 1.0 / G, accumulate=False, act_amax=amax)
+        acc64 += one.grads.double()
+        del act
+    torch.cuda.synchronize()
+    assert torch.equal(ref.grads, g_hub)
+    assert torch.equal(ref_parts, loss_parts)
+    assert rel_err(g_hub.double().cpu().numpy(), acc64.cpu().numpy()) <= 1e-5
+
+    # sampled rows vs a small batch of the same samples
+    _, s_small = init_models(seed=8)
+    small = ServerStage(s_small, device=gpu)
+    for k, ci in ((0, 0), (1, 3), (3, 6)):
+        x, y = parts[k * nc + ci]
+        rows = torch.tensor([0, 1, b // 2, b - 1])
+        act = cl.forward(x[rows].contiguous().to(gpu)).clone()
+        amax = cl._act_amax.clone()
+        cut_s, _, _, _ = small.forward_backward(act, y[rows].contiguous().to(gpu), 1.0 / G, act_amax=amax)
+        got = cut_hub[ci * B + k * b + rows.to(gpu)]
+        want = torch.where(act != 0, cut_s, torch.zeros_like(cut_s))
+        assert torch.equal(got, want), (k, ci)
+    assert len(gv) == m * nc and all(g.numel() > 0 for g in gv)

@@ -8,8 +8,8 @@ engine.ServerStage through call sequences the single-GPU trainer never uses:
   bind_grads into an all-reduce bucket.
 Each of them must reproduce the reference's ONE SGD step at the concatenated batch
 (src/server_part.py:47-52, src/client_part.py:132-133), which the golden fixtures pin:
-split_step_b12.npz is exactly "3 clients x 4 samples, concatenated", split_step_b4.npz three
-consecutive B = 4 steps.
+split_step_b12.npz is exactly "3 clients x 4 samples, concatenated", split_step_b14.npz "7 clients x 2
+samples" (BASELINE config 4's client count), split_step_b4.npz three consecutive B = 4 steps.
 
 Two layers:
   * loopback tests — the protocol's exact stage-call sequence in one process (no transport);
@@ -114,16 +114,19 @@ def test_pipeline_sequence_loopback(gpu, m):
         prev = got
 
 
-@pytest.mark.parametrize("nclients,m", [(3, 1), (3, 2), (2, 2)])
-def test_hub_sequence_loopback(gpu, nclients, m):
+@pytest.mark.parametrize("nclients,m,fixture", [(3, 1, "split_step_b12.npz"), (3, 2, "split_step_b12.npz"),
+                                                (2, 2, "split_step_b12.npz"), (7, 1, "split_step_b14.npz"),
+                                                (7, 2, "split_step_b14.npz")])
+def test_hub_sequence_loopback(gpu, nclients, m, fixture):
     """dist.Hub's call order in one process: each client (own ClientStage, same init) forwards its
     micro-batches; the server consumes (micro-batch, client) parts with mean scale 1/G, accumulating;
     clients back-propagate their slices with accumulate, their 320-float gradients are summed (the
-    client all-reduce) and every client steps — vs split_step_b12.npz (12 samples = nclients x B)."""
+    client all-reduce) and every client steps — vs split_step_b12.npz (12 samples = nclients x B) and,
+    at K4's 7 clients, split_step_b14.npz."""
     from splitcnn import ops
     from splitcnn.engine import ClientStage, ServerStage
-    fx = load_fixture("split_step_b12.npz")
-    G = 12
+    fx = load_fixture(fixture)
+    G = int(fx["B"])
     B = G // nclients
     b = B // m
     clients = []
@@ -349,11 +352,13 @@ def test_pipeline_two_ranks_vs_fixture(gpu, tmp_path, micro):
         prev = got
 
 
-@pytest.mark.parametrize("world,micro", [(4, 2), (3, 1)])
-def test_hub_vs_fixture(gpu, tmp_path, world, micro):
-    """K4 protocol (N-1 client ranks -> 1 server rank, client all-reduce) vs split_step_b12.npz."""
-    fx = load_fixture("split_step_b12.npz")
-    out = _spawn(world, "hub", "split_step_b12.npz", micro, tmp_path)
+@pytest.mark.parametrize("world,micro,fixture", [(4, 2, "split_step_b12.npz"), (3, 1, "split_step_b12.npz"),
+                                                (8, 2, "split_step_b14.npz")])
+def test_hub_vs_fixture(gpu, tmp_path, world, micro, fixture):
+    """K4 protocol (N-1 client ranks -> 1 server rank, client all-reduce) vs split_step_b12.npz, and at
+    BASELINE config 4's own world (7 client ranks + 1 server rank, 2 chunks) vs split_step_b14.npz."""
+    fx = load_fixture(fixture)
+    out = _spawn(world, "hub", fixture, micro, tmp_path)
     prev = {k: fx[f"init_{k}"] for k in PARAMS}
     srv = out[world - 1]
     act = np.concatenate([out[r]["act_1"] for r in range(world - 1)])
@@ -410,7 +415,8 @@ def test_widened_splitfed_hub_vs_fused_step(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("topo,world,micro,fixture", [("pipeline", 2, 2, "split_step_b4.npz"),
-                                                      ("hub", 3, 2, "split_step_b12.npz")])
+                                                      ("hub", 3, 2, "split_step_b12.npz"),
+                                                      ("hub", 8, 2, "split_step_b14.npz")])
 def test_cut_codec_bit_identical_to_dense(gpu, tmp_path, topo, world, micro, fixture):
     """The sparse cut codec (the default on CUDA tensors) vs the dense exchange (compress=False):
     every rank's weights, gradients and losses are BIT-identical; the codec moved fewer bytes; the
@@ -562,7 +568,8 @@ def test_hub_image_exchange_matches_f32_cut_bitwise(gpu):
 
 
 @pytest.mark.parametrize("topo,world,micro,fixture", [("pipeline", 2, 2, "split_step_b4.npz"),
-                                                      ("hub", 3, 2, "split_step_b12.npz")])
+                                                      ("hub", 3, 2, "split_step_b12.npz"),
+                                                      ("hub", 8, 2, "split_step_b14.npz")])
 def test_image_exchange_bit_identical_to_dense(gpu, tmp_path, topo, world, micro, fixture):
     """The image exchange (images=True: the client's x3 split images + per-sample max up, the f32 cut
     gradient back) vs the dense f32 exchange, multi-process: every rank's weights, gradients, cut

@@ -329,7 +329,7 @@ def _check(out, ref, nclients):
 
 @pytest.mark.parametrize("shared", [False, True])
 @pytest.mark.parametrize("nclients,micro,codec", [(1, 1, False), (1, 4, False), (1, 4, True), (3, 2, True),
-                                                  (2, 1, True), (3, 2, False)])
+                                                  (2, 1, True), (3, 2, False), (7, 2, True), (7, 4, False)])
 def test_hub_drains_under_rccl_semantics(monkeypatch, nclients, micro, codec, shared):
     """K3 (1 client) and K4 (N-1 clients) with the dense exchange and the codec, micro-batched: both
     sides' op sequences drain under strict rendezvous FIFO semantics, and the result is the oracle's
