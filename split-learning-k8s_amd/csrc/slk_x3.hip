@@ -639,6 +639,9 @@ __global__ __launch_bounds__(X3F_THREADS, 1) void conv2_fwd_pool_x3_kernel(
 #ifndef SLK_X3W_ROUND4
 #define SLK_X3W_ROUND4 0
 #endif
+#ifndef SLK_X3W_SPARSE
+#define SLK_X3W_SPARSE 1
+#endif
 constexpr int RB_SAMPLE = 4 * (A_PIX / 4);  // 676 u32 = 2,704 B per sample: [channel group 4][169]
 constexpr int X3D_THREADS = 512;
 constexpr int X3D_REC = 160;                       // bytes per image pixel: h 64 | l 64 | pad 32
@@ -1774,6 +1777,365 @@ __global__ __launch_bounds__(X3Q_THREADS, 1) void conv2_wgrad_x3q_kernel(
     }
 }
 
+// ============================================================================ conv2 wgrad on the 2:4-sparse f16 MFMA
+// Round 6. dY is the max-pool routing of dpooled: in each 2 x 2 pool window at most ONE position carries a
+// value. Take the GEMM's K (output pixels) in blocks of 4 consecutive pixels of one output row starting at a
+// multiple of 4: such a block holds two positions of each of two windows, so at most 2 of its 4 dY values
+// are nonzero for any co — exactly the 2:4 structure of v_smfmac_f32_16x16x64_f16, which multiplies a
+// 16 x 64 A given as its nonzeros (2 per group of 4 + a 2-bit position each) by a dense 64 x 16 B at the
+// issue cost of one dense v_mfma_f32_16x16x32_f16 (tools/ubench/smfmac_probe.hip: 17.6-18.2 vs 18.1-19.1
+// cycles per instruction): half the MFMA instructions of the dense x3 wgrad for the same products.
+// Operand layouts of the instruction, measured by that probe (one-hot A against distinct B):
+//   B (dense, K x N): lane (gb = lane >> 4, n = lane & 15) holds K slots (gb, j), j = 0..15, of column n;
+//   A (compressed, M x K): lane (ga = lane >> 4, m = lane & 15) value i (0..7) is the row-m entry of K slot
+//     (gb = 2 (ga & 1) + (i >> 2), j = 8 (ga >> 1) + 4 ((i >> 1) & 1) + idx_i), idx_i = (index >> 2i) & 3;
+//   D as the dense 16x16x32 (lane l: D[4 (l >> 4) + r][l & 15]).
+// Here M = co (4 tiles), N = (ci half, tap), K = the unit's 192 output pixels (sample, third: output rows
+// 8t..8t+7) = 3 K-steps of 64 = 48 blocks: block L = 16 s + 4 gb + jb (jb = j >> 2) is output row L / 6,
+// columns 4 (L % 6) .. +3. B = the act16 input image (both planes, LDS-DMA as the forward's) read with
+// ds_read_b64_tr_b16, one 4-pixel block per read, 4 per fragment. A = compressed dY records [s][ga][co] of
+// 8 halves (h plane, l plane) + a u16 index word each, written by the staging items (co, window row,
+// window quad): the 4 windows of a quad are two blocks of each of the two output rows of the window row,
+// and those two blocks are one half of one record (8 B) + one byte of its index word. A record is the exact
+// register image of a lane's A fragment: one conflict-free ds_read_b128 per (M tile, plane) per K-step.
+// Waves: 4 M tiles (all 64 co) per wave, so every B fragment feeds 12 MFMAs; (ci half, tap group) items:
+// waves 0/1 taps 0-2, 4/5 taps 3-4, 2/3 taps 5-6, 6/7 taps 7-8 (ci half = wave & 1): SIMD pairs (w, w + 4)
+// carry 5, 5, 4, 4 taps. Scales, db and the slab format as conv2_wgrad_x3q_kernel.
+#ifndef SLK_X3P_PLAN
+#define SLK_X3P_PLAN 0  // 0: staging before (waves 4-7) / after (0-3) the MFMA steps; 1: in pieces between K-steps
+#endif
+#ifndef SLK_X3P_STG
+#define SLK_X3P_STG 0  // 0: items q = wave and 8 + wave (waves 0-3); 1: only the 4-tap SIMDs' waves (2, 3, 6, 7), 3 each
+#endif
+#ifndef SLK_X3P_ABL
+#define SLK_X3P_ABL 0  // profiling only (wrong results): 1 no in-loop dY staging, 2 no MFMA steps, 4 no in-loop DMA
+#endif
+constexpr int X3P_THREADS = 512;
+constexpr int X3P_STEPS = 3;                                   // K64 steps per unit (192 pixels)
+constexpr int X3P_REC = X3P_STEPS * 4 * 64 * 16;               // 12,288 B per compressed dY plane
+constexpr int X3P_IDXB = X3P_STEPS * 4 * 64 * 2;               // 1,536 B of index words
+constexpr int X3P_DYOFF = 2 * X3F_PLANE;                       // after the unit's input image (h | l)
+constexpr int X3P_IDXOFF = X3P_DYOFF + 2 * X3P_REC;
+constexpr int X3P_BUF = (X3P_IDXOFF + X3P_IDXB + 1023) / 1024 * 1024;  // 59,392 B
+constexpr int X3P_ITEMS = C2 * 12;                             // (co, window row of 4, window quad of 3)
+static_assert(2 * X3P_BUF <= 163840 && X3P_ITEMS <= 2 * X3P_THREADS && X3P_ITEMS > X3P_THREADS, "x3p layout");
+
+template <int TGI, class F>
+__device__ __forceinline__ void x3p_steps(const char* img, const int (&pb)[X3P_STEPS][4], const int (&sw)[3], int arec,
+                                          int aidx, f32x4 (&acc)[3][4], F&& after_step) {
+    constexpr int T0 = TGI == 0 ? 0 : (TGI == 1 ? 3 : (TGI == 2 ? 5 : 7));
+    constexpr int NT = TGI == 0 ? 3 : 2;
+    typedef __fp16 hf4 __attribute__((__vector_size__(8)));
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 f16x16 __attribute__((ext_vector_type(16)));
+    typedef __attribute__((address_space(3))) hf4* lp4;
+    auto tr = [&](const char* p) -> f16x4 { return __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lp4)p)); };
+#pragma unroll
+    for (int s = 0; s < X3P_STEPS; ++s) {
+        f16x8 ah[4], al[4];
+        int ix[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            ah[mt] = *reinterpret_cast<const f16x8*>(img + X3P_DYOFF + arec + s * 4096 + mt * 256);
+            al[mt] = *reinterpret_cast<const f16x8*>(img + X3P_DYOFF + X3P_REC + arec + s * 4096 + mt * 256);
+            ix[mt] = *reinterpret_cast<const uint16_t*>(img + X3P_IDXOFF + aidx + s * 512 + mt * 32);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int tap = T0 + t, ky = tap / 3, kx = tap % 3;
+            f16x4 bh[4], bl[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) {
+                const char* p = img + pb[s][jb] + sw[kx] + (ky * A_HW + kx) * 64;
+                bh[jb] = tr(p);
+                bl[jb] = tr(p + X3F_PLANE);
+            }
+            const f16x16 Bh = __builtin_shufflevector(__builtin_shufflevector(bh[0], bh[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                      __builtin_shufflevector(bh[2], bh[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                      0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+            const f16x16 Bl = __builtin_shufflevector(__builtin_shufflevector(bl[0], bl[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                      __builtin_shufflevector(bl[2], bl[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                      0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                f32x4 c = acc[t][mt];
+                c = __builtin_amdgcn_smfmac_f32_16x16x64_f16(ah[mt], Bh, c, ix[mt], 0, 0);
+                c = __builtin_amdgcn_smfmac_f32_16x16x64_f16(ah[mt], Bl, c, ix[mt], 0, 0);
+                c = __builtin_amdgcn_smfmac_f32_16x16x64_f16(al[mt], Bh, c, ix[mt], 0, 0);
+                acc[t][mt] = c;
+            }
+        }
+        after_step(s);
+    }
+}
+
+__global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
+    const uint16_t* __restrict__ act16, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
+    const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * X3P_BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = wave & 1, tgi = ((wave >> 1) & 1) * 2 + (wave >> 2);  // 0: taps 0-2, 1: 3-4, 2: 5-6, 3: 7-8
+    const int ks = blockIdx.x, nks = gridDim.x;
+    const int U = 3 * B;
+    float* red = reinterpret_cast<float*>(smem);
+    X3Q_TS(0, 7);
+
+    // launch scales: max over the batch of the per-sample maxima (as conv2_wgrad_x3q_kernel)
+    float ma = 0.f, md = 0.f;
+    for (int i = tid; i < B; i += X3P_THREADS) {
+        ma = fmaxf(ma, act_amax[i]);
+        md = fmaxf(md, dp_amax[i]);
+    }
+    ma = wave_max(ma);
+    md = wave_max(md);
+    if (lane == 0) {
+        red[wave] = ma;
+        red[16 + wave] = md;
+    }
+    __syncthreads();
+    ma = red[0];
+    md = red[16];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+        ma = fmaxf(ma, red[i]);
+        md = fmaxf(md, red[16 + i]);
+    }
+    __syncthreads();
+    const int sx = x3_exp(ma), sd = x3_exp(md);
+
+    // staging items (co, q = 3 window row + window quad): co = lane (fastest, so a 16-lane LDS store group
+    // writes 16 consecutive 16-B records: 2-way banks instead of the 6-12-way of 12 items of one co), q = wave
+    // and, for waves 0-3, 8 + wave. Per item the global offset within the unit and the two LDS destinations
+    // (one per output row of the window row) do not depend on the unit: computed once.
+#if SLK_X3P_STG == 0
+    constexpr int NI = 2;
+    const bool two = wave < 4;
+    const int nit = two ? 2 : 1;
+#else
+    constexpr int NI = 3;
+    const bool two = false;
+    const int sidx = (wave & 1) + 2 * (wave >> 2);           // waves 2, 3, 6, 7 -> 0, 1, 2, 3
+    const int nit = (wave & 2) ? 3 : 0;
+#endif
+    int goff[NI], ldo[NI][2];
+#pragma unroll
+    for (int r = 0; r < NI; ++r) {
+#if SLK_X3P_STG == 0
+        const int q = r == 0 ? wave : 8 + (wave & 3);
+#else
+        const int q = 3 * sidx + r;
+#endif
+        const int wyl = q / 3, wq = q - (q / 3) * 3;
+        goff[r] = lane * P_WIN + wyl * P_HW + 4 * wq;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const int L = 6 * (2 * wyl + d) + 2 * wq;  // even: the quad's first block
+            const int st = L >> 4, gb = (L >> 2) & 3, jb = L & 3;
+            const int rec = (st * 4 + 2 * (jb >> 1) + (gb >> 1)) * 64 + lane;
+            ldo[r][d] = rec * 16 + 8 * (gb & 1);  // h plane; the index byte is rec * 2 + (gb & 1)
+        }
+    }
+    float4 dv[NI];
+    uint32_t dcw[NI];
+    int sb_ld = 0;
+    auto load_dy = [&](int uu) {
+        const int b = uu / 3, t3 = uu - (uu / 3) * 3;
+        const size_t o = (size_t)b * P_SAMPLE + t3 * 4 * P_HW;
+#pragma unroll
+        for (int r = 0; r < NI; ++r) {
+            if (r < nit) {
+                dv[r] = *reinterpret_cast<const float4*>(dpooled + o + goff[r]);
+                dcw[r] = *reinterpret_cast<const uint32_t*>(code + o + goff[r]);
+            }
+        }
+        sb_ld = max(x3_exp(act_amax[b]), sx);
+    };
+    float dbacc[NI] = {};
+    int trk = 0;  // (trace builds: the unit index of the stamps inside the staging)
+    (void)trk;
+    auto store_dy1 = [&](char* img, bool real, int r) {
+        const float dsc = ldexpf(1.f, sd + sx - sb_ld);
+        {
+            {
+                const float v[4] = {dv[r].x, dv[r].y, dv[r].z, dv[r].w};
+#if SLK_X3D_TRACE
+                if (r == 0) {
+                    asm volatile("" ::"v"(v[0]), "v"(dcw[0]));
+                    X3Q_TS(trk, 4);
+                }
+#endif
+                const uint32_t cw = dcw[r];
+                // index byte: window j's position in its block = its dx, +2 for the block's second window
+                const uint32_t ib = (cw & 1u) | ((cw >> 6) & 4u) | ((cw >> 12) & 16u) | ((cw >> 18) & 64u) | 0x88u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t c = (cw >> (8 * j)) & 0xFFu;
+                    if (real && c < (uint32_t)CODE_NONE) dbacc[r] += v[j];
+                }
+                // per byte (c >> 1): 0 / 1 = the routed row parity, 2 = ReLU-blocked (CODE_NONE): never a row
+                const uint32_t rowp = (cw >> 1) & 0x7F7F7F7Fu;
+                uint32_t H[2], Lw[2];
+#pragma unroll
+                for (int jp = 0; jp < 2; ++jp) {
+                    const float a = v[2 * jp] * dsc, bb = v[2 * jp + 1] * dsc;
+                    const _Float16 ha = (_Float16)a, hb = (_Float16)bb;
+                    const _Float16 la = (_Float16)(a - (float)ha), lb = (_Float16)(bb - (float)hb);
+                    H[jp] = __builtin_bit_cast(uint32_t, f16x2{ha, hb});
+                    Lw[jp] = __builtin_bit_cast(uint32_t, f16x2{la, lb});
+                }
+#pragma unroll
+                for (int d = 0; d < 2; ++d) {
+                    // byte j -> 0xFF where window j routes to row parity d; then halves [b0 b0 b1 b1], [b2 b2 b3 b3]
+                    // (bytes are 0..2, so bits 0-1 decide; the shift's carry-in from the next byte is masked)
+                    const uint32_t z = (d ? (rowp & ~(rowp >> 1)) : ~(rowp | (rowp >> 1))) & 0x01010101u;
+                    const uint32_t m8 = z * 0xFFu;
+                    const uint32_t mA = __builtin_amdgcn_perm(0u, m8, 0x01010000u), mB = __builtin_amdgcn_perm(0u, m8, 0x03030202u);
+                    char* ph = img + X3P_DYOFF + ldo[r][d];
+                    *reinterpret_cast<uint2*>(ph) = make_uint2(H[0] & mA, H[1] & mB);
+                    *reinterpret_cast<uint2*>(ph + X3P_REC) = make_uint2(Lw[0] & mA, Lw[1] & mB);
+                    img[X3P_IDXOFF + ((ldo[r][d] >> 4) << 1) + ((ldo[r][d] >> 3) & 1)] = (char)ib;
+                }
+            }
+        }
+    };
+    auto store_dy = [&](char* img, bool real) {
+#pragma unroll
+        for (int r = 0; r < NI; ++r)
+            if (r < nit) store_dy1(img, real, r);
+        X3Q_TS(trk, 5);
+    };
+
+    // B (tr-read) lane bases: lane (gb, qq, pp) of block (s, jb) -> pixel (y, 4 xb + qq), channels 4 pp.. of
+    // its ci half; the chunk-slot swizzle (h ^ (x >> 1) & 1) depends on kx + qq only (4 xb is a multiple of 4)
+    const int gbl = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    int pb[X3P_STEPS][4], sw[3];
+#pragma unroll
+    for (int s = 0; s < X3P_STEPS; ++s)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+            const int L = 16 * s + 4 * gbl + jb, y = L / 6, xb = L - (L / 6) * 6;
+            pb[s][jb] = (y * A_HW + 4 * xb + qq) * 64 + pp * 8;
+        }
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) sw[kx] = (h ^ (((kx + qq) >> 1) & 1)) * 32;
+    const int arec = ((lane >> 4) * 64 + (lane & 15)) * 16, aidx = ((lane >> 4) * 64 + (lane & 15)) * 2;
+
+    f32x4 acc[3][4];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int per = (U + nks - 1) / nks;
+    const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
+    int u = u0;
+    if (u < u1) {
+        x3_issue_unit_img(act16, u, wave, lane, lds_u32(smem));
+        load_dy(u);
+        store_dy(smem, true);
+        load_dy(min(u + 1, u1 - 1));
+    }
+    int k = 0;
+#pragma unroll 1
+    for (; u < u1; ++u, ++k) {
+        // this unit's image DMA landed; the dY loads (every wave's last memory instructions, issued after its
+        // DMA pieces) may stay in flight
+        X3Q_TS(k, 6);
+        if ((SLK_X3P_ABL & 1) || nit == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (nit == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (nit == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        __syncthreads();  // buffer k&1 complete; buffer (k+1)&1 free
+        X3Q_TS(k, 0);
+        trk = k;
+        const int nx = u + 1, nx2 = u + 2;
+        const char* img = smem + (k & 1) * X3P_BUF;
+        char* nimg = smem + ((k & 1) ^ 1) * X3P_BUF;
+        // half the waves route dY before their MFMAs, half after (the two waves of a SIMD overlap routing with
+        // MFMAs); store_dy before the DMA issue (hipcc does not count the asm DMAs)
+#if SLK_X3P_PLAN == 0
+        const bool dfirst = wave >= 4 && !(SLK_X3P_ABL & 1);
+        if (dfirst) store_dy(nimg, nx < u1);
+        if (!(SLK_X3P_ABL & 4)) x3_issue_unit_img(act16, min(nx, u1 - 1), wave, lane, lds_u32(nimg));
+        if (dfirst) load_dy(min(nx2, u1 - 1));
+        auto hook = [&](int) {};
+        X3Q_TS(k, 1);
+#else
+        // plan 1: the next unit's image pieces and dY routing in pieces between this unit's K-steps; the dY
+        // loads last (after every DMA piece: the counted vmcnt at the top)
+        const char* srch = x3_unit_img_src(act16, min(nx, u1 - 1));
+        const uint32_t nl = lds_u32(nimg);
+        auto hook = [&](int st) {
+            if (st == 0) {
+                if (!(SLK_X3P_ABL & 4)) {
+                    x3_issue_img_full(srch, wave, lane, nl, 0);
+                    x3_issue_img_full(srch, wave, lane, nl, 1);
+                }
+                if (!(SLK_X3P_ABL & 1)) store_dy1(nimg, nx < u1, 0);
+            } else if (st == 1) {
+                if (!(SLK_X3P_ABL & 4)) {
+                    x3_issue_img_full(srch, wave, lane, nl, 2);
+                    x3_issue_img_full(srch, wave, lane, nl, 3);
+                    if (wave < 2) x3_issue_img_quarter(srch, wave, lane, nl);
+                }
+                if (!(SLK_X3P_ABL & 1) && two) store_dy1(nimg, nx < u1, 1);
+            } else {
+                if (!(SLK_X3P_ABL & 1)) load_dy(min(nx2, u1 - 1));
+            }
+        };
+#endif
+        if (!(SLK_X3P_ABL & 2)) {
+            if (tgi == 0) x3p_steps<0>(img, pb, sw, arec, aidx, acc, hook);
+            else if (tgi == 1) x3p_steps<1>(img, pb, sw, arec, aidx, acc, hook);
+            else if (tgi == 2) x3p_steps<2>(img, pb, sw, arec, aidx, acc, hook);
+            else x3p_steps<3>(img, pb, sw, arec, aidx, acc, hook);
+        } else {
+            hook(0);
+            hook(1);
+            hook(2);
+        }
+        X3Q_TS(k, 2);
+#if SLK_X3P_PLAN == 0
+        if (!dfirst && !(SLK_X3P_ABL & 1)) {
+            store_dy(nimg, nx < u1);
+            load_dy(min(nx2, u1 - 1));
+        }
+#endif
+        X3Q_TS(k, 3);
+    }
+    X3Q_TS(127, 7);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped) image DMA lands before LDS reuse
+    __syncthreads();
+    // db partials per item -> LDS; co's 12 items summed in order
+    float* dbs = reinterpret_cast<float*>(smem);  // [item = 64 q + co]
+#pragma unroll
+    for (int r = 0; r < NI; ++r)
+        if (r < nit) dbs[(SLK_X3P_STG == 0 ? (r == 0 ? wave : 8 + (wave & 3)) : 3 * ((wave & 1) + 2 * (wave >> 2)) + r) * 64 + lane] = dbacc[r];
+    __syncthreads();
+    float* slab = slabs + (size_t)ks * (W2_N + C2);
+    if (tid < C2) {
+        float sum = 0.f;
+        for (int q = 0; q < 12; ++q) sum += dbs[q * 64 + tid];
+        slab[W2_N + tid] = sum;
+    }
+    const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
+    const int ci = 16 * h + (lane & 15);
+    const int T0 = tgi == 0 ? 0 : (tgi == 1 ? 3 : (tgi == 2 ? 5 : 7)), nt = tgi == 0 ? 3 : 2;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+        if (t < nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = 16 * mt + 4 * (lane >> 4) + r;
+                    slab[(co * C1 + ci) * 9 + T0 + t] = x3_unscale(acc[t][mt][r], us1, us2);
+                }
+}
+
 // ============================================================================ conv1 -> x3 input images
 // The client's conv1 + ReLU (src/model_def.py:8-9, the per-pixel FMA order of slk_client.hip's
 // conv1_fwd_kernel: taps from 0, then + bias) writing the server's x3 operand directly: per sample, the
@@ -2124,6 +2486,9 @@ extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax,
 #if SLK_X3W_ROUND4  // profiling A/B: the round-4 kernel (one co half per workgroup, 8-row units)
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<true>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), nullptr,
                        act_amax, dpooled, dp_amax, code, slabs, B, act16);
+#elif SLK_X3W_SPARSE  // round 6: the 2:4-sparse MFMA form (conv2_wgrad_x3p_kernel)
+    hipLaunchKernelGGL(conv2_wgrad_x3p_kernel, dim3(nks), dim3(X3P_THREADS), 0, slk_stream(stream), act16, act_amax,
+                       dpooled, dp_amax, code, slabs, B);
 #else
     hipLaunchKernelGGL(conv2_wgrad_x3q_kernel, dim3(nks), dim3(X3Q_THREADS), 0, slk_stream(stream), act16, act_amax,
                        dpooled, dp_amax, code, slabs, B);

@@ -297,8 +297,9 @@ class ServerStage:
                          cut_grad: Optional[torch.Tensor] = None, act_amax: Optional[torch.Tensor] = None,
                          act16: Optional[torch.Tensor] = None, client_fuse=None, cut_pack=None):
         """Server forward + CE + backward WITHOUT the optimizer step. Returns (cut_grad, loss_i,
-        conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample max
-        of act when the client produced it (ClientStage.emit_amax); the x3 kernels compute it otherwise.
+        conv2 slabs, fc slabs). grad_scale = 1/global_batch (mean loss). act_amax: the per-sample x3
+        scale bound of act when the client produced it (ClientStage.emit_amax: conv1_cut_bound, >= max act;
+        only its power of two is used); the x3 kernels compute the exact max otherwise.
         act16 (with act_amax, x3 forward + wgrad only): the client's split input images
         (ClientStage.emit_act16) — act is then not read and may be None. client_fuse = (x, relu_bits,
         slabs) (x3 dgrad only, single-GPU step): the dgrad also runs the client's ReLU backward +

@@ -238,6 +238,10 @@ def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16):
     if "x3" in (di, wi):
         # fc1's input gradient comes with its per-sample max (linear_dgrad, fused); recomputed otherwise
         dpa = _MEMO.take("dp_amax", dpooled)
+        # a per-row max fits only the producer's row layout: a permuted / transposed view of the same storage
+        # (same key) must recompute
+        if dpa is not None and not (dpooled.is_contiguous() and dpooled.shape[0] == dpa.numel()):
+            dpa = None
         if dpa is None:
             dpa = torch.ops.splitcnn.row_amax(dpooled)
     gact = None

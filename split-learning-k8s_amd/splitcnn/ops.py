@@ -57,7 +57,9 @@ def batch_of(x: torch.Tensor, tail: tuple, name: str) -> int:
 
 # ------------------------------------------------------------------------------------ client stage
 def conv1_fwd(x, W1, b1, out=None, act_amax=None):
-    """act = relu(conv1(x)); with act_amax (a [B] f32 tensor) also its per-sample max, fused."""
+    """act = relu(conv1(x)); with act_amax (a [B] f32 tensor) also its per-sample x3 SCALE BOUND, fused:
+    conv1_cut_bound (csrc/slk_common.h) = max_c (sum |W1[c]| * max |x| + max(b1[c], 0)) >= max act, not the
+    max itself (only its power of two is used)."""
     B = batch_of(x, (1, 28, 28), "x")
     act = _out(out, (B, 32, 26, 26), x)
     if act_amax is not None:
@@ -77,7 +79,8 @@ def relu_bits_buffer(B: int, device) -> torch.Tensor:
 
 
 def conv1_fwd_x3(x, W1, b1, act_amax, act16, act=None, relu_bits=None):
-    """conv1 + ReLU writing the x3 server operand: act_amax [B] and the act16 images
+    """conv1 + ReLU writing the x3 server operand: act_amax [B] (the per-sample scale bound
+    conv1_cut_bound, >= max act; see conv1_fwd) and the act16 images
     (conv2_act16_bytes(B) uint8), plus the f32 act when `act` is given and the cut's ReLU bit map
     (int32 [B, RELU_BITS_WORDS], the fused client backward's mask) when `relu_bits` is. Returns act (or None)."""
     B = batch_of(x, (1, 28, 28), "x")
@@ -177,8 +180,9 @@ def _act16(t, B):
 def conv2_fwd_pool(act, W2, b2, pooled=None, code=None, direct=False, impl=None, act_amax=None, act16=None,
                    act_amax_out=None):
     """impl: 'wino' (Winograd F(2x2,3x3) on the f32 MFMA, default), 'direct' (direct f32 MFMA kernel,
-    cross-check; also direct=True) or 'x3' (direct on the f16 MFMA with split operands; act_amax =
-    per-sample max |act|, computed here when not given). act16 (x3 only, a uint8 tensor of
+    cross-check; also direct=True) or 'x3' (direct on the f16 MFMA with split operands; act_amax = a
+    per-sample scale bound >= max |act| — the client's conv1_cut_bound, or the exact max (row_amax), computed
+    here when not given; only its power of two matters). act16 (x3 only, a uint8 tensor of
     conv2_act16_bytes(B)): also write the split input images for conv2_wgrad_slabs(act16=...).
     act_amax_out (x3 with act16, act_amax not given; a float tensor [B]): the forward kernel computes the
     per-sample max itself and writes it there (slk_conv2_fwd_pool_x3sa: no separate pass over act; the

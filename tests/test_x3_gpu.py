@@ -613,3 +613,44 @@ def test_trajectory_100_steps_b4096_default_vs_f32_preset(gpu):
         d, r = arr[sl], ref[k][sl]
         err = np.abs(d - r).max() / np.abs(r).max()
         assert err <= 1e-3, (k, err)
+
+
+@pytest.mark.parametrize("k", [4, 6])
+def test_x3_loose_scale_bound_error_within_2x_of_f32(gpu, k):
+    """act_amax from the client's conv1 is conv1_cut_bound (>= max act), not the max; with mixed-sign
+    W1 or cancelling inputs it can sit several times above the cut's max, which moves the hi/lo split lower and
+    drops the low parts of small elements into f16's subnormal range. Bounds 2^k x the true per-sample max
+    (k = 4, 6; the dgrad's dp_amax likewise): forward, wgrad and dgrad stay within the f32 path's bars against
+    fp64 (1e-5 of max |ref|, <= 2x the f32 Winograd kernel's own error)."""
+    from oracle.split_step import conv3x3, conv3x3_dgrad, conv3x3_wgrad, maxpool2_bwd, relu, tie_discrepancies
+    from splitcnn import ops
+    B = 64
+    act, p, y = _inputs(gpu, B, seed=31 + k)
+    loose = ops.row_amax(act) * 2.0 ** k
+    px, cx = ops.conv2_fwd_pool(act, p["W2"], p["b2"], impl="x3", act_amax=loose)
+    pw, cw = ops.conv2_fwd_pool(act, p["W2"], p["b2"])
+    a64 = act.double().cpu().numpy()
+    r = relu(conv3x3(a64, p["W2"].double().cpu().numpy(), p["b2"].double().cpu().numpy()))
+    pr = r.reshape(B, 64, 12, 2, 12, 2).max(axis=(3, 5))
+    n, ok = tie_discrepancies(r, cw.cpu().numpy().astype(np.int64), cx.cpu().numpy().astype(np.int64))
+    assert ok, f"{n} routing differences that are not ties"
+    ex, ew = rel_err(px.cpu().numpy(), pr), rel_err(pw.cpu().numpy(), pr)
+    assert ex <= 1e-5 and ex <= max(2 * ew, 1e-6), (ex, ew)
+
+    _, _, _, dp = ops.fc_xent(pw, p["W3"], p["b3"], y, 1.0 / B)
+    codes = cw.cpu().numpy().astype(np.int64)
+    dp64 = dp.double().cpu().numpy().reshape(B, 64, 12, 12)
+    dc = maxpool2_bwd(np.where(codes < 4, dp64, 0.0), np.minimum(codes, 3), (B, 64, 24, 24))
+    dloose = ops.row_amax(dp.reshape(B, -1)) * 2.0 ** k
+    sx = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw, impl="x3", act_amax=loose, dp_amax=dloose)).cpu().numpy()
+    sw = ops.reduce_slabs(ops.conv2_wgrad_slabs(act, dp, cw)).cpu().numpy()
+    dW, db = conv3x3_wgrad(a64, dc)
+    for got, w, ref in ((sx[:18432], sw[:18432], dW.reshape(-1)), (sx[18432:], sw[18432:], db)):
+        ex, ew = rel_err(got, ref), rel_err(w, ref)
+        assert ex <= 1e-5 and ex <= max(2 * ew, 1e-6), (ex, ew)
+
+    gx = ops.conv2_dgrad(dp, cw, p["W2"], impl="x3", dp_amax=dloose)
+    gw = ops.conv2_dgrad(dp, cw, p["W2"])
+    ref = conv3x3_dgrad(dc, p["W2"].double().cpu().numpy())
+    ex, ew = rel_err(gx.cpu().numpy(), ref), rel_err(gw.cpu().numpy(), ref)
+    assert ex <= 1e-5 and ex <= max(2 * ew, 1e-6), (ex, ew)

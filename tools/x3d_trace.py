@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--B", type=int, default=4096)
-    ap.add_argument("--kernel", default="dgrad", choices=["dgrad", "wgrad"])
+    ap.add_argument("--kernel", default="dgrad", choices=["dgrad", "wgrad", "wgradp"])
     args = ap.parse_args()
     from splitcnn import ops
     from splitcnn.data import SyntheticMNIST, init_models
@@ -57,7 +57,7 @@ def main():
     L.slk_conv2_dgrad_x3_c1w.argtypes = [P] * 7 + [ctypes.c_int, P]
     sl = torch.empty(L.slk_conv2_dgrad_x3_c1w_nslab(B), 320, device=dev)
     run = lambda: L.slk_conv2_dgrad_x3_c1w(p(dp), p(dpa), p(code), p(W2), p(xg), p(bits), p(sl), B, st)  # noqa: E731
-    if args.kernel == "wgrad":
+    if args.kernel in ("wgrad", "wgradp"):
         L.slk_conv2_wgrad_x3_nslab.restype = ctypes.c_int
         L.slk_conv2_wgrad_x3s.restype = ctypes.c_int
         L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
@@ -73,7 +73,7 @@ def main():
         ms.append(e0.elapsed_time(e1))
     ms = sorted(ms[2:])
     buf = np.zeros(256 * 8 * NU * NS, dtype=np.uint64)
-    rd = L.slk_x3q_trace_read if args.kernel == "wgrad" else L.slk_x3d_trace_read
+    rd = L.slk_x3q_trace_read if args.kernel != "dgrad" else L.slk_x3d_trace_read
     assert rd(ctypes.c_void_p(buf.ctypes.data)) == 0
     T = buf.reshape(256, 8, NU, NS).astype(np.int64)
     t_start = T[:, :, 0, 7]
@@ -83,6 +83,10 @@ def main():
     G = 256
     if args.kernel == "wgrad":
         wgrad_report(T, (6 * B + G - 1) // G)
+        return
+    if args.kernel == "wgradp":  # the sparse wgrad: 3 units per sample, nslab = min(6 B, 256) K shares
+        per = (3 * B + G - 1) // G
+        wgrad_report(T, per)
         return
     per = (3 * B + G - 1) // G
     nu = 2 * per
@@ -137,6 +141,15 @@ def wgrad_report(T, nu):
     gap[:, :, :-1] = T[:, :, u[1:], 6] - T[:, :, u[:-1], 3]
     unit = np.zeros_like(bar)
     unit[:, :, :-1] = T[:, :, u[1:], 0] - T[:, :, u[:-1], 0]
+    dwait = np.zeros_like(bar)
+    sto = np.zeros_like(bar)
+    if T[:, :, u, 4].any():  # the sparse kernel's stamps inside its staging: data ready (4), stores done (5)
+        first = np.where(np.arange(8)[None, :, None] >= 4, T[:, :, u, 0], T[:, :, u, 2])
+        dwait = T[:, :, u, 4] - first
+        sto = T[:, :, u, 5] - T[:, :, u, 4]
+        print("staging: cycles from its start to its data (the loads' wait) and then to its last store, by wave")
+        for w in range(8):
+            print(f"{w:>4} wait {dwait[:, w].mean():8.0f}  stores {sto[:, w].mean():8.0f}")
     print("wave = 4 tg + 2 c + h; tg 1 (waves 4-7) route before their MFMAs; waves 6-7 route nothing")
     print(f"{'wave':>4} {'barrier':>8} {'route<':>8} {'mfma':>8} {'route>':>8} {'gap':>6} {'unit':>8}")
     for w in range(8):
