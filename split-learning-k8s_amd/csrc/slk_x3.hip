@@ -1818,6 +1818,7 @@ constexpr int X3P_DYOFF = 2 * X3F_PLANE;                       // after the unit
 constexpr int X3P_IDXOFF = X3P_DYOFF + 2 * X3P_REC;
 constexpr int X3P_BUF = (X3P_IDXOFF + X3P_IDXB + 1023) / 1024 * 1024;  // 59,392 B
 constexpr int X3P_ITEMS = C2 * 12;                             // (co, window row of 4, window quad of 3)
+constexpr int X3P_SBN = (163840 - 2 * X3P_BUF) / 4;            // per-sample scale table entries (11,264)
 static_assert(2 * X3P_BUF <= 163840 && X3P_ITEMS <= 2 * X3P_THREADS && X3P_ITEMS > X3P_THREADS, "x3p layout");
 
 template <int TGI, class F>
@@ -1874,7 +1875,10 @@ __device__ __forceinline__ void x3p_steps(const char* img, const int (&pb)[X3P_S
 __global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
     const uint16_t* __restrict__ act16, const float* __restrict__ act_amax, const float* __restrict__ dpooled,
     const float* __restrict__ dp_amax, const uint8_t* __restrict__ code, float* __restrict__ slabs, int B) {
-    __shared__ __attribute__((aligned(1024))) char smem[2 * X3P_BUF];
+    __shared__ __attribute__((aligned(1024))) char smem[163840];
+    // after both buffers: the K share's per-sample dY scale exponents sd + sx - s_b (a scalar load of act_amax per
+    // unit in the loop would hold the next LDS waits behind it: lgkmcnt counts both)
+    int* sbt = reinterpret_cast<int*>(smem + 2 * X3P_BUF);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = wave & 1, tgi = ((wave >> 1) & 1) * 2 + (wave >> 2);  // 0: taps 0-2, 1: 3-4, 2: 5-6, 3: 7-8
@@ -1940,7 +1944,7 @@ __global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
     }
     float4 dv[NI];
     uint32_t dcw[NI];
-    int sb_ld = 0;
+    int ld_b = 0, sb0 = 0;
     auto load_dy = [&](int uu) {
         const int b = uu / 3, t3 = uu - (uu / 3) * 3;
         const size_t o = (size_t)b * P_SAMPLE + t3 * 4 * P_HW;
@@ -1951,13 +1955,13 @@ __global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
                 dcw[r] = *reinterpret_cast<const uint32_t*>(code + o + goff[r]);
             }
         }
-        sb_ld = max(x3_exp(act_amax[b]), sx);
+        ld_b = b;
     };
     float dbacc[NI] = {};
     int trk = 0;  // (trace builds: the unit index of the stamps inside the staging)
     (void)trk;
     auto store_dy1 = [&](char* img, bool real, int r) {
-        const float dsc = ldexpf(1.f, sd + sx - sb_ld);
+        const float dsc = ldexpf(1.f, sbt[ld_b - sb0]);
         {
             {
                 const float v[4] = {dv[r].x, dv[r].y, dv[r].z, dv[r].w};
@@ -2031,6 +2035,10 @@ __global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
 
     const int per = (U + nks - 1) / nks;
     const int u0 = min(ks * per, U), u1 = min(u0 + per, U);
+    sb0 = u0 / 3;
+    const int nsb = u1 > u0 ? (u1 - 1) / 3 - sb0 + 1 : 0;
+    for (int j = tid; j < nsb; j += X3P_THREADS) sbt[j] = sd + sx - max(x3_exp(act_amax[sb0 + j]), sx);
+    __syncthreads();
     int u = u0;
     if (u < u1) {
         x3_issue_unit_img(act16, u, wave, lane, lds_u32(smem));
@@ -2487,6 +2495,11 @@ extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax,
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<true>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), nullptr,
                        act_amax, dpooled, dp_amax, code, slabs, B, act16);
 #elif SLK_X3W_SPARSE  // round 6: the 2:4-sparse MFMA form (conv2_wgrad_x3p_kernel)
+    if (((3 * B + nks - 1) / nks) / 3 + 2 > X3P_SBN) {  // a K share's samples exceed the LDS scale table
+        hipLaunchKernelGGL(conv2_wgrad_x3q_kernel, dim3(nks), dim3(X3Q_THREADS), 0, slk_stream(stream), act16, act_amax,
+                           dpooled, dp_amax, code, slabs, B);
+        return slk_launch_status();
+    }
     hipLaunchKernelGGL(conv2_wgrad_x3p_kernel, dim3(nks), dim3(X3P_THREADS), 0, slk_stream(stream), act16, act_amax,
                        dpooled, dp_amax, code, slabs, B);
 #else
