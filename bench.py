@@ -188,7 +188,7 @@ ALGO_BYTES = {"conv2_fwd_pool": 132_608, "conv2_dgrad": 46_080, "conv2_wgrad": 1
 ROCPROF_SYMBOL = {("conv2_dgrad", "x3_fused"): "conv2_dgrad_x3_kernel<true>",
                   ("conv2_dgrad", "x3"): "conv2_dgrad_x3_kernel<false>",
                   ("conv2_fwd_pool", "x3_images"): "conv2_fwd_pool_x3_kernel<true>",
-                  ("conv2_wgrad", "x3_images"): "conv2_wgrad_x3q_kernel"}
+                  ("conv2_wgrad", "x3_images"): "conv2_wgrad_x3p_kernel"}
 
 
 def rocprof_avg(symbol, pattern="kernel_stats_k2.csv"):
@@ -229,10 +229,27 @@ def conv_roofline(name, avg_ms, B, impl):
         flops, peak = WINO_FLOP_PER_SAMPLE[name] * B, FP32_PEAK_TFLOPS
         algo = "Winograd F(2x2,3x3), f32 MFMA (flop_per_launch = its transform-domain GEMMs)"
     ach = flops / (avg_ms * 1e-3) / 1e12
-    return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": pmc_traffic(name + ("_x3" if impl == "x3" else ""), B),
-            "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "algorithm": algo,
-            "direct_conv_equivalent_tflops": round(direct_eq, 2)}
+    r = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+         "frac": round(ach / peak, 4), "traffic": pmc_traffic(name + ("_x3" if impl == "x3" else ""), B),
+         "flop_per_launch": flops, "avg_ms": round(avg_ms, 4), "algorithm": algo,
+         "direct_conv_equivalent_tflops": round(direct_eq, 2)}
+    if impl == "x3" and name == "conv2_wgrad" and wgrad_x3_form() == 2:
+        # round 6: the 2:4-sparse f16 MFMA issues half of those products (the routed dY's structural zeros are
+        # skipped); priced against the SPARSE peak (2x the dense one) the kernel's executed work sits at:
+        r["algorithm"] = ("direct implicit GEMM on v_smfmac_f32_16x16x64_f16 (2:4 sparse: dY has <= 2 nonzeros in "
+                          "every 4-pixel block of a row), f32 operands split hi/lo (3 products); flop_per_launch = "
+                          "the dense-equivalent f16 FLOPs (structural zeros included), half of them issued")
+        r["frac_of_sparse_peak"] = round(ach / (2 * peak), 4)
+    return r
+
+
+def wgrad_x3_form():
+    """slk_conv2_wgrad_x3_form() of the loaded library (2 = sparse MFMA, 1 = dense x3), None without one."""
+    try:
+        from splitcnn import _lib
+        return _lib.query("slk_conv2_wgrad_x3_form")
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def roofline_from(kern, B, impls=None, variants=None):
@@ -269,8 +286,9 @@ def roofline_from(kern, B, impls=None, variants=None):
                                             "hip_event_avg_ms": (pj.get("roofline") or {}).get("avg_ms")}
                 except (OSError, ValueError, KeyError, TypeError):
                     pass
-    r["per_kernel"] = {k: {kk: conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino"))[kk]
-                           for kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops")}
+    r["per_kernel"] = {k: {kk: vv for kk, vv in conv_roofline(k, v["avg_ms"], B, impls.get(k, "wino")).items()
+                           if kk in ("avg_ms", "achieved", "peak", "frac", "direct_conv_equivalent_tflops",
+                                     "frac_of_sparse_peak")}
                        for k, v in conv.items()}
     return r
 

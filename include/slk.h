@@ -183,6 +183,11 @@ int slk_conv2_fwd_pool_x3s(const float* act, const float* act_amax, const float*
                            uint8_t* code, uint16_t* act16, int B, void* stream);
 int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled, const float* dp_amax,
                         const uint8_t* code, float* slabs, int B, void* stream);
+/* Which kernel slk_conv2_wgrad_x3s runs (round 6): 2 = on the 2:4-sparse f16 MFMA (v_smfmac_f32_16x16x64_f16:
+ * the max-pool routing leaves at most 2 nonzeros of dY in every 4 consecutive output pixels of a row starting at
+ * a multiple of 4, so half the dense x3 products are never issued), 1 = the dense x3 kernel, 0 = the round-4
+ * kernel. Measurement only (bench.py prices the executed products against the matching peak). */
+int slk_conv2_wgrad_x3_form(void);
 /* slk_conv2_fwd_pool_x3s with the per-sample max |act| computed inside the forward (written to act_amax,
  * the values slk_row_amax gives) instead of read: the drop-in module path has no separate pass over the cut.
  * act 16-byte aligned. Replaces the row_amax + forward pair behind ModelPartB.forward (src/model_def.py:25-26). */

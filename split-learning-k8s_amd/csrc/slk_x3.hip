@@ -2486,6 +2486,8 @@ extern "C" int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const
     return slk_launch_status();
 }
 
+extern "C" int slk_conv2_wgrad_x3_form() { return SLK_X3W_ROUND4 ? 0 : (SLK_X3W_SPARSE ? 2 : 1); }
+
 extern "C" int slk_conv2_wgrad_x3s(const uint16_t* act16, const float* act_amax, const float* dpooled,
                                    const float* dp_amax, const uint8_t* code, float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && act16 && act_amax && dpooled && dp_amax && code && slabs);

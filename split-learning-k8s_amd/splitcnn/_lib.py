@@ -68,6 +68,7 @@ _SIGS = {
     "slk_mfma_probe": [_P, _I, _P],
     "slk_mfma_probe_blocks": [],
     "slk_conv2_wgrad_x3s": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "slk_conv2_wgrad_x3_form": [],
     "slk_conv2_act16_bytes": [_I],
     "slk_conv1_fwd_x3": [_P, _P, _P, _P, _P, _P, _P, _I, _P],
     "slk_relu_bits_bytes": [_I],
