@@ -88,6 +88,8 @@ def parse():
                     help="skip the short run of the other conv preset reported beside the headline")
     ap.add_argument("--no-images", action="store_true",
                     help="dense exchange of the f32 cut instead of the client's x3 split images (same bytes)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the reference's step code on the drop-in modules (side object)")
     ap.add_argument("--no-hub-loopback", action="store_true",
                     help="skip the 1-GPU loopback of the K4 hub server's compute (7 clients x --micro chunks)")
     return ap.parse_args()
@@ -1003,9 +1005,10 @@ def main():
                 out.setdefault("k4_server_loopback", {})["error"] = repr(e)[:300]
         try:
             import torch
-            X, Y = make_pool(args.batch, 4, torch.device("cuda:0"))
-            out["dropin_modules"] = run_dropin(X, Y, max(5, min(args.steps, 20)), 3)
-            del X, Y
+            if not args.no_dropin:
+                X, Y = make_pool(args.batch, 4, torch.device("cuda:0"))
+                out["dropin_modules"] = run_dropin(X, Y, max(5, min(args.steps, 20)), 3)
+                del X, Y
         except Exception as e:  # the headline stands on its own
             out["dropin_modules"] = {"error": repr(e)[:300]}
         if not args.no_k5:

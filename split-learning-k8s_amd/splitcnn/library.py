@@ -98,13 +98,14 @@ def _conv1_setup(ctx, inputs, output):
     ctx.save_for_backward(x, W1, b1)
 
 
-def _conv1_backward(ctx, g):
+def _conv1_backward(ctx, g, K=None):
+    K = K or torch.ops.splitcnn
     x, W1, b1 = ctx.saved_tensors
     if ctx.needs_input_grad[0]:
         raise NotImplementedError(
             "splitcnn: gradient w.r.t. the client INPUT images is not part of the split step "
             "(the reference's data never requires grad, src/client_part.py:110-114)")
-    flat = torch.ops.splitcnn.conv1_wgrad(x, W1, b1, g)
+    flat = K.conv1_wgrad(x, W1, b1, g)
     return None, flat[:288].view(32, 1, 3, 3), flat[288:].view(32)
 
 
@@ -229,7 +230,8 @@ def _conv2_setup(ctx, inputs, output):
     ctx.set_materialize_grads(False)
 
 
-def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16):
+def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16, K=None):
+    K = K or torch.ops.splitcnn
     if dpooled is None:   # pooled did not reach the loss (grads are not materialized, _conv2_setup)
         return None, None, None
     code, W2, *kept = ctx.saved_tensors
@@ -243,15 +245,14 @@ def _conv2_backward(ctx, dpooled, _dcode, _damax, _da16):
         if dpa is not None and not (dpooled.is_contiguous() and dpooled.shape[0] == dpa.numel()):
             dpa = None
         if dpa is None:
-            dpa = torch.ops.splitcnn.row_amax(dpooled)
+            dpa = K.row_amax(dpooled)
     gact = None
     if ctx.needs_input_grad[0]:
-        gact = (torch.ops.splitcnn.conv2_dgrad_x3(dpooled, code, W2, dpa) if di == "x3"
-                else torch.ops.splitcnn.conv2_dgrad(dpooled, code, W2))
+        gact = (K.conv2_dgrad_x3(dpooled, code, W2, dpa) if di == "x3" else K.conv2_dgrad(dpooled, code, W2))
     dW2 = db2 = None
     if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-        flat = (torch.ops.splitcnn.conv2_wgrad_x3(kept[0], kept[1], dpooled, dpa, code) if wi == "x3"
-                else torch.ops.splitcnn.conv2_wgrad(kept[0], dpooled, code))
+        flat = (K.conv2_wgrad_x3(kept[0], kept[1], dpooled, dpa, code) if wi == "x3"
+                else K.conv2_wgrad(kept[0], dpooled, code))
         dW2, db2 = flat[:18432].view(64, 32, 3, 3), flat[18432:].view(64)
     return gact, dW2, db2
 
@@ -302,15 +303,16 @@ def _linear_setup(ctx, inputs, output):
     ctx.save_for_backward(flat, W3)
 
 
-def _linear_backward(ctx, dlogits):
+def _linear_backward(ctx, dlogits, K=None):
+    K = K or torch.ops.splitcnn
     flat, W3 = ctx.saved_tensors
     dW3 = db3 = None
     # the weight gradient first: it re-reads flat (151 MB at B = 4096) while the forward's copy is still in
     # the Infinity Cache; the input gradient's 151 MB write would evict it (the fused step's order too)
     if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-        g = torch.ops.splitcnn.linear_wgrad(dlogits, flat)
+        g = K.linear_wgrad(dlogits, flat)
         dW3, db3 = g[:92160].view(10, 9216), g[92160:].view(10)
-    dflat = torch.ops.splitcnn.linear_dgrad(dlogits, W3) if ctx.needs_input_grad[0] else None
+    dflat = K.linear_dgrad(dlogits, W3) if ctx.needs_input_grad[0] else None
     return dflat, dW3, db3
 
 
@@ -354,9 +356,83 @@ def _xent_setup(ctx, inputs, output):
     ctx.save_for_backward(logits, labels)
 
 
-def _xent_backward(ctx, gloss):
+def _xent_backward(ctx, gloss, K=None):
+    K = K or torch.ops.splitcnn
     logits, labels = ctx.saved_tensors
-    return torch.ops.splitcnn.cross_entropy_grad(logits, labels, gloss), None
+    return K.cross_entropy_grad(logits, labels, gloss), None
 
 
 cross_entropy.register_autograd(_xent_backward, setup_context=_xent_setup)
+
+
+# ----------------------------------------------------------------------------------- eager fast path
+# The same implementations and backward formulas as the ops above, as plain autograd.Functions, for eager
+# calls on real tensors (the reference's own step code on the drop-in modules): a torch.library custom-op
+# call costs ~65 us of Python dispatch (CustomOpDef -> autograd_impl -> redispatch -> backend_impl), an
+# autograd.Function ~15 us, and after the step's loss.item() sync the client backward + the next client
+# forward sit on the GPU's critical path. Tracing (make_fx / torch.export / torch.compile: a dispatch mode,
+# fake or functional tensors) keeps the custom ops, so the traced graphs are unchanged; results are the same
+# kernels, bit for bit (tests/test_gpu_parity.py). SLK_EAGER_OPS=0 turns the fast path off.
+class _Direct:
+    """The ops' bodies without torch.library dispatch (the backward formulas' K for eager calls)."""
+
+
+for _n in ("conv1_wgrad", "row_amax", "conv2_dgrad", "conv2_dgrad_x3", "conv2_wgrad", "conv2_wgrad_x3",
+           "linear_dgrad", "linear_wgrad", "cross_entropy_grad"):
+    setattr(_Direct, _n, staticmethod(globals()[_n]._init_fn))
+_EAGER = os.environ.get("SLK_EAGER_OPS", "1") != "0"
+
+
+def eager(*ts) -> bool:
+    """True for an eager call on plain tensors (no dispatch mode, not compiling): the fast path applies."""
+    if not _EAGER or torch.compiler.is_compiling() or torch._C._len_torch_dispatch_stack() > 0:
+        return False
+    return all(type(t) in (torch.Tensor, torch.nn.Parameter) for t in ts)
+
+
+class Conv1ReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W1, b1):
+        out = conv1_relu._init_fn(x, W1, b1)
+        _conv1_setup(ctx, (x, W1, b1), out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return _conv1_backward(ctx, g, _Direct)
+
+
+class Conv2ReluPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, act, W2, b2):
+        out = conv2_relu_pool._init_fn(act, W2, b2)
+        _conv2_setup(ctx, (act, W2, b2), out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dpooled, dcode, damax, da16):
+        return _conv2_backward(ctx, dpooled, dcode, damax, da16, _Direct)
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, W3, b3):
+        out = linear._init_fn(flat, W3, b3)
+        _linear_setup(ctx, (flat, W3, b3), out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        return _linear_backward(ctx, dlogits, _Direct)
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        out = cross_entropy._init_fn(logits, labels)
+        _xent_setup(ctx, (logits, labels), out)
+        return out
+
+    @staticmethod
+    def backward(ctx, gloss):
+        return _xent_backward(ctx, gloss, _Direct)

@@ -4,7 +4,7 @@ Same class names, attribute names, state_dict keys, parameter shapes, default in
 consumption order (conv1, conv2, fc1 — src/model_def.py:8,18,22), and the same `get_model(role)`
 dispatch on LEARNING_MODE (src/model_def.py:49-71). What changes is where the arithmetic runs: every
 forward and backward goes through the hand-written gfx950 kernels of libslk.so via the autograd
-Functions below. The nn.Conv2d / nn.Linear submodules are kept ONLY as parameter containers (so
+Functions below (eager calls: autograd.Functions over the same implementations, library.eager). The nn.Conv2d / nn.Linear submodules are kept ONLY as parameter containers (so
 `model.conv1.weight`, `load_state_dict` and default init behave exactly as in the reference); their
 own forward is never called. Modules must live on a ROCm device; CPU tensors raise. The ops are
 registered with torch.library (library.py), with fake kernels, so the modules also trace under
@@ -29,8 +29,23 @@ from . import ops
 # registrations with fake kernels and autograd formulas over libslk.so), so the modules trace under
 # torch.export / make_fx as opaque differentiable operators.
 from . import library  # noqa: E402,F401  (registers torch.ops.splitcnn.*)
+from .library import Conv1ReluFn, Conv2ReluPoolFn, CrossEntropyFn, LinearFn, eager  # noqa: E402
 
 _OPS = torch.ops.splitcnn
+
+
+# eager calls on plain tensors take the same kernels through autograd.Functions (library.eager: less Python
+# dispatch on the step's critical path); traced / exported / compiled calls go through the custom ops
+def _conv1(x, W, b):
+    return Conv1ReluFn.apply(x, W, b) if eager(x, W, b) else _OPS.conv1_relu(x, W, b)
+
+
+def _conv2(x, W, b):
+    return (Conv2ReluPoolFn.apply(x, W, b) if eager(x, W, b) else _OPS.conv2_relu_pool(x, W, b))[0]
+
+
+def _linear(f, W, b):
+    return LinearFn.apply(f, W, b) if eager(f, W, b) else _OPS.linear(f, W, b)
 
 
 # ----------------------------------------------------------------------------- modules
@@ -51,7 +66,7 @@ class ModelPartA(nn.Module):
 
     def forward(self, x):
         _require_device(x, "ModelPartA")
-        return _OPS.conv1_relu(x, self.conv1.weight, self.conv1.bias)
+        return _conv1(x, self.conv1.weight, self.conv1.bias)
 
 
 class ModelPartB(nn.Module):
@@ -67,8 +82,8 @@ class ModelPartB(nn.Module):
 
     def forward(self, x):
         _require_device(x, "ModelPartB")
-        pooled = _OPS.conv2_relu_pool(x, self.conv2.weight, self.conv2.bias)[0]
-        return _OPS.linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
+        pooled = _conv2(x, self.conv2.weight, self.conv2.bias)
+        return _linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
 
 
 class FullModel(nn.Module):
@@ -85,9 +100,9 @@ class FullModel(nn.Module):
 
     def forward(self, x):
         _require_device(x, "FullModel")
-        act = _OPS.conv1_relu(x, self.conv1.weight, self.conv1.bias)
-        pooled = _OPS.conv2_relu_pool(act, self.conv2.weight, self.conv2.bias)[0]
-        return _OPS.linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
+        act = _conv1(x, self.conv1.weight, self.conv1.bias)
+        pooled = _conv2(act, self.conv2.weight, self.conv2.bias)
+        return _linear(pooled.view(pooled.shape[0], 9216), self.fc1.weight, self.fc1.bias)
 
 
 class CrossEntropyLoss(nn.Module):
@@ -95,7 +110,7 @@ class CrossEntropyLoss(nn.Module):
 
     def forward(self, logits, labels):
         _require_device(logits, "CrossEntropyLoss")
-        return _OPS.cross_entropy(logits, labels)
+        return CrossEntropyFn.apply(logits, labels) if eager(logits, labels) else _OPS.cross_entropy(logits, labels)
 
 
 def get_model(role="client"):

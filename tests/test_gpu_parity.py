@@ -107,6 +107,48 @@ def test_dropin_modules_reference_code(gpu, name):
         assert weight_ok(sd[f"{mod}.{attr}"].cpu().numpy(), fx[f"post_{k}_1"], fx[f"init_{k}"]), k
 
 
+@pytest.mark.parametrize("B", [4, 300])
+def test_dropin_eager_fast_path_bitwise_vs_custom_ops(gpu, B):
+    """Eager calls of the drop-in modules take autograd.Functions over the same op bodies (library.eager: less
+    Python dispatch per call); with the fast path off every call goes through the torch.library custom ops.
+    Three steps of the reference's step code (client_part.py:112-133, server_part.py:45-57) each way: every
+    activation, loss, cut gradient and parameter bit for bit the same, and the fast path really was taken."""
+    from splitcnn import library
+    from splitcnn.data import SyntheticMNIST, init_models
+    from splitcnn.model_def import CrossEntropyLoss
+    data = SyntheticMNIST(12)
+    batches = [tuple(t.to(gpu) for t in data.batch(B)) for _ in range(3)]
+    runs = []
+    for fast in (True, False):
+        old = library._EAGER
+        library._EAGER = fast
+        try:
+            client_m, server_m = (m.to(gpu) for m in init_models(seed=4))
+            copt = torch.optim.SGD(client_m.parameters(), lr=0.01)
+            sopt = torch.optim.SGD(server_m.parameters(), lr=0.01)
+            crit = CrossEntropyLoss()
+            rec = []
+            for x, y in batches:
+                copt.zero_grad()
+                activations = client_m(x)
+                assert (type(activations.grad_fn).__name__.startswith("Conv1ReluFn")) == fast
+                ca = activations.clone().detach()
+                ca.requires_grad_(True)
+                sopt.zero_grad()
+                loss = crit(server_m(ca), y)
+                loss.backward()
+                sopt.step()
+                cut = ca.grad.clone().detach()
+                activations.backward(cut)
+                copt.step()
+                rec += [activations.detach().clone(), loss.detach().clone(), cut]
+            rec += [p.detach().clone() for p in list(client_m.parameters()) + list(server_m.parameters())]
+            runs.append(rec)
+        finally:
+            library._EAGER = old
+    assert all(torch.equal(a, b) for a, b in zip(*runs))
+
+
 def test_fullmodel_matches_split(gpu):
     from splitcnn.data import init_models
     from splitcnn.model_def import CrossEntropyLoss
