@@ -1821,11 +1821,29 @@ constexpr int X3P_ITEMS = C2 * 12;                             // (co, window ro
 constexpr int X3P_SBN = (163840 - 2 * X3P_BUF) / 4;            // per-sample scale table entries (11,264)
 static_assert(2 * X3P_BUF <= 163840 && X3P_ITEMS <= 2 * X3P_THREADS && X3P_ITEMS > X3P_THREADS, "x3p layout");
 
+#ifndef SLK_X3P_BAL
+#define SLK_X3P_BAL 0  // measured: 0.1677 vs 0.1648 ms unbalanced (profiles/r06_ab_wgrad_balance.txt): not the limiter
+#endif
+// Work of the four wave types (TGI = 2 ((wave >> 1) & 1) + (wave >> 2); ci half = wave & 1): (tap, M tiles) items,
+// 4 M tiles = all 64 co. Waves w and w + 4 share a SIMD, so SIMDs 0-1 carry TGI 0 + 1 and SIMDs 2-3 TGI 2 + 3.
+// Taps 0-2 | 3-4 | 5-6 | 7-8 gave them 5 and 4 taps (20 vs 16 (tap, M tile) items: the lighter SIMDs waited
+// at every unit barrier); BAL moves tap 2's M tiles 2-3 from TGI 0 to TGI 2: 18 items per SIMD.
+template <int TGI>
+struct X3pTaps {
+    static constexpr bool BAL = SLK_X3P_BAL;
+    static constexpr int NT = (TGI == 0 || (TGI == 2 && BAL)) ? 3 : 2;
+    static constexpr int tap(int t) {
+        return TGI == 0 ? t : (TGI == 1 ? 3 + t : (TGI == 2 ? (t < 2 ? 5 + t : 2) : 7 + t));
+    }
+    static constexpr int mlo(int t) { return (TGI == 2 && t == 2) ? 2 : 0; }
+    static constexpr int mhi(int t) { return (TGI == 0 && t == 2 && BAL) ? 2 : 4; }
+};
+
 template <int TGI, class F>
 __device__ __forceinline__ void x3p_steps(const char* img, const int (&pb)[X3P_STEPS][4], const int (&sw)[3], int arec,
                                           int aidx, f32x4 (&acc)[3][4], F&& after_step) {
-    constexpr int T0 = TGI == 0 ? 0 : (TGI == 1 ? 3 : (TGI == 2 ? 5 : 7));
-    constexpr int NT = TGI == 0 ? 3 : 2;
+    using TT = X3pTaps<TGI>;
+    constexpr int NT = TT::NT;
     typedef __fp16 hf4 __attribute__((__vector_size__(8)));
     typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
     typedef _Float16 f16x16 __attribute__((ext_vector_type(16)));
@@ -1843,9 +1861,7 @@ __device__ __forceinline__ void x3p_steps(const char* img, const int (&pb)[X3P_S
         }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            constexpr int dummy = 0;
-            (void)dummy;
-            const int tap = T0 + t, ky = tap / 3, kx = tap % 3;
+            const int tap = TT::tap(t), ky = tap / 3, kx = tap % 3;
             f16x4 bh[4], bl[4];
 #pragma unroll
             for (int jb = 0; jb < 4; ++jb) {
@@ -1860,7 +1876,7 @@ __device__ __forceinline__ void x3p_steps(const char* img, const int (&pb)[X3P_S
                                                       __builtin_shufflevector(bl[2], bl[3], 0, 1, 2, 3, 4, 5, 6, 7),
                                                       0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
+            for (int mt = TT::mlo(t); mt < TT::mhi(t); ++mt) {
                 f32x4 c = acc[t][mt];
                 c = __builtin_amdgcn_smfmac_f32_16x16x64_f16(ah[mt], Bh, c, ix[mt], 0, 0);
                 c = __builtin_amdgcn_smfmac_f32_16x16x64_f16(ah[mt], Bl, c, ix[mt], 0, 0);
@@ -2131,17 +2147,22 @@ __global__ __launch_bounds__(X3P_THREADS, 1) void conv2_wgrad_x3p_kernel(
     }
     const float us1 = ldexpf(1.f, -sx), us2 = ldexpf(1.f, -sd);
     const int ci = 16 * h + (lane & 15);
-    const int T0 = tgi == 0 ? 0 : (tgi == 1 ? 3 : (tgi == 2 ? 5 : 7)), nt = tgi == 0 ? 3 : 2;
+    auto write_slab = [&](auto TG) {
+        using TT = X3pTaps<decltype(TG)::value>;
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
-        if (t < nt)
+        for (int t = 0; t < TT::NT; ++t)
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
+            for (int mt = TT::mlo(t); mt < TT::mhi(t); ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int co = 16 * mt + 4 * (lane >> 4) + r;
-                    slab[(co * C1 + ci) * 9 + T0 + t] = x3_unscale(acc[t][mt][r], us1, us2);
+                    slab[(co * C1 + ci) * 9 + TT::tap(t)] = x3_unscale(acc[t][mt][r], us1, us2);
                 }
+    };
+    if (tgi == 0) write_slab(std::integral_constant<int, 0>{});
+    else if (tgi == 1) write_slab(std::integral_constant<int, 1>{});
+    else if (tgi == 2) write_slab(std::integral_constant<int, 2>{});
+    else write_slab(std::integral_constant<int, 3>{});
 }
 
 // ============================================================================ conv1 -> x3 input images
