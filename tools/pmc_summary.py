@@ -57,7 +57,11 @@ if args.traffic_out:
                   "conv2_fwd_pool_x3_kernel<false>": "conv2_fwd_pool_x3_f32in",
                   "conv2_wgrad_x3_kernel<true>": "conv2_wgrad_x3", "conv2_wgrad_x3_kernel<false>": "conv2_wgrad_x3_gather",
                   "conv1_fwd_x3_kernel": "conv1_fwd",
-                  "conv2_dgrad_x3_kernel<true>": "conv2_dgrad_x3", "conv2_dgrad_x3_kernel<false>": "conv2_dgrad_x3_cut"})
+                  "conv2_dgrad_x3_kernel<true>": "conv2_dgrad_x3", "conv2_dgrad_x3_kernel<false>": "conv2_dgrad_x3_cut",
+                  # round 5-6: the images wgrad (dense x3q, then the 2:4-sparse x3p) and the split fc head
+                  "conv2_wgrad_x3q_kernel": "conv2_wgrad_x3", "conv2_wgrad_x3p_kernel": "conv2_wgrad_x3",
+                  "conv1_fwd_x3_kernel<true, false>": "conv1_fwd", "conv2_fwd_pool_x3_kernel<true, false>": "conv2_fwd_pool_x3",
+                  "fc_head16_kernel<1>": "fc_logits", "fc_head16_kernel<4>": "fc_dgrad"})
     # widened (K5) template instantiations -> bench.py's kernel names (csrc/slk_wide.hip:824-836, 1055)
     wide = [("wide_conv32_kernel<Conv32Cfg<64, 128, 32", "wide_conv2_fwd"),
             ("wide_conv_kernel<ConvCfg<64, 128, 32", "wide_conv2_fwd"),
