@@ -656,6 +656,14 @@ static_assert(2 * X3D_IMG <= 163840, "LDS");
 #ifndef SLK_X3D_TRACE
 #define SLK_X3D_TRACE 0
 #endif
+// the fused dgrad's client epilogue on the f16 MFMA (split operands) instead of the f32 MFMA
+#ifndef SLK_X3D_EPI16
+#define SLK_X3D_EPI16 0
+#endif
+// profiling only (wrong results): bit 1 no dY staging, bit 2 no client epilogue, bit 4 its f32 MFMAs as one fma
+#ifndef SLK_X3D_ABL
+#define SLK_X3D_ABL 0
+#endif
 #if SLK_X3D_TRACE
 // profiling probe: per (workgroup, wave, unit) shader-clock stamps of the dgrad's phases (lane 0, vector stores)
 __device__ unsigned long long g_x3d_trace[256 * 8 * 128 * 8];
@@ -966,6 +974,35 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 ++y0;
             }
         }
+#if SLK_X3D_EPI16
+        // the same GEMM on the f16 MFMA: g (scaled by 2^-22: |g| < 576 * 2^28 before it, so hi < 36,864)
+        // and x split hi/lo, K = the lane group's 8 (tile, r) pixels per instruction, 2 hi*hi + 4 cross
+        // products in two chains from zero per pair (the accumulation-bias note above)
+        f16x8 gh[2], gl[2], bh[2], bl[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            float gv[8], xw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = 2 * s + (j >> 2), r = j & 3;
+                gv[j] = __uint_as_float(__float_as_uint(acc[i][r]) & (0u - ((mw[i] >> r) & 1u)));
+                xw[j] = xv[i][r];
+            }
+            x3_split8(gv, 0x1p-22f, gh[s], gl[s]);
+            x3_split8(xw, 1.f, bh[s], bl[s]);
+        }
+        f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f}, dc = f32x4{0.f, 0.f, 0.f, 0.f};
+        slk_keep(dh);
+        slk_keep(dc);
+        dh = mfma_f16(gh[0], bh[0], dh);
+        dc = mfma_f16(gh[0], bl[0], dc);
+        dh = mfma_f16(gh[1], bh[1], dh);
+        dc = mfma_f16(gl[0], bh[0], dc);
+        dc = mfma_f16(gh[1], bl[1], dc);
+        dc = mfma_f16(gl[1], bh[1], dc);
+        d1s[tid] = d1s[tid] + (dh + dc) * (us1e * 0x1p22f);
+        return;
+#endif
         f32x4 dr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -981,7 +1018,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                     const uint32_t keep = 0u - ((mw[i] >> r) & 1u);
                     // (by value: __builtin_bit_cast of the vector element acc[i][r] read one element for all r)
                     const float gm = __uint_as_float(__float_as_uint(acc[i][r]) & keep);
+#if SLK_X3D_ABL & 4
+                    dr[r][0] = fmaf(gm, xv[i][r], dr[r][0]);
+#else
                     dr[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(gm, xv[i][r], dr[r], 0, 0, 0);
+#endif
                 }
             }
         }
@@ -1027,7 +1068,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
             // the next unit's dY (always: past the last unit it stages a clamped valid unit, unused).
             // Half the waves stage before their MFMAs, half after, so the two waves of a SIMD overlap
             // one's staging with the other's MFMAs (both staging at once left the SIMD's MFMA idle).
-            if (sfirst) {
+            if (sfirst && !(SLK_X3D_ABL & 1)) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
@@ -1054,7 +1095,7 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 if (st + 3 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
             X3D_TS(k, 2);
-            if (!sfirst) {
+            if (!sfirst && !(SLK_X3D_ABL & 1)) {
                 store_dy(unx, nimg);
                 load_dy(unx2);
             }
@@ -1082,7 +1123,11 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
         // epilogue: unscale (exact) and store 4 consecutive pixels per lane
         const float us1 = ldexpf(1.f, -x3_exp(amax_b)), us2 = ldexpf(1.f, -sw);
         if constexpr (C1W) {
-            c1w_epi(T0, T1, us1, q);
+            if (!(SLK_X3D_ABL & 2)) c1w_epi(T0, T1, us1, q);
+            else {
+#pragma unroll
+                for (int i = 0; i < X3D_MPW; ++i) slk_keep(acc[i]);  // the MFMA stream stays live
+            }
             X3D_TS(k - 1, 5);
         } else if (pack) {
             // the lane's 4 pixels are 4 consecutive elements of one mask word (A_PIX and p are multiples of 4);
