@@ -245,6 +245,14 @@ def conv_roofline(name, avg_ms, B, impl):
     return r
 
 
+def _query_or_none(name):
+    try:
+        from splitcnn import _lib
+        return _lib.query(name)
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def wgrad_x3_form():
     """slk_conv2_wgrad_x3_form() of the loaded library (2 = sparse MFMA, 1 = dense x3), None without one."""
     try:
@@ -525,6 +533,17 @@ def run_wide(args, B, steps, warmup, kernel_pass_on=True):
         r["roofline"] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(name, B),
                          "flop_per_launch": WIDE_CONV_FLOP[name] * B, "avg_ms": round(conv[name]["avg_ms"], 4)}
+        # every conv kernel on its direct-convolution FLOPs; the weight gradients on the 2:4-sparse MFMA (round 6)
+        # execute half the products as sparse instructions: also priced against the sparse peak (2x dense)
+        sparse_wg = _query_or_none("slk_wide_wgrad_form") == 1
+        per = {}
+        for k, v in sorted(conv.items(), key=lambda kv: -kv[1]["avg_ms"]):
+            a_k = WIDE_CONV_FLOP[k] * B / (v["avg_ms"] * 1e-3) / 1e12
+            per[k] = {"achieved": round(a_k, 1), "frac": round(a_k / BF16_PEAK_TFLOPS, 4), "avg_ms": round(v["avg_ms"], 4)}
+            if sparse_wg and k.endswith("_wgrad") and k != "wide_conv1_wgrad":
+                per[k]["frac_of_sparse_peak"] = round(a_k / (2 * BF16_PEAK_TFLOPS), 4)
+                per[k]["algorithm"] = "v_smfmac_f32_16x16x64_bf16 on the max-pool-routed dC (2 of every 4 pixels)"
+        r["roofline"]["per_kernel"] = per
         r["conv_tflops"] = {k: round(WIDE_CONV_FLOP[k] * B / (v["avg_ms"] * 1e-3) / 1e12, 1) for k, v in conv.items()}
     return r
 

@@ -384,6 +384,8 @@ int slk_wide_conv3_dgrad(const uint16_t* dcut, const uint8_t* code3, const uint1
 int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
                          void* stream);
 int slk_wide_conv2_wgrad_nslab(int B);
+/* 1 when the K5 weight gradients run on the 2:4-sparse bf16 MFMA (the max-pool-routed dC), 0 dense. */
+int slk_wide_wgrad_form(void);
 int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* w2d, const uint64_t* a1bits,
                          uint16_t* da1m, int B, void* stream);
 int slk_wide_conv1_wgrad(const float* x, const uint16_t* da1m, float* slabs, int B, void* stream);

@@ -976,6 +976,13 @@ extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, c
 // one wait + barrier per tile). db rides along as one MFMA per step against a ones fragment. Each
 // workgroup writes its partial dW/db into its own slab (torch layout [co][ci][3][3] | db), reduced in
 // fixed order by slk_reduce_slabs / slk_adam_from_slabs.
+// SP (round 6, the default): dC is the max-pool backward of a pooled gradient, so in every block of 4
+// consecutive pixels of one row (x % 4 == 0: two pool windows' columns) at most 2 values per co are nonzero —
+// the 2:4 structure of v_smfmac_f32_16x16x64_bf16 (layout measured on the f16 form: slk_x3.hip's x3p notes,
+// tools/ubench/smfmac_probe.hip). The staging writes dC as compressed records (the exact register image of a
+// lane's A fragment: 8 bf16 + a u16 index word) instead of the dense tile, and each K64 step issues 4 x 9
+// sparse instructions instead of 2 x 4 x 9 dense ones on the same B fragments: the same products, summed in
+// another order (slabs within ~1e-8 of the dense form's).
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 template <int CI_, int CO_, int HW_, int TR_, int EXP_ = 0>
@@ -1002,17 +1009,27 @@ struct WgCfg {
     static constexpr int RB = HW / TR;
     static constexpr int SLAB = CO * CI * 9 + CO;
     static constexpr int KSPLIT = 256 / NBLK;            // one workgroup per CU
+    // SP (the 2:4-sparse form, wide_wgrad_kernel<C, true>): the tile's dC as compressed records
+    // [K64 step][ga 4][co 128][8 bf16] + u16 index words [step][ga][co], then the input tile
+    static constexpr int KS64 = NPX / 64;
+    static constexpr int SREC = KS64 * 4 * COB * 16, SIDX = KS64 * 4 * COB * 2;
+    static constexpr int SDC = (SREC + SIDX + 1023) / 1024 * 1024;
+    static constexpr int SBUF = SDC + IN_BYTES;
     static_assert(NPX % 32 == 0 && (HW == 32 || HW == 16), "tile");
+    static_assert(!EXP || (NPX == 128 && COB == 128 && (HW == 32 ? TR == 4 : TR == 8)), "SP staging geometry");
     static_assert(DC_BYTES % 16 == 0 && ((NPX * 16) % 1024) == 0, "dC rows move in whole KiB");
     static_assert(!EXP || XITEMS == 512, "EXP: one pooled chunk per thread");
 };
 
-template <class C>
+template <class C, bool SP = false>
 __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __restrict__ dc,
                                                             const uint16_t* __restrict__ in,
                                                             float* __restrict__ slabs, int B,
                                                             const uint8_t* __restrict__ dcode = nullptr) {
-    __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+    static_assert(!SP || C::EXP, "the sparse form stages dC from the pooled gradient");
+    constexpr int BUF = SP ? C::SBUF : C::BUF;           // one of the two tile buffers
+    constexpr int DCB = SP ? C::SDC : C::DC_BYTES;       // offset of the input tile in a buffer
+    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + C::RAW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = wave >> 1;
@@ -1028,7 +1045,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     const int a_base = (((wm * 64 + 4 * p) >> 3) * C::NPXP + 8 * q + a) * 16 + (p & 1) * 8;
     const int pl = 8 * q + a, r0 = pl / C::HW, x0 = pl % C::HW;
     // wave wn owns input channels cib*64 + 16*wn .. +15 (chunks 2wn, 2wn+1) for all 9 taps
-    const int b_base = C::DC_BYTES + (((2 * wn + (p >> 1)) * C::NPI) + (r0 + 1) * C::PW + x0 + 1) * 16 + (p & 1) * 8;
+    const int b_base = DCB + (((2 * wn + (p >> 1)) * C::NPI) + (r0 + 1) * C::PW + x0 + 1) * 16 + (p & 1) * 8;
     const bool do_db = cib == 0;
     const short one = 0x3F80;  // bf16 1.0
     const bf16x8 ones = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(8))) short){one, one, one, one, one, one, one, one});
@@ -1059,7 +1076,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     };
     // EXP: pooled dC chunk tid = (plane c, pooled row pr, pooled col px) of tile t, staged by this
     // thread's own wave (LDS-DMA into `raw`), so its expansion needs only that wave's vmcnt wait
-    char* raw = smem + 2 * C::BUF;
+    char* raw = smem + 2 * BUF;
     auto exp_issue_dc = [&](int t) {
         int n, rb;
         tile_of(t, n, rb);
@@ -1113,7 +1130,63 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
             const int y = rb * C::TR - 1 + ry, x = rx - 1;
             const bool ok = P < C::NP && y >= 0 && y < C::HW && x >= 0 && x < C::HW;
             const char* src = ok ? plane + (size_t)(y * C::HW + x) * 16 : reinterpret_cast<const char*>(slk_wide_zero);
-            glds16((const void*)src, lds_u32(buf + C::DC_BYTES + wave * C::NPI * 16 + d * 1024));
+            glds16((const void*)src, lds_u32(buf + DCB + wave * C::NPI * 16 + d * 1024));
+        }
+    };
+
+    // SP geometry. K64 step s of a tile = 16 blocks of 4 pixels of one row (x % 4 == 0): block L = 16 s + 4 gb + jb
+    // is row y, block xb (pixels 4 xb .. +3) with, for HW = 32, y = 2 s + (gb >> 1), xb = 2 (gb & 1) + (jb & 1) +
+    // 4 (jb >> 1); for HW = 16, y = 4 s + 2 (gb >> 1) + (jb >> 1), xb = 2 (gb & 1) + (jb & 1). So blocks jb, jb + 1
+    // (one record half) are adjacent (a window quad), and the two lane groups gb = 0, 1 of a 32-lane half of a
+    // B read are 8 pixels (128 B) apart: their transposed reads hit disjoint banks.
+    // B (input tile, ds_read_b64_tr_b16): lane (gb, ig = 4 a + p) reads pixel 4 xb + a of row y, chunk plane
+    // 2 wn + (p >> 1), 8-B half p & 1 (as the dense read): one read per block, 4 per fragment.
+    // one per-lane base (block L = 4 gb) + a compile-time offset per (s, jb)
+    const int spb0 = DCB + (((2 * wn + (p >> 1)) * C::NPI) + ((C::HW == 32 ? (q >> 1) : 2 * (q >> 1)) + 1) * C::PW +
+                            8 * (q & 1) + a + 1) * 16 + (p & 1) * 8;
+    auto spb_off = [](int st, int jb) {
+        return C::HW == 32 ? (2 * st * C::PW + 4 * (jb & 1) + 16 * (jb >> 1)) * 16
+                           : ((4 * st + (jb >> 1)) * C::PW + 4 * (jb & 1)) * 16;
+    };
+    // A: lane (ga = q, m = ig) of M tile i reads record (s, ga, co = 64 wm + 16 i + m) and its index word
+    const int sp_arec = ((q * C::COB) + wm * 64 + ig) * 16, sp_aidx = C::SREC + ((q * C::COB) + wm * 64 + ig) * 2;
+    // SP staging: thread (wave w, lane l) = items (co = 8 c + (l & 7), c = 2 w + k, k = 0, 1; pooled row pr; window quad
+    // P): the quad's 4 windows (pooled px = 4 P .. +3, the raw items this wave's own DMA staged) are the two blocks
+    // 2 P, 2 P + 1 of output rows 2 pr + d, i.e. one record half (8 B) + one index byte per d. Lane bits 0-2 = co,
+    // bit 3 = the half (P & 1): a 16-lane ds_write_b64 group covers 16 distinct 8-B slots of 128 B.
+    const int sco = lane & 7, sP0 = (lane >> 3) & 1, srest = lane >> 4;
+    const int spr = C::HW == 32 ? (srest & 1) : srest, sP = C::HW == 32 ? sP0 + 2 * (srest >> 1) : sP0;
+    auto sp_expand = [&](char* buf) {
+        constexpr int PH = C::HW / 2, PR = C::TR / 2;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = 2 * wave + k, co = 8 * c + sco;
+            const int i0 = c * (PR * PH) + spr * PH + 4 * sP;
+            const char* rv = raw + i0 * 16 + sco * 2;
+            const char* rc = raw + C::XITEMS * 16 + (sco >> 2) * C::XITEMS * 4 + i0 * 4 + (sco & 3);
+            uint32_t v[4], cb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = *reinterpret_cast<const uint16_t*>(rv + j * 16);
+                cb[j] = *reinterpret_cast<const uint8_t*>(rc + j * 4);
+            }
+            const uint32_t cw = cb[0] | (cb[1] << 8) | (cb[2] << 16) | (cb[3] << 24);
+            // index byte: window j's position in its block = its dx (code bit 0), + 2 for the block's second window
+            // (a window routed elsewhere keeps that position with a zero value)
+            const uint32_t ib = (cw & 1u) | ((cw >> 6) & 4u) | ((cw >> 12) & 16u) | ((cw >> 18) & 64u) | 0x88u;
+            const uint32_t rowp = (cw >> 1) & 0x7F7F7F7Fu;  // per byte: 0 / 1 = routed row parity, 2 = blocked
+            const uint32_t H0 = v[0] | (v[1] << 16), H1 = v[2] | (v[3] << 16);
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                const uint32_t z = (d ? (rowp & ~(rowp >> 1)) : ~(rowp | (rowp >> 1))) & 0x01010101u;
+                const uint32_t m8 = z * 0xFFu;
+                const uint32_t mA = __builtin_amdgcn_perm(0u, m8, 0x01010000u), mB = __builtin_amdgcn_perm(0u, m8, 0x03030202u);
+                const int ga = C::HW == 32 ? 2 * (sP >> 1) + d : 2 * d + (spr & 1);
+                const int st = C::HW == 32 ? spr : spr >> 1;
+                const int rec = (st * 4 + ga) * C::COB + co;
+                *reinterpret_cast<uint2*>(buf + rec * 16 + sP0 * 8) = make_uint2(H0 & mA, H1 & mB);
+                buf[C::SREC + rec * 2 + sP0] = (char)ib;
+            }
         }
     };
 
@@ -1123,7 +1196,8 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         if constexpr (C::EXP) {
             exp_issue_dc(t);
             wait_vmcnt<0>();
-            exp_expand_dc(smem);
+            if constexpr (SP) sp_expand(smem);
+            else exp_expand_dc(smem);
         }
     }
 #pragma unroll 1
@@ -1134,12 +1208,49 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         asm volatile("" ::: "memory");
         const bool more = valid(t + C::KSPLIT);
         if (more) {
-            issue_tile(t + C::KSPLIT, smem + (b ^ 1) * C::BUF);
+            issue_tile(t + C::KSPLIT, smem + (b ^ 1) * BUF);
             if constexpr (C::EXP) exp_issue_dc(t + C::KSPLIT);
         }
-        const char* buf = smem + b * C::BUF;
+        const char* buf = smem + b * BUF;
+        if constexpr (SP) {
+            typedef __attribute__((address_space(3))) bf16x4* lp4;
+            typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
+            const bf16x16 ones16 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
 #pragma unroll
-        for (int j = 0; j < C::KS; ++j) {
+            for (int st = 0; st < C::KS64; ++st) {
+                bf16x8 av[4];
+                int ix[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    av[i] = *reinterpret_cast<const bf16x8*>(buf + sp_arec + st * 4 * C::COB * 16 + i * 256);
+                    ix[i] = *reinterpret_cast<const uint16_t*>(buf + sp_aidx + st * 4 * C::COB * 2 + i * 32);
+                }
+                if (do_db) {  // wave (wm, wn) sums co fragment wn
+                    bf16x8 adb = av[0];
+                    int idb = ix[0];
+#pragma unroll
+                    for (int i = 1; i < 4; ++i) {
+                        adb = wn == i ? av[i] : adb;
+                        idb = wn == i ? ix[i] : idb;
+                    }
+                    accb = __builtin_amdgcn_smfmac_f32_16x16x64_bf16(adb, ones16, accb, idb, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 9; ++u) {  // u = tap
+                    const int toff = ((u / 3 - 1) * C::PW + (u % 3 - 1)) * 16;
+                    bf16x4 r4[4];
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb) r4[jb] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(buf + spb0 + spb_off(st, jb) + toff));
+                    const bf16x16 bv = __builtin_shufflevector(__builtin_shufflevector(r4[0], r4[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                               __builtin_shufflevector(r4[2], r4[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                                               0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i][u] = __builtin_amdgcn_smfmac_f32_16x16x64_bf16(av[i], bv, acc[i][u], ix[i], 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < (SP ? 0 : C::KS); ++j) {
             typedef __attribute__((address_space(3))) bf16x4* lp4;
             bf16x8 av[4];
 #pragma unroll
@@ -1173,7 +1284,8 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         if constexpr (C::EXP) {
             if (more) {
                 wait_vmcnt<0>();
-                exp_expand_dc(smem + (b ^ 1) * C::BUF);
+                if constexpr (SP) sp_expand(smem + (b ^ 1) * BUF);
+                else exp_expand_dc(smem + (b ^ 1) * BUF);
             }
         }
         b ^= 1;
@@ -1200,6 +1312,10 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     }
 }
 
+// the K5 weight gradients on the 2:4-sparse bf16 MFMA (wide_wgrad_kernel<C, true>; 0: the dense form)
+#ifndef SLK_WIDE_WG_SPARSE
+#define SLK_WIDE_WG_SPARSE 1
+#endif
 using CfgWg2 = WgCfg<64, 128, 32, 4, 1>;   // dC = routed dp2 (EXP)
 using CfgWg3 = WgCfg<128, 256, 16, 8, 1>;   // dC = routed dcut (EXP)
 
@@ -1207,11 +1323,13 @@ template <class C>
 static int launch_wgrad(const uint16_t* dc, const uint16_t* in, float* slabs, int B, void* stream,
                         const uint8_t* dcode = nullptr) {
     SLK_CHECK_ARG(B >= 0 && dc && in && slabs && (!C::EXP || dcode));
-    hipLaunchKernelGGL(wide_wgrad_kernel<C>, dim3(256), dim3(512), 0, slk_stream(stream), dc, in, slabs, B, dcode);
+    hipLaunchKernelGGL((wide_wgrad_kernel<C, SLK_WIDE_WG_SPARSE != 0>), dim3(256), dim3(512), 0, slk_stream(stream), dc, in,
+                       slabs, B, dcode);
     return slk_launch_status();
 }
 
 extern "C" int slk_wide_conv2_wgrad_nslab(int B) { return B >= 0 ? CfgWg2::KSPLIT : 0; }
+extern "C" int slk_wide_wgrad_form() { return SLK_WIDE_WG_SPARSE ? 1 : 0; }
 extern "C" int slk_wide_conv3_wgrad_nslab(int B) { return B >= 0 ? CfgWg3::KSPLIT : 0; }
 extern "C" int slk_wide_conv2_wgrad(const uint16_t* dp2, const uint8_t* code2, const uint16_t* a1, float* slabs, int B,
                                     void* stream) {

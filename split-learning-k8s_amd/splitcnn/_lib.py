@@ -97,6 +97,7 @@ _SIGS = {
     "slk_wide_conv3_dgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv2_wgrad": [_P, _P, _P, _P, _I, _P],
     "slk_wide_conv2_wgrad_nslab": [_I],
+    "slk_wide_wgrad_form": [],
     "slk_wide_conv2_dgrad": [_P, _P, _P, _P, _P, _I, _P],
     "slk_wide_conv1_wgrad": [_P, _P, _P, _I, _P],
     "slk_wide_conv1_wgrad_nslab": [_I],

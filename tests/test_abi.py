@@ -47,6 +47,13 @@ def test_slab_counts_are_functions_of_batch_only():
     assert ops.conv2_wgrad_nslab(0) == 0
 
 
+def test_shipped_kernel_forms():
+    """The default build's weight gradients run on the 2:4-sparse MFMA (K2 x3 images wgrad: form 2; K5: 1)."""
+    from splitcnn import _lib
+    assert _lib.query("slk_conv2_wgrad_x3_form") == 2
+    assert _lib.query("slk_wide_wgrad_form") == 1
+
+
 def test_ops_refuse_cpu_tensors():
     from splitcnn import ops
     with pytest.raises(RuntimeError, match="no CPU fallback"):

@@ -146,6 +146,9 @@ for name, ts in outs.items():
         assert calls(L)[name]() == 0
         torch.cuda.synchronize()
         chk[f"{args.libs[i]}:{name}:bitwise"] = all(torch.equal(a, b) for a, b in zip(ts, ref))
+        if name.endswith("wgrad"):  # summed slabs (the gradient) relative to the first library's
+            g0, g1 = ref[0].double().sum(0), ts[0].double().sum(0)
+            chk[f"{args.libs[i]}:{name}:rel"] = float((g1 - g0).abs().max() / g0.abs().max().clamp_min(1e-30))
 out = {"check_vs_lib0": chk}
 for i, path in enumerate(args.libs):
     d = {}
