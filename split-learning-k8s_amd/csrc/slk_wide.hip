@@ -984,6 +984,13 @@ extern "C" int slk_wide_conv2_dgrad(const uint16_t* dp2, const uint8_t* code2, c
 // sparse instructions instead of 2 x 4 x 9 dense ones on the same B fragments: the same products, summed in
 // another order (slabs within ~1e-8 of the dense form's).
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+// the K5 weight gradients on the 2:4-sparse bf16 MFMA (wide_wgrad_kernel<C, true>; 0: the dense form)
+#ifndef SLK_WIDE_WG_SPARSE
+#define SLK_WIDE_WG_SPARSE 1
+#endif
+#ifndef SLK_WIDE_WG_SPLIT
+#define SLK_WIDE_WG_SPLIT 1
+#endif
 
 template <int CI_, int CO_, int HW_, int TR_, int EXP_ = 0>
 struct WgCfg {
@@ -1029,7 +1036,13 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     static_assert(!SP || C::EXP, "the sparse form stages dC from the pooled gradient");
     constexpr int BUF = SP ? C::SBUF : C::BUF;           // one of the two tile buffers
     constexpr int DCB = SP ? C::SDC : C::DC_BYTES;       // offset of the input tile in a buffer
-    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + C::RAW];
+    // SPLIT: the raw pooled dC double-buffered (DMA two tiles ahead), so half the waves (4-7) can stage the next
+    // tile's records before their MFMAs and the other half after (the SIMD pair (w, w + 4) overlaps one's staging
+    // with the other's MFMAs); otherwise every wave stages after its MFMAs
+    // (conv2's kernel only: conv3's spilled 13 VGPRs with it, 0.369 -> 0.490 ms; conv2 0.373 -> 0.365,
+    // profiles/r06_ab_wide_wgrad_split.txt)
+    constexpr bool SPLIT = SP && SLK_WIDE_WG_SPLIT && C::HW == 32;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + (SPLIT ? 2 : 1) * C::RAW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = wave >> 1;
@@ -1076,8 +1089,8 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     };
     // EXP: pooled dC chunk tid = (plane c, pooled row pr, pooled col px) of tile t, staged by this
     // thread's own wave (LDS-DMA into `raw`), so its expansion needs only that wave's vmcnt wait
-    char* raw = smem + 2 * BUF;
-    auto exp_issue_dc = [&](int t) {
+    char* const raw = smem + 2 * BUF;  // SPLIT: raw buffer k & 1 holds the pooled dC of this workgroup's tile k
+    auto exp_issue_dc = [&](int t, char* raw) {
         int n, rb;
         tile_of(t, n, rb);
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
@@ -1156,7 +1169,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     // bit 3 = the half (P & 1): a 16-lane ds_write_b64 group covers 16 distinct 8-B slots of 128 B.
     const int sco = lane & 7, sP0 = (lane >> 3) & 1, srest = lane >> 4;
     const int spr = C::HW == 32 ? (srest & 1) : srest, sP = C::HW == 32 ? sP0 + 2 * (srest >> 1) : sP0;
-    auto sp_expand = [&](char* buf) {
+    auto sp_expand = [&](char* buf, const char* raw) {
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -1194,12 +1207,14 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     if (valid(t)) {
         issue_tile(t, smem);
         if constexpr (C::EXP) {
-            exp_issue_dc(t);
+            exp_issue_dc(t, raw);
             wait_vmcnt<0>();
-            if constexpr (SP) sp_expand(smem);
+            if constexpr (SP) sp_expand(smem, raw);
             else exp_expand_dc(smem);
+            if (SPLIT && valid(t + C::KSPLIT)) exp_issue_dc(t + C::KSPLIT, raw + C::RAW);
         }
     }
+    const bool sfirst = wave >= 4;
 #pragma unroll 1
     for (; valid(t); t += C::KSPLIT) {
         wait_vmcnt<0>();
@@ -1209,8 +1224,15 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         const bool more = valid(t + C::KSPLIT);
         if (more) {
             issue_tile(t + C::KSPLIT, smem + (b ^ 1) * BUF);
-            if constexpr (C::EXP) exp_issue_dc(t + C::KSPLIT);
+            if constexpr (SPLIT) {
+                // tile k + 2's pooled dC into raw buffer k & 1 (tile k's, staged during tile k - 1)
+                if (valid(t + 2 * C::KSPLIT)) exp_issue_dc(t + 2 * C::KSPLIT, raw + b * C::RAW);
+            } else if constexpr (C::EXP) {
+                exp_issue_dc(t + C::KSPLIT, raw);
+            }
         }
+        // SPLIT: tile k + 1's raw dC landed by the wait above (its DMA was issued a tile ago)
+        if (SPLIT && more && sfirst) sp_expand(smem + (b ^ 1) * BUF, raw + (b ^ 1) * C::RAW);
         const char* buf = smem + b * BUF;
         if constexpr (SP) {
             typedef __attribute__((address_space(3))) bf16x4* lp4;
@@ -1281,10 +1303,12 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         }
         // EXP: the next tile's dC, routed into the other buffer (free since this tile's barrier) once
         // this wave's staging DMA has landed
-        if constexpr (C::EXP) {
+        if constexpr (SPLIT) {
+            if (more && !sfirst) sp_expand(smem + (b ^ 1) * BUF, raw + (b ^ 1) * C::RAW);
+        } else if constexpr (C::EXP) {
             if (more) {
                 wait_vmcnt<0>();
-                if constexpr (SP) sp_expand(smem + (b ^ 1) * BUF);
+                if constexpr (SP) sp_expand(smem + (b ^ 1) * BUF, raw);
                 else exp_expand_dc(smem + (b ^ 1) * BUF);
             }
         }
@@ -1312,10 +1336,6 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     }
 }
 
-// the K5 weight gradients on the 2:4-sparse bf16 MFMA (wide_wgrad_kernel<C, true>; 0: the dense form)
-#ifndef SLK_WIDE_WG_SPARSE
-#define SLK_WIDE_WG_SPARSE 1
-#endif
 using CfgWg2 = WgCfg<64, 128, 32, 4, 1>;   // dC = routed dp2 (EXP)
 using CfgWg3 = WgCfg<128, 256, 16, 8, 1>;   // dC = routed dcut (EXP)
 
