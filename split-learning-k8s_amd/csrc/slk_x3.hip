@@ -660,7 +660,8 @@ static_assert(2 * X3D_IMG <= 163840, "LDS");
 #ifndef SLK_X3D_EPI16
 #define SLK_X3D_EPI16 0
 #endif
-// profiling only (wrong results): bit 1 no dY staging, bit 2 no client epilogue, bit 4 its f32 MFMAs as one fma
+// profiling only (wrong results): bit 1 no dY staging, bit 2 no client epilogue, bit 4 its f32 MFMAs as one fma,
+// bit 8 no dY global loads (the staging stores kept)
 #ifndef SLK_X3D_ABL
 #define SLK_X3D_ABL 0
 #endif
@@ -810,8 +811,13 @@ __global__ __launch_bounds__(X3D_THREADS, 1) void conv2_dgrad_x3_kernel(
                 // compiler wait for the loads on the spot (a full memory latency per unit)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+#if SLK_X3D_ABL & 8
+                    dv[r][j] = (float)((o + j) & 255) * 1e-3f;  // no global loads
+                    dcb[r][j] = (uint32_t)(o + j) & 3u;
+#else
                     dv[r][j] = dpooled[o + j * P_WIN];
                     dcb[r][j] = code[o + j * P_WIN];
+#endif
                 }
             }
         }
