@@ -2544,15 +2544,26 @@ extern "C" int slk_conv2_dgrad_x3_c1w(const float* dpooled, const float* dp_amax
     return slk_launch_status();
 }
 
-// round 5: the slab count of both x3 wgrad entries is the images kernel's (conv2_wgrad_x3q_kernel: 6 units a
-// sample, up to X3Q_NKS shares); the f32-act kernel runs nslab / 2 K shares x 2 co halves into the same slabs
+// round 5: the slab count of both x3 wgrad entries is the images kernel's (conv2_wgrad_x3q/x3p: 6 units a
+// sample, up to X3Q_NKS shares). The f32-act kernel (3 units a sample) keeps its own share count min(3B,
+// X3W_NKS) x 2 co halves (round 6, ADVICE r5: with the images kernel's count over half its shares were empty
+// below B = 86 and it launched 512 one-per-CU workgroups); the slabs past its shares are zeroed.
 extern "C" int slk_conv2_wgrad_x3_nslab(int B) { return B <= 0 ? 0 : (6 * B < X3Q_NKS ? 6 * B : X3Q_NKS); }
 
 extern "C" int slk_conv2_wgrad_x3(const float* act, const float* act_amax, const float* dpooled, const float* dp_amax,
                                   const uint8_t* code, float* slabs, int B, void* stream) {
     SLK_CHECK_ARG(B >= 0 && act && act_amax && dpooled && dp_amax && code && slabs);
     if (B == 0) return 0;
-    const int nks = slk_conv2_wgrad_x3_nslab(B);  // one slab per K share (both co-half workgroups write it)
+    const int nslab = slk_conv2_wgrad_x3_nslab(B);
+#ifndef SLK_X3W_F32NKS
+#define SLK_X3W_F32NKS 1  // 0: the round-5 launch (nslab shares), kept for the A/B
+#endif
+    const int nks = SLK_X3W_F32NKS ? (3 * B < X3W_NKS ? 3 * B : X3W_NKS) : nslab;  // one slab per K share
+    if (nks < nslab) {
+        const hipError_t e = hipMemsetAsync(slabs + (size_t)nks * (W2_N + C2), 0,
+                                            sizeof(float) * (size_t)(nslab - nks) * (W2_N + C2), slk_stream(stream));
+        if (e != hipSuccess) return (int)e;
+    }
     hipLaunchKernelGGL(conv2_wgrad_x3_kernel<false>, dim3(2 * nks), dim3(X3W_THREADS), 0, slk_stream(stream), act,
                        act_amax, dpooled, dp_amax, code, slabs, B, nullptr);
     return slk_launch_status();

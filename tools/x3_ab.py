@@ -180,7 +180,12 @@ def main():
             slw = torch.empty(L.slk_fc_wgrad_nslab(B), 92170, device=dev)
             cases[f"fcw {tag}"] = (lambda L=L, dlw=dlw, slw=slw: L.slk_fc_wgrad(p(dlw), p(pooled), p(slw), B, st))
             outs[f"fcw {tag}"] = slw
-        if "wgrad" in args.ops:
+        if "wgradf" in args.ops.split(","):  # the f32-act entry (forward images not shared)
+            slf = torch.zeros(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
+            L.slk_conv2_wgrad_x3.argtypes = [P] * 6 + [ctypes.c_int, P]
+            cases[f"wgradf {tag}"] = (lambda L=L, sl=slf: L.slk_conv2_wgrad_x3(p(act), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
+            outs[f"wgradf {tag}"] = slf
+        if "wgrad" in args.ops.split(","):
             sl = torch.empty(L.slk_conv2_wgrad_x3_nslab(B), ops.CONV2_SLAB, device=dev)
             L.slk_conv2_wgrad_x3s.argtypes = [P] * 6 + [ctypes.c_int, P]
             cases[f"wgrad {tag}"] = (lambda L=L, sl=sl, a16=a16: L.slk_conv2_wgrad_x3s(p(a16), p(amax), p(dp), p(dpa), p(code), p(sl), B, st))
@@ -213,7 +218,7 @@ def main():
             first[op] = t
             continue
         r = first[op]
-        red = (lambda z: z.sum(0)) if op in ("dgc1", "fcw", "wgrad") else (lambda z: z)
+        red = (lambda z: z.sum(0)) if op in ("dgc1", "fcw", "wgrad", "wgradf") else (lambda z: z)
         a, b_ = red(t.double()), red(r.double())
         print(f"check {k:18s} max|diff|/max|ref| {((a - b_).abs().max() / b_.abs().max()).item():.3e}", flush=True)
 
