@@ -991,6 +991,9 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #ifndef SLK_WIDE_WG_SPLIT
 #define SLK_WIDE_WG_SPLIT 1
 #endif
+#ifndef SLK_WIDE_WG_ABL
+#define SLK_WIDE_WG_ABL 0  // profiling only (wrong results): 1 no dC staging (sparse records), 2 no MFMA steps
+#endif
 
 template <int CI_, int CO_, int HW_, int TR_, int EXP_ = 0>
 struct WgCfg {
@@ -1170,6 +1173,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
     const int sco = lane & 7, sP0 = (lane >> 3) & 1, srest = lane >> 4;
     const int spr = C::HW == 32 ? (srest & 1) : srest, sP = C::HW == 32 ? sP0 + 2 * (srest >> 1) : sP0;
     auto sp_expand = [&](char* buf, const char* raw) {
+        if (SLK_WIDE_WG_ABL & 1) return;  // profiling only
         constexpr int PH = C::HW / 2, PR = C::TR / 2;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -1234,7 +1238,7 @@ __global__ __launch_bounds__(512, 1) void wide_wgrad_kernel(const uint16_t* __re
         // SPLIT: tile k + 1's raw dC landed by the wait above (its DMA was issued a tile ago)
         if (SPLIT && more && sfirst) sp_expand(smem + (b ^ 1) * BUF, raw + (b ^ 1) * C::RAW);
         const char* buf = smem + b * BUF;
-        if constexpr (SP) {
+        if constexpr (SP && !(SLK_WIDE_WG_ABL & 2)) {
             typedef __attribute__((address_space(3))) bf16x4* lp4;
             typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
             const bf16x16 ones16 = __builtin_shufflevector(ones, ones, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
