@@ -17,13 +17,21 @@ grep '^{' gpurun_out/bench.log | cut -c1-300
 timeout -k 10 300 python -u bench.py --config k5 --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/bench_k5.log 2>&1
 rc=$?; echo "bench k5 rc=$rc"; stop_if_fatal $rc bench_k5
 for cfg in k2 k5; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 20 --warmup 5 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-dropin > gpurun_out/prof_$cfg.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 50 --warmup 5 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-dropin > gpurun_out/prof_$cfg.log 2>&1
   rc=$?; echo "rocprof $cfg rc=$rc"; stop_if_fatal $rc rocprof
   python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_$cfg.build_id
   grep '^{' gpurun_out/prof_$cfg.log | tail -1 > gpurun_out/prof_$cfg.bench.json || true
   OUT=gpurun_out/pmc_$cfg KARGS="--config $cfg --steps 3" bash tools/pmc.sh || exit $?
   python tools/pmc_summary.py --dir gpurun_out/pmc_$cfg --out gpurun_out/pmc_${cfg}_summary.json > /dev/null
 done
+elif [ "${PART}" = "3" ]; then
+# the K2 rocprofv3 kernel-stats pass alone (same command as in part 1)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_k2 -o run --output-format csv -- python bench.py --config k2 --no-k5 --steps 50 --warmup 5 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-dropin > gpurun_out/prof_k2.log 2>&1
+rc=$?; echo "rocprof k2 rc=$rc"; stop_if_fatal $rc rocprof
+python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_k2.build_id
+grep '^{' gpurun_out/prof_k2.log | tail -1 > gpurun_out/prof_k2.bench.json || true
+timeout -k 10 400 python -u bench.py --no-k5 --no-cpu-baseline --no-dropin --no-hub-loopback > gpurun_out/bench_after_prof.log 2>&1
+echo "bench rc=$?"
 else
 for N in 2 4; do
   SLK_BENCH_BACKEND=gloo SLK_BENCH_ONE_GPU=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port 2961$N bench.py --gpus $N --steps 5 --warmup 2 --batch 512 --k5-batch 512 > gpurun_out/reh$N.log 2>&1
