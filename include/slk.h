@@ -228,10 +228,11 @@ int slk_conv2_dgrad_x3_c1w_nslab(int B);
 
 /* out[i] = (accumulate ? out[i] : 0) + sum_{s=0}^{nslab-1} slabs[s*n + i]  (fixed slab order).
  * accumulate = 1 sums micro-batches into one gradient (pipeline topologies).
- * Summation order (all slab reductions, incl. SGD / Adam from slabs): nslab <= 64 -> slabs in
- * ascending order per column; nslab > 64 -> 16 partial sums over slabs w, w+16, w+32, ... (w = 0..15)
- * added in w order. Either is a fixed function of (slabs, nslab): bit-stable run to run, but a result
- * at nslab <= 64 is not bitwise comparable with one at nslab > 64. */
+ * Summation order (this and SGD from slabs): nslab <= 16 -> slabs in ascending order per column;
+ * 16 < nslab <= 64 -> 4 partial sums over slabs w, w+4, w+8, ... (w = 0..3) added in w order; nslab > 64 ->
+ * 16 partial sums over slabs w, w+16, ... added in w order (Adam from slabs: ascending up to 64 slabs, the
+ * 16-partial form above). Each is a fixed function of (slabs, nslab): bit-stable run to run, but results
+ * from different forms are not bitwise comparable. */
 int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, int accumulate, void* stream);
 
 /* Fused deterministic slab reduction + SGD (lr, no momentum, no weight decay):

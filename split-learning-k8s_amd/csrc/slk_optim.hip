@@ -10,11 +10,18 @@
 // slabs w, w+16, w+32, ... of those columns in order (8 loads in flight), then wave 0 adds the 16
 // partials in wave order. The result is a fixed function of the inputs (no atomics).
 constexpr int RS_WAVES = 16;
-// Few slabs (<= RS_COLS_MAX: the fc wgrad set) -> thread = column, slabs summed in ascending order
-// with 8 loads in flight, 1024 columns per block (64-column blocks over 92,170 columns were ~1,400
-// dispatch-bound blocks); many slabs -> 64 columns per block, 16 waves over the slab range.
-constexpr int RS_COLS_MAX = 64;
-__host__ __device__ constexpr int rs_cols_per_block(int nslab) { return nslab <= RS_COLS_MAX ? 1024 : 64; }
+// Few slabs (<= RS_COLS_MAX) -> thread = column, slabs summed in ascending order with 8 loads in flight,
+// 1024 columns per block; up to RS_MID_MAX (the fc wgrad set, 64 at B = 4096) -> 256 columns per block,
+// 4 waves per 64 columns each summing every 4th slab, the 4 partials added in order (round 6: one thread
+// per column walked 64 slabs in 8 dependent rounds on 91 blocks; 64-column blocks over 92,170 columns
+// were ~1,400 dispatch-bound blocks); many slabs -> 64 columns per block, 16 waves over the slab range.
+#ifndef SLK_RS_MID
+#define SLK_RS_MID 1  // 0: the round-5 forms (<= 64 slabs thread per column), kept for the A/B
+#endif
+constexpr int RS_COLS_MAX = SLK_RS_MID ? 16 : 64, RS_MID_MAX = 64;
+__host__ __device__ constexpr int rs_cols_per_block(int nslab) {
+    return nslab <= RS_COLS_MAX ? 1024 : (nslab <= RS_MID_MAX ? 256 : 64);
+}
 static inline int rs_blocks(int n, int nslab) { return (n + rs_cols_per_block(nslab) - 1) / rs_cols_per_block(nslab); }
 
 __device__ __forceinline__ void slab_reduce_sgd_cols(float* __restrict__ param, float* __restrict__ grad,
@@ -68,11 +75,44 @@ __device__ __forceinline__ void slab_reduce_sgd_rows(float* __restrict__ param, 
     }
 }
 
+__device__ __forceinline__ void slab_reduce_sgd_mid(float* __restrict__ param, float* __restrict__ grad,
+                                                    const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                    int acc, int blk) {
+    __shared__ float part[4][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = (wave & 3) * 64 + lane, sg = wave >> 2;  // column within the block, slab group
+    const int i = blk * 256 + c;
+    float g = 0.f;
+    if (i < n) {
+        const float* s = slabs + i;
+        int k = sg;
+        for (; k + 7 * 4 < nslab; k += 8 * 4) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(k + 4 * u) * n];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g += v[u];
+        }
+        for (; k < nslab; k += 4) g += s[(size_t)k * n];
+    }
+    part[sg][c] = g;
+    __syncthreads();
+    if (sg == 0 && i < n) {
+        float t = acc ? grad[i] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += part[q][c];
+        if (grad) grad[i] = t;
+        if (param) param[i] = param[i] - lr * t;
+    }
+}
+
 __device__ __forceinline__ void slab_reduce_sgd(float* __restrict__ param, float* __restrict__ grad,
                                                 const float* __restrict__ slabs, int nslab, int n, float lr,
                                                 int acc, int blk) {
     if (rs_cols_per_block(nslab) == 1024)
         slab_reduce_sgd_cols(param, grad, slabs, nslab, n, lr, acc, blk);
+    else if (rs_cols_per_block(nslab) == 256)
+        slab_reduce_sgd_mid(param, grad, slabs, nslab, n, lr, acc, blk);
     else
         slab_reduce_sgd_rows(param, grad, slabs, nslab, n, lr, acc, blk);
 }

@@ -377,11 +377,12 @@ def test_graph_alternating_batch_sizes_equal_eager(gpu):
     assert results[0][2] == results[1][2]
 
 
-@pytest.mark.parametrize("nslab", [16, 17, 64, 65, 256])
+@pytest.mark.parametrize("nslab", [16, 17, 33, 64, 65, 256])
 def test_slab_reduction_both_orders_vs_float64(gpu, nslab):
-    """slk_reduce_slabs / slk_sgd_from_slabs pick their summation order by slab count (<= 64:
-    thread per column, ascending; > 64: 16 waves over slabs w, w+16, ..., combined in wave order —
-    include/slk.h). Both are fixed orders (run-to-run identical) and both match a float64 sum."""
+    """slk_reduce_slabs / slk_sgd_from_slabs pick their summation order by slab count (<= 16: thread per
+    column, ascending; 17-64: 4 waves per 64 columns over slabs w, w+4, ...; > 64: 16 waves over slabs w,
+    w+16, ..., partials combined in wave order — include/slk.h). All are fixed orders (run-to-run
+    identical) and all match a float64 sum (n = 5000: partial column blocks at every form)."""
     from splitcnn import ops
     g = torch.Generator(device=gpu).manual_seed(nslab)
     n = 5000

@@ -24,6 +24,7 @@ for path in args.libs:
     for n in ("slk_conv2_fwd_pool", "slk_conv2_dgrad", "slk_conv2_wgrad", "slk_conv1_fwd", "slk_conv1_wgrad",
               "slk_fc_xent", "slk_fc_wgrad", "slk_conv1_wgrad_remask"):
         getattr(L, n).restype = ctypes.c_int
+    L.slk_sgd_from_slabs.restype = ctypes.c_int
     L.slk_conv2_wgrad_nslab.restype = ctypes.c_int
     L.slk_conv1_wgrad_nslab.restype = ctypes.c_int
     L.slk_fc_wgrad_nslab.restype = ctypes.c_int
@@ -81,9 +82,14 @@ def calls(L):
         "conv1_wgrad_remask": lambda: L.slk_conv1_wgrad_remask(p(x), p(W1), p(b1), p(gcut), p(slabs), B, P(s)),
         "fc_wgrad": lambda: L.slk_fc_wgrad(p(dl), p(pooled), p(slabs), B, P(s)),
         "row_amax": lambda: L.slk_row_amax(p(act), B, 32 * 26 * 26, p(amx), P(s)),
+        # the step's two server slab sets through the fused reduce + SGD (64 fc slabs, 256 conv2 slabs)
+        "sgd_fc": lambda: L.slk_sgd_from_slabs(p(prm), p(grd), p(slabs), 64, 92170, ctypes.c_float(0.01), P(s)),
+        "sgd_conv2": lambda: L.slk_sgd_from_slabs(p(prm), p(grd), p(slabs), 256, 18496, ctypes.c_float(0.01), P(s)),
     }
 
 amx = torch.empty(B, device=dev)
+prm = torch.zeros(92170, device=dev)
+grd = torch.empty(92170, device=dev)
 _all_calls = calls
 if args.cases:
     calls = lambda L: {k: v for k, v in _all_calls(L).items() if k in args.cases.split(",")}  # noqa: E731
