@@ -107,6 +107,12 @@ int slk_fc_fwd(const float* pooled, const float* W3, const float* b3, float* log
 int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, float* loss_i, float* dlogits,
                      float grad_scale, int* err_flag, int B, void* stream);
 
+/* slk_fc_fwd + slk_xent_fwd_bwd in one launch (the cross-entropy of a workgroup's 16 samples from the logits it
+ * just reduced, in LDS): the same logits, loss_i and dlogits bit for bit. src/server_part.py:48-49 + the CE part
+ * of :51. */
+int slk_fc_logits_xent(const float* pooled, const float* W3, const float* b3, const int64_t* labels, float* logits,
+                       float* loss_i, float* dlogits, float grad_scale, int* err_flag, int B, void* stream);
+
 /* dpooled = dlogits @ W3 (fc1 input gradient). Replaces the fc1 part of loss.backward()
  * (src/server_part.py:51). */
 int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpooled, int B, void* stream);

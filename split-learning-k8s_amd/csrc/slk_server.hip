@@ -846,6 +846,17 @@ extern "C" int slk_xent_fwd_bwd(const float* logits, const int64_t* labels, floa
     return slk_launch_status();
 }
 
+extern "C" int slk_fc_logits_xent(const float* pooled, const float* W3, const float* b3, const int64_t* labels,
+                                  float* logits, float* loss_i, float* dlogits, float grad_scale, int* err_flag, int B,
+                                  void* stream) {
+    SLK_CHECK_ARG(B >= 0);
+    if (B == 0) return 0;
+    SLK_CHECK_ARG(pooled && W3 && b3 && labels && logits && loss_i && dlogits);
+    fc_head16_kernel<3><<<(B + FCH_S - 1) / FCH_S, FCH_T, 0, slk_stream(stream)>>>(
+        pooled, W3, b3, labels, logits, loss_i, dlogits, nullptr, grad_scale, err_flag, B, nullptr);
+    return slk_launch_status();
+}
+
 extern "C" int slk_fc_dgrad(const float* dlogits, const float* W3, float* dpooled, int B,
                             void* stream) {
     SLK_CHECK_ARG(B >= 0);

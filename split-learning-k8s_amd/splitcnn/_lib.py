@@ -46,6 +46,7 @@ _SIGS = {
     "slk_conv2_fwd_pool_direct": [_P, _P, _P, _P, _P, _I, _P],
     "slk_fc_fwd": [_P, _P, _P, _P, _I, _P],
     "slk_xent_fwd_bwd": [_P, _P, _P, _P, _F, _P, _I, _P],
+    "slk_fc_logits_xent": [_P, _P, _P, _P, _P, _P, _P, _F, _P, _I, _P],
     "slk_fc_dgrad": [_P, _P, _P, _I, _P],
     "slk_fc_dgrad_amax": [_P, _P, _P, _P, _I, _P],
     "slk_fc_xent": [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _I, _P],

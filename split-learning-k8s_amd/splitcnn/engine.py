@@ -279,6 +279,8 @@ class ServerStage:
         # evicts it); same kernels, bit-identical results (tools/x3_ab.py --ops fcord --flush: 0.1010 ->
         # 0.0970 ms for head + fc1 wgrad from cold caches)
         self.fc_split = True
+        # ... with its logits and cross-entropy in one launch (slk_fc_logits_xent, round 6; bitwise the two)
+        self.fc_one_launch = True
         self._buf = _Buffers()
 
     def bind_grads(self, view: torch.Tensor):
@@ -333,9 +335,14 @@ class ServerStage:
         split = self.fc_split and dp_amax is not None
         if split:
             with TIMER("fc_xent"):
-                logits = ops.fc_fwd(pooled, W3, b3, out=self._b("logits", (B, 10)))
-                loss_i, dlogits = ops.xent_fwd_bwd(logits, labels, grad_scale, loss_i=self._b("loss_i", (B,)),
-                                                   dlogits=self._b("dlogits", (B, 10)), err_flag=self.err_flag)
+                if self.fc_one_launch:
+                    _, loss_i, dlogits = ops.fc_logits_xent(
+                        pooled, W3, b3, labels, grad_scale, logits=self._b("logits", (B, 10)),
+                        loss_i=self._b("loss_i", (B,)), dlogits=self._b("dlogits", (B, 10)), err_flag=self.err_flag)
+                else:
+                    logits = ops.fc_fwd(pooled, W3, b3, out=self._b("logits", (B, 10)))
+                    loss_i, dlogits = ops.xent_fwd_bwd(logits, labels, grad_scale, loss_i=self._b("loss_i", (B,)),
+                                                       dlogits=self._b("dlogits", (B, 10)), err_flag=self.err_flag)
             with TIMER("fc_wgrad"):
                 s3 = ops.fc_wgrad_slabs(dlogits, pooled, slabs=self._b("s3", (ops.fc_wgrad_nslab(B), ops.FC_SLAB)))
             dpooled = self._b("dpooled", (B, 64, 12, 12))

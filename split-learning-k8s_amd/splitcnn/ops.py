@@ -232,6 +232,19 @@ def fc_fwd(pooled, W3, b3, out=None):
     return logits
 
 
+def fc_logits_xent(pooled, W3, b3, labels, grad_scale, logits=None, loss_i=None, dlogits=None, err_flag=None):
+    """fc_fwd + xent_fwd_bwd in one launch (slk_fc_logits_xent), bitwise their outputs."""
+    B = _pooled_batch(pooled)
+    logits = _out(logits, (B, 10), pooled, name="logits")
+    loss_i = _out(loss_i, (B,), pooled, name="loss_i")
+    dlogits = _out(dlogits, (B, 10), pooled, name="dlogits")
+    eptr = _dev(err_flag, "err_flag", (1,), torch.int32) if err_flag is not None else None
+    _lib.call("slk_fc_logits_xent", _dev(pooled, "pooled"), _dev(W3, "fc1.weight", (10, 9216)),
+              _dev(b3, "fc1.bias", (10,)), _labels(labels, B), _dev(logits, "logits"), _dev(loss_i, "loss_i"),
+              _dev(dlogits, "dlogits"), float(grad_scale), eptr, B, _stream(pooled))
+    return logits, loss_i, dlogits
+
+
 def _labels(labels, B):
     _dev(labels, "labels", (B,), torch.int64)
     return labels.data_ptr()

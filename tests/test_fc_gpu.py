@@ -85,6 +85,24 @@ def test_split_head_bitwise_vs_fused_head_with_amax(gpu, B):
     assert torch.equal(dl2, dlogits)
     assert torch.equal(dp2.reshape(dp.shape), dp)
     assert torch.equal(dpa2, dpa)
+    # the step's launch (round 6): logits + cross-entropy in one kernel, bitwise the two launches
+    lg3, l3, dl3 = ops.fc_logits_xent(pooled, W3, b3, y, 1.0 / B)
+    assert torch.equal(lg3, logits) and torch.equal(l3, loss_i) and torch.equal(dl3, dlogits)
+
+
+def test_fc_logits_xent_bad_label_sets_flag(gpu):
+    from splitcnn import ops
+    B = 20
+    pooled = torch.rand(B, 64, 12, 12, device=gpu)
+    W3 = torch.randn(10, 9216, device=gpu) * 0.01
+    b3 = torch.zeros(10, device=gpu)
+    y = torch.randint(0, 10, (B,), device=gpu)
+    y[7] = 10
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _, loss_i, dlogits = ops.fc_logits_xent(pooled, W3, b3, y, 1.0 / B, err_flag=flag)
+    assert int(flag.item()) == 1
+    assert torch.isnan(loss_i[7]) and torch.isnan(dlogits[7]).all()
+    assert torch.isfinite(loss_i[:7]).all() and torch.isfinite(dlogits[8:]).all()
 
 
 @pytest.mark.parametrize("B", [17, 4096])

@@ -29,11 +29,14 @@ def main():
     variants = {}
     configs = {"x3": {}, "x3_unfused": {"fuse_client_backward": False}, "x3w": {"conv": "x3w"}, "f32": {"conv": "f32"}}
     # the default splits the head (fc_split); the fused-head orders set it off
-    server_attrs = {"x3_fused_head": {"fc_split": False},
+    server_attrs = {"x3_fused_head": {"fc_split": False}, "x3_two_launch_head": {"fc_one_launch": False},
                     "x3_fcw_early": {"fc_split": False, "fc_wgrad_early": True},
                     "x3_wgrad_first": {"wgrad_first": True}}
+    ap_head = os.environ.get("AB_HEAD") == "1"  # the round-6 one-launch head vs the two launches only
     if args.order:
         configs = {"x3": {}, **{k: {} for k in server_attrs}}
+    if ap_head:
+        configs = {"x3": {}, "x3_two_launch_head": {}}
     for name, kw in configs.items():
         tr = SplitTrainer(*init_models(seed=0), device=dev, graph=True, **kw)
         for a, v in server_attrs.get(name, {}).items():
