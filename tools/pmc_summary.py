@@ -61,7 +61,8 @@ if args.traffic_out:
                   # round 5-6: the images wgrad (dense x3q, then the 2:4-sparse x3p) and the split fc head
                   "conv2_wgrad_x3q_kernel": "conv2_wgrad_x3", "conv2_wgrad_x3p_kernel": "conv2_wgrad_x3",
                   "conv1_fwd_x3_kernel<true, false>": "conv1_fwd", "conv2_fwd_pool_x3_kernel<true, false>": "conv2_fwd_pool_x3",
-                  "fc_head16_kernel<1>": "fc_logits", "fc_head16_kernel<4>": "fc_dgrad"})
+                  "fc_head16_kernel<1>": "fc_logits", "fc_head16_kernel<4>": "fc_dgrad",
+                  "fc_head16_kernel<3>": "fc_logits"})  # round 6: logits + CE in one launch
     # widened (K5) template instantiations -> bench.py's kernel names (csrc/slk_wide.hip:824-836, 1055)
     wide = [("wide_conv32_kernel<Conv32Cfg<64, 128, 32", "wide_conv2_fwd"),
             ("wide_conv_kernel<ConvCfg<64, 128, 32", "wide_conv2_fwd"),
