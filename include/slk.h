@@ -236,9 +236,9 @@ int slk_conv2_dgrad_x3_c1w_nslab(int B);
  * accumulate = 1 sums micro-batches into one gradient (pipeline topologies).
  * Summation order (this and SGD from slabs): nslab <= 16 -> slabs in ascending order per column;
  * 16 < nslab <= 64 -> 4 partial sums over slabs w, w+4, w+8, ... (w = 0..3) added in w order; nslab > 64 ->
- * 16 partial sums over slabs w, w+16, ... added in w order (Adam from slabs: ascending up to 64 slabs, the
- * 16-partial form above). Each is a fixed function of (slabs, nslab): bit-stable run to run, but results
- * from different forms are not bitwise comparable. */
+ * 16 partial sums over slabs w, w+16, ... added in w order (Adam from slabs: the same three forms). Each is
+ * a fixed function of (slabs, nslab): bit-stable run to run, but results from different forms are not
+ * bitwise comparable. */
 int slk_reduce_slabs(const float* slabs, int nslab, int n, float* out, int accumulate, void* stream);
 
 /* Fused deterministic slab reduction + SGD (lr, no momentum, no weight decay):

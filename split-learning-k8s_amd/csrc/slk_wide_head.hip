@@ -311,11 +311,68 @@ __global__ __launch_bounds__(256) void wide_head_back_kernel(const uint16_t* __r
 //   m = m + (1-b1)(g - m)  [lerp]; v = v*b2 + (1-b2) g*g  [mul_ + addcmul_];
 //   p = p - (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)  [addcdiv_].
 constexpr int AD_WAVES = 16;
-// Few slabs (<= AD_COLS_MAX, the conv2/conv3/fc wgrad slab sets): thread = column, the slabs summed
-// in ascending order with 8 loads in flight, 1024 columns per block (coalesced rows); many slabs
-// (the conv1 set): 64 columns per block, 16 waves over the slab range, partials added in wave order.
-constexpr int AD_COLS_MAX = 64;
-__host__ __device__ constexpr int adam_cols_per_block(int nslab) { return nslab <= AD_COLS_MAX ? 1024 : 64; }
+// Few slabs (<= AD_COLS_MAX): thread = column, the slabs summed in ascending order with 8 loads in flight,
+// 1024 columns per block (coalesced rows); many slabs (the conv1 and conv2 sets): 64 columns per block, 16
+// waves over the slab range, partials added in wave order.
+// Round 6: 17-64 slabs (the conv3 and fc sets at B = 4096) as 4 waves per 64 columns, each summing every 4th
+// slab, partials added in order, 256 columns per block (a thread per column walked 64 slabs in 8 dependent rounds).
+#ifndef SLK_AD_MID
+#define SLK_AD_MID 1
+#endif
+constexpr int AD_COLS_MAX = SLK_AD_MID ? 16 : 64, AD_MID_MAX = 64;
+__host__ __device__ constexpr int adam_cols_per_block(int nslab) {
+    return nslab <= AD_COLS_MAX ? 1024 : (nslab <= AD_MID_MAX ? 256 : 64);
+}
+
+// the Adam update of element i from its summed gradient t (shared by the reduction forms below)
+__device__ __forceinline__ void adam_apply(int i, float t, float* __restrict__ param, float* __restrict__ grad,
+                                           float* __restrict__ m_, float* __restrict__ v_, float lr, float b1,
+                                           float b2, float eps, const int* __restrict__ step_ptr) {
+    if (grad) grad[i] = t;
+    const double tt = (double)(*step_ptr + 1);
+    const double bc1 = 1.0 - pow((double)b1, tt);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(1.0 - pow((double)b2, tt));
+    float m = m_[i], v = v_[i];
+    m = m + (1.f - b1) * (t - m);
+    v = v * b2 + t * t * (1.f - b2);
+    const float denom = sqrtf(v) / bc2s + eps;
+    param[i] = param[i] + (-step_size) * (m / denom);
+    m_[i] = m;
+    v_[i] = v;
+}
+
+__device__ __forceinline__ void adam_slab_block_mid(float* __restrict__ param, float* __restrict__ grad,
+                                                    float* __restrict__ m_, float* __restrict__ v_,
+                                                    const float* __restrict__ slabs, int nslab, int n, float lr,
+                                                    float b1, float b2, float eps, const int* __restrict__ step_ptr,
+                                                    int blk) {
+    __shared__ float part[4][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = (wave & 3) * 64 + lane, sg = wave >> 2;  // column within the block, slab group
+    const int i = blk * 256 + c;
+    float g = 0.f;
+    if (i < n) {
+        const float* s = slabs + i;
+        int k = sg;
+        for (; k + 7 * 4 < nslab; k += 8 * 4) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(k + 4 * u) * n];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g += v[u];
+        }
+        for (; k < nslab; k += 4) g += s[(size_t)k * n];
+    }
+    part[sg][c] = g;
+    __syncthreads();
+    if (sg == 0 && i < n) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += part[q][c];
+        adam_apply(i, t, param, grad, m_, v_, lr, b1, b2, eps, step_ptr);
+    }
+}
 
 __device__ __forceinline__ void adam_slab_block_rows(float* __restrict__ param, float* __restrict__ grad,
                                                 float* __restrict__ m_, float* __restrict__ v_,
@@ -398,6 +455,8 @@ __device__ __forceinline__ void adam_slab_block(float* __restrict__ param, float
                                                 int blk) {
     if (adam_cols_per_block(nslab) == 1024)
         adam_slab_block_cols(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blk);
+    else if (adam_cols_per_block(nslab) == 256)
+        adam_slab_block_mid(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blk);
     else
         adam_slab_block_rows(param, grad, m_, v_, slabs, nslab, n, lr, b1, b2, eps, step_ptr, blk);
 }

@@ -77,6 +77,7 @@ for path in args.libs:
                "slabs": torch.empty(L.slk_wide_head_nslab(B), 163850, device=dev)}
     libs.append(L)
 hlab = torch.randint(0, 10, (B,), device=dev, generator=g)
+ad_p, ad_m, ad_v = torch.zeros(295168, device=dev), torch.zeros(295168, device=dev), torch.zeros(295168, device=dev)
 herr = torch.zeros(1, dtype=torch.int32, device=dev)
 
 
@@ -94,6 +95,13 @@ def calls(L):
         "conv2_dgrad": lambda: L.slk_wide_conv2_dgrad(p(dp2), p(code2), p(w2d), p(a1bits if L._bits else a1),
                                                       p(out_da1m), B, P(s)),
         "conv1_wgrad": lambda: L.slk_wide_conv1_wgrad(p(x), p(da1m), p(slabs), B, P(s)),
+        # Adam from slabs at the step's two <= 64-slab sets: conv3's (64 x 295,168) and the head's (64 x 163,850)
+        "adam_conv3": lambda: L.slk_adam_from_slabs(p(ad_p), None, p(ad_m), p(ad_v), p(slabs), 64, 295168,
+                                                    ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999),
+                                                    ctypes.c_float(1e-8), p(stepc), P(s)),
+        "adam_fc": lambda: L.slk_adam_from_slabs(p(ad_p), None, p(ad_m), p(ad_v), p(slabs), 64, 163850,
+                                                 ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999),
+                                                 ctypes.c_float(1e-8), p(stepc), P(s)),
         "head_fwd": lambda: L.slk_wide_head_fwd(p(cut), p(wf8), p(bfc), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hlog),
                                                 0, B, P(s)),
         "head_bwd": lambda: L.slk_wide_head_bwd(p(cut), p(wf8), p(hdl), p(stepc), 7, 1 << 30, 4.0 / 3.0, p(hdcut),
