@@ -520,7 +520,10 @@ extern "C" int slk_conv2_wgrad_direct_nslab(int B) { return B > 0 ? (2 * B < C2W
 #ifndef SLK_FCH_NS
 #define SLK_FCH_NS 2
 #endif
-constexpr int FCH_S = 16, FCH_T = 512, FCH_W = FCH_T / 64;
+#ifndef SLK_FCH_S
+#define SLK_FCH_S 16  // samples per workgroup (8: 256-thread workgroups, two per CU at B = 4096)
+#endif
+constexpr int FCH_S = SLK_FCH_S, FCH_T = 32 * FCH_S, FCH_W = FCH_T / 64;
 constexpr int FCH_KW = P_SAMPLE / FCH_W;  // 1152 features per wave
 constexpr int FCH_CK = SLK_FCH_CK;        // features per chunk (64)
 constexpr int FCH_NS = SLK_FCH_NS;        // LDS slots per wave = chunks in flight + 1 (2)
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(FCH_T, 1) void fc_head16_kernel(
             float v = 0.f;
 #pragma unroll
             for (int w = 0; w < FCH_W; ++w) v += red[w * 64 + l][r];
-            if (n < NCLS) {
+            if (n < NCLS && s < FCH_S) {  // (FCH_S = 8: MFMA rows 8-15 read stand-in rows, never stored)
                 v += b3[n];
                 zl[s][n] = v;
                 if (s < ns) logits[(size_t)(s0 + s) * NCLS + n] = v;

@@ -172,6 +172,19 @@ def main():
                 | L.slk_xent_fwd_bwd(p(o[0]), p(yo), p(o[1]), p(o[2]), 1.0 / B, None, B, st)
                 | L.slk_fc_wgrad(p(o[2]), p(pooled), p(o[5]), B, st) | L.slk_fc_dgrad(p(o[2]), p(W3), p(o[3]), B, st))
             cases[f"fcwA {tag}"] = (lambda L=L, o=oA: L.slk_fc_wgrad(p(o[2]), p(pooled), p(o[5]), B, st))
+        if "fch" in args.ops.split(","):  # the step's head launches: logits + CE (one launch), dpooled (+ dp_amax)
+            L.slk_fc_logits_xent.restype = ctypes.c_int
+            L.slk_fc_logits_xent.argtypes = [P] * 7 + [ctypes.c_float, P, ctypes.c_int, P]
+            L.slk_fc_dgrad_amax.restype = ctypes.c_int
+            L.slk_fc_dgrad_amax.argtypes = [P] * 4 + [ctypes.c_int, P]
+            yo = y.to(dev)
+            oh = [torch.empty(B, 10, device=dev), torch.empty(B, device=dev), torch.empty(B, 10, device=dev),
+                  torch.empty_like(dp), torch.empty(B, device=dev)]
+            cases[f"fch3 {tag}"] = (lambda L=L, o=oh: L.slk_fc_logits_xent(p(pooled), p(W3), p(b3), p(yo), p(o[0]), p(o[1]),
+                                                                          p(o[2]), 1.0 / B, None, B, st))
+            cases[f"fch4 {tag}"] = (lambda L=L, o=oh: L.slk_fc_dgrad_amax(p(o[2]), p(W3), p(o[3]), p(o[4]), B, st))
+            outs[f"fch3 {tag}"] = oh[0]
+            outs[f"fch4 {tag}"] = oh[3]
         if "fcw" in args.ops.split(","):
             L.slk_fc_wgrad_nslab.restype = ctypes.c_int
             L.slk_fc_wgrad.restype = ctypes.c_int
