@@ -14,9 +14,10 @@ rc=$?; echo "bench rc=$rc"; stop_if_fatal $rc bench
 timeout -k 10 300 python -u bench.py --config k5 --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/bench_k5.log 2>&1
 rc=$?; echo "bench k5 rc=$rc"; stop_if_fatal $rc bench_k5
 for cfg in k2 k5; do
-  # eager steps (--no-graph): under --kernel-trace the graph-replayed step runs ~1/3 slower and its kernels
-  # 7-15 % slower, while eager launches time the same with and without the profiler (tools/x3_ab.py control)
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 10 --warmup 3 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-graph > gpurun_out/prof_$cfg.log 2>&1
+  # graph-replayed steps, as benched: round 6 measured the profiled process within 0.1-0.7 % of an unprofiled
+  # run on the same box (profiles/r06_final*_bench_unprofiled_same_box.txt); rounds 4-5 profiled eager steps
+  # because the graph step then ran ~1/3 slower under --kernel-trace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$cfg -o run --output-format csv -- python bench.py --config $cfg --no-k5 --steps 50 --warmup 5 --no-cpu-baseline --no-conv-compare --no-hub-loopback --no-dropin > gpurun_out/prof_$cfg.log 2>&1
   rc=$?; echo "rocprof $cfg rc=$rc"; stop_if_fatal $rc rocprof
   # the library build this profile belongs to (bench.py reports rocprof_avg_ms only for a matching build)
   python -c "import sys; sys.path.insert(0, 'split-learning-k8s_amd'); from splitcnn import _lib; print(_lib.build_id())" > gpurun_out/prof_$cfg.build_id
