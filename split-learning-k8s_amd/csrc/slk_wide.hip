@@ -918,8 +918,13 @@ using CfgConv3Fwd = ConvCfg<128, 256, 16, 128, wide::MODE_FWD_POOL, SLK_WIDE_FW,
 // Backward: no unpooled gradient is ever materialised. conv3's dgrad and wgrad read the pooled cut
 // gradient dcut + code3 and route it while staging (EXP); conv3's dgrad writes dp2 (the gradient of
 // p2, 16 x 16), which conv2's dgrad and wgrad route by code2 the same way.
-using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_NWV, 1>;
-using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4, 1>;
+// waves per workgroup of the two dgrads (round 6: conv3's at 8 waves, one workgroup per CU, 0.4915 -> 0.4648 ms,
+// bitwise equal; conv3's forward stays at 4: 0.517 vs 0.526; profiles/r06_ab_wide_conv_waves.txt)
+#ifndef SLK_WIDE_C3D_NWV
+#define SLK_WIDE_C3D_NWV 8
+#endif
+using CfgConv3Dgrad = ConvCfg<256, 128, 16, 128, wide::MODE_DGRAD_PLAIN, SLK_WIDE_FW, SLK_WIDE_C3D_NWV, 1>;
+using CfgConv2Dgrad = ConvCfg<128, 64, 32, 64, wide::MODE_DGRAD_MASK, 4, 4, 1>;  // (8 waves: its 4-KB weight slices do not split)
 
 template <class C>
 static int launch_conv(const uint16_t* in, const uint16_t* wsh, const void* aux, uint16_t* out, uint8_t* out2,
